@@ -1,0 +1,336 @@
+#!/usr/bin/env python3
+"""Golden-vector generator: runs the REFERENCE implementation (read-only import from
+/root/reference) with shims S1-S7 and writes small fixtures to
+tests/golden/.  TEST INFRASTRUCTURE ONLY -- runs in the build container, never on the
+GPU box and never as part of the product.  The reference's source is not copied:
+it is imported at run time; only its outputs (inputs + expected outputs) are stored.
+
+Weights come from oracle/weights.py (regenerated from a formula on both sides).
+
+Usage:  python oracle/gen_golden.py [--only sinkhorn,mhc,blocks,model]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+REF = os.environ.get("HV_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, REF)
+
+from oracle import weights as W  # noqa: E402
+from oracle.cases import (MHC_CASES, MODEL_CASES, SK_CASES, gen_seed,  # noqa: E402
+                          mhc_input, sinkhorn_raw)
+
+_TINY = {"on": False}
+
+
+def apply_shims():
+    """Monkey-patch the reference classes with S1-S7 and the tiny-config knobs."""
+    import src.models.manifold_layers as ml
+    import src.models.vision_backbone as vb
+    import src.models.vit_encoder_decoder as ve
+    import src.models.yolo_head as yh
+    import src.models.hybrid_vision as hv
+
+    # S1: 2-D Sinkhorn input goes through the 3-D path (m = matrix.shape[-1]).
+    sk_fwd = ml.SinkhornKnoppProjection.forward
+
+    def sk_forward(self, matrix, return_history=False):
+        if matrix.dim() == 2:
+            r = sk_fwd(self, matrix.unsqueeze(0), return_history)
+            if return_history:
+                return r[0].squeeze(0), r[1]
+            return r.squeeze(0)
+        return sk_fwd(self, matrix, return_history)
+    ml.SinkhornKnoppProjection.forward = sk_forward
+
+    # S2: a 4-D NCHW map handed to mHC is processed channels-last.
+    mhc_fwd = ml.ManifoldHyperConnection.forward
+
+    def mhc_forward(self, x):
+        if x.dim() == 4:
+            return mhc_fwd(self, x.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        return mhc_fwd(self, x)
+    ml.ManifoldHyperConnection.forward = mhc_forward
+
+    # tiny config knobs
+    mhc_init = ml.ManifoldHyperConnection.__init__
+
+    def mhc_init_w(self, *a, **k):
+        if _TINY["on"]:
+            k["sk_iterations"] = 5
+        mhc_init(self, *a, **k)
+    ml.ManifoldHyperConnection.__init__ = mhc_init_w
+    bb_init = vb.HybridVisionBackbone.__init__
+
+    def bb_init_w(self, *a, **k):
+        if _TINY["on"]:
+            k["num_blocks"] = [1, 1, 1, 1]
+        bb_init(self, *a, **k)
+    vb.HybridVisionBackbone.__init__ = bb_init_w
+    hv.HybridVisionBackbone = vb.HybridVisionBackbone
+    he_init = ve.HybridVisionEncoder.__init__
+
+    def he_init_w(self, *a, **k):
+        if _TINY["on"]:
+            k["vit_depth"] = 1
+        he_init(self, *a, **k)
+    ve.HybridVisionEncoder.__init__ = he_init_w
+
+    # S3: interpolate the 256 learned patch positions to H*W, keeping the CLS slot.
+    def pe_forward(self, x):
+        B = x.shape[0]
+        x = self.projection(x).flatten(2).transpose(1, 2)
+        x = self.mhc_enhance(x)
+        x = torch.cat([self.cls_token.expand(B, -1, -1), x], dim=1)
+        pe = self.position_embeddings
+        if pe.shape[1] != x.shape[1]:
+            body = F.interpolate(pe[:, 1:].transpose(1, 2), size=(x.shape[1] - 1,),
+                                 mode="linear").transpose(1, 2)
+            pe = torch.cat([pe[:, :1], body], dim=1)
+        return self.norm(x + pe)
+    ve.PatchEmbedding.forward = pe_forward
+
+    # S4: per-scale anchors [S, A, 1, 1, 4] (only w, h are used by the decoder).
+    def gen_anchors(self):
+        rows = []
+        for sizes in self.anchor_sizes:
+            rows.append(torch.tensor([[0.5, 0.5, w / 416.0, h / 416.0] for (w, h) in sizes]
+                                     ).view(len(sizes), 1, 1, 4))
+        return torch.stack(rows)
+    yh.YOLOAnchorGenerator._generate_anchors = gen_anchors
+
+    # S5: grid view (1,1,H,W,1) -> boxes [B, A, H, W, 4].
+    def dec_forward(self, predictions, anchors, grid_size):
+        B, A, H, W_, _ = predictions.shape
+        xy = torch.sigmoid(predictions[..., 0:2])
+        wh = predictions[..., 2:4]
+        obj = torch.sigmoid(predictions[..., 4:5])
+        cls = torch.sigmoid(predictions[..., 5:])
+        gy, gx = torch.meshgrid(torch.arange(H), torch.arange(W_), indexing="ij")
+        gx = gx.view(1, 1, H, W_, 1)
+        gy = gy.view(1, 1, H, W_, 1)
+        bx = (gx + xy[..., 0:1]) / W_
+        by = (gy + xy[..., 1:2]) / H
+        bw = anchors[..., 2:3] * torch.exp(wh[..., 0:1])
+        bh = anchors[..., 3:4] * torch.exp(wh[..., 1:2])
+        boxes = torch.cat([bx - bw / 2, by - bh / 2, bx + bw / 2, by + bh / 2], dim=-1)
+        scores = obj * cls
+        cs, ci = torch.max(scores, dim=-1)
+        return {"boxes": boxes, "scores": scores, "class_scores": cs, "class_indices": ci,
+                "objectness": obj, "raw_predictions": predictions}
+    yh.YOLODecoder.forward = dec_forward
+
+    # S6: the pooled [B, 1792] vector goes through output_projection[2:] only.
+    def final_feats(self, fused):
+        lst = [F.adaptive_avg_pool2d(fused[k], (1, 1)).flatten(1)
+               for k in ("fused_small", "fused_medium", "fused_large") if k in fused]
+        c = self.final_fusion(torch.cat(lst, dim=1))
+        return self.output_projection[2:](c)
+    hv.HybridVisionSystem._extract_final_features = final_feats
+
+    # S7: get_stability_metrics must skip the root module.
+    def stab(self):
+        out = {}
+        for name, m in self.named_modules():
+            if m is self or not hasattr(m, "get_stability_metrics"):
+                continue
+            for k, v in m.get_stability_metrics().items():
+                out[f"{name}.{k}"] = v
+        return out
+    hv.HybridVisionSystem.get_stability_metrics = stab
+    return ml, vb, ve, yh, hv
+
+
+def save(name, **arrs):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **{k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v))
+                                 for k, v in arrs.items()})
+    print(f"  wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def gen_sinkhorn(ml):
+    print("G1 sinkhorn")
+    for fam in ("wc", "init"):
+        for D, it in SK_CASES:
+            raw = sinkhorn_raw(D, it, fam).requires_grad_(True)
+            sk = ml.SinkhornKnoppProjection(num_iterations=it)
+            M = sk(raw)
+            gG = gen_seed(D, it, 3)
+            G = torch.randn(D, D, generator=gG)
+            (M * G).sum().backward()
+            rec = {"D": D, "iters": it, "history": sk.convergence_history.clone(),
+                   "row_sums": M.sum(1), "col_sums": M.sum(0)}
+            idx = torch.tensor([0, 1, D // 2, D - 1])
+            rec["rows"] = M[idx]
+            rec["cols"] = M[:, idx].T
+            rec["grad_rows"] = raw.grad[idx]
+            if D <= 256:
+                rec["M"] = M
+                rec["grad"] = raw.grad
+            save(f"sk_{fam}_D{D}_it{it}", **rec)
+    # the reference test's own cases (test_models.py:33-100): batched 3-D inputs
+    g = torch.Generator().manual_seed(7)
+    mat = torch.randn(4, 8, 8, generator=g)
+    sk = ml.SinkhornKnoppProjection(num_iterations=20)
+    save("sk_batched_4x8x8", raw=mat, M=sk(mat), history=sk.convergence_history.clone())
+    mat = torch.randn(2, 5, 7, generator=g)
+    sk = ml.SinkhornKnoppProjection(num_iterations=10)
+    save("sk_batched_2x5x7", raw=mat, M=sk(mat), history=sk.convergence_history.clone())
+
+
+# ------------------------------------------------------------------ G2 mHC
+
+
+def gen_mhc(ml):
+    print("G2 mhc")
+    for fam in ("wc", "init"):
+        for D, e in MHC_CASES:
+            torch.manual_seed(0)
+            m = ml.ManifoldHyperConnection(D, expansion_rate=e).eval()
+            W.load_formula_weights(m, fam)
+            x = mhc_input(D, e).requires_grad_(True)
+            y = m(x)
+            G = torch.randn(64, D, generator=gen_seed(D, e, 12))
+            (y * G).sum().backward()
+            with torch.no_grad():
+                m64 = ml.ManifoldHyperConnection(D, expansion_rate=e).double().eval()
+                W.load_formula_weights(m64, fam)
+                y64 = m64(x.detach().double())
+            ghres = m.H_res_raw.grad if D <= 256 else m.H_res_raw.grad[:4]
+            save(f"mhc_{fam}_D{D}_e{e}", x=x, y=y, y64=y64.float(), gx=x.grad,
+                 g_hres=ghres, g_hpre_sum=m.H_pre_raw.grad.abs().sum(),
+                 g_w1_sum=m.mlp[0].weight.grad.abs().sum())
+
+
+# ------------------------------------------------------------------ G3 blocks
+def gen_blocks(ml, vb, ve, yh):
+    print("G3 blocks")
+    fam = "wc"
+    # ConvMHCLayer stem.0 config (3->32, s2) and 64->64 (residual path)
+    for (cin, cout, k, s, HW) in [(3, 32, 3, 2, 32), (64, 64, 3, 1, 16), (64, 128, 3, 2, 16)]:
+        torch.manual_seed(0)
+        m = vb.ConvMHCLayer(cin, cout, kernel_size=k, stride=s).eval()
+        W.load_formula_weights(m, fam)
+        x = torch.randn(2, cin, HW, HW, generator=gen_seed(cin, cout, HW))
+        with torch.no_grad():
+            save(f"convmhc_{cin}_{cout}_s{s}", x=x, y=m(x))
+    torch.manual_seed(0)
+    m = vb.ResidualMHCLayer(128, num_blocks=2, expansion_rate=4, bottleneck=True).eval()
+    W.load_formula_weights(m, fam)
+    x = torch.randn(2, 128, 8, 8, generator=gen_seed(128, 8))
+    with torch.no_grad():
+        save("residual_128", x=x, y=m(x))
+    torch.manual_seed(0)
+    m = ve.TransformerEncoderBlock(embed_dim=256, num_heads=8).eval()
+    W.load_formula_weights(m, fam)
+    x = torch.randn(2, 50, 256, generator=gen_seed(256, 50))
+    with torch.no_grad():
+        save("encblock_256_n50", x=x, y=m(x))
+    # decoder on random logits
+    dec = yh.YOLODecoder()
+    ag = yh.YOLOAnchorGenerator()
+    p = torch.randn(2, 3, 7, 9, 85, generator=gen_seed(85, 7)) * 2
+    out = dec(p, ag(1), (13, 13))
+    save("decode_s1", pred=p, boxes=out["boxes"], scores=out["scores"],
+         class_scores=out["class_scores"], class_indices=out["class_indices"].to(torch.int16))
+
+
+# ------------------------------------------------------------------ G4 full model
+def top2_margin(scores: torch.Tensor) -> torch.Tensor:
+    t = torch.topk(scores, 2, dim=-1).values
+    return t[..., 0] - t[..., 1]
+
+
+def gen_model(hv, only=None):
+    print("G4 model")
+    for tag, tiny, fam, S, B, sub in MODEL_CASES:
+        if only and tag not in only:
+            continue
+        t0 = time.time()
+        _TINY["on"] = tiny
+        torch.manual_seed(0)
+        model = hv.HybridVisionSystem({"image_size": S}).eval()
+        _TINY["on"] = False
+        W.load_formula_weights(model, fam)
+        x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+        with torch.no_grad():
+            out = model(x, task="detection")
+            model64 = model.double()
+            out64 = model64(x.double(), task="detection")
+        rec = {"x_seed": 1, "B": B, "S": S, "tiny": int(tiny), "threads": torch.get_num_threads(),
+               "sub": sub}
+        for s in range(3):
+            k = f"scale_{s}"
+            pr = out["predictions"][k]
+            pr64 = out64["predictions"][k]
+            d = out["decoded"][k]
+            d64 = out64["decoded"][k]
+            step = sub if s == 0 else 1
+            rec[f"pred{s}"] = pr[:, :, ::step]
+            rec[f"pred{s}_f64"] = pr64[:, :, ::step].float()
+            rec[f"cls{s}"] = d["class_indices"].to(torch.uint8)
+            rec[f"cls{s}_f64"] = d64["class_indices"].to(torch.uint8)
+            rec[f"margin{s}"] = top2_margin(d64["scores"]).float()
+            rec[f"clsscore{s}"] = d["class_scores"]
+            rec[f"boxes{s}"] = d["boxes"][:, :, ::step]
+        rec["final_features"] = out["final_features"]
+        rec["final_features_f64"] = out64["final_features"].float()
+        rec["vit_features_pool"] = out["vit_features"].mean(dim=(2, 3))
+        rec["fused_small_pool"] = out["fused_features"]["fused_small"].mean(dim=(2, 3))
+        save(f"model_{tag}", **rec)
+        print(f"  {tag}: {time.time() - t0:.1f}s")
+        del model, model64
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout")
+    ap.add_argument("--models", default="")
+    a = ap.parse_args()
+    torch.set_num_threads(8)
+    ml, vb, ve, yh, hv = apply_shims()
+    parts = a.only.split(",")
+    if "sinkhorn" in parts:
+        gen_sinkhorn(ml)
+    if "mhc" in parts:
+        gen_mhc(ml)
+    if "blocks" in parts:
+        gen_blocks(ml, vb, ve, yh)
+    if "model" in parts:
+        gen_model(hv, [m for m in a.models.split(",") if m])
+    if "layout" in parts:
+        gen_layout(hv)
+
+
+
+def gen_layout(hv):
+    """Record the reference state_dict layout (names, shapes, dtypes) for tiny and base."""
+    import json
+    for tag, tiny in (("tiny", True), ("base", False)):
+        _TINY["on"] = tiny
+        torch.manual_seed(0)
+        model = hv.HybridVisionSystem({})
+        _TINY["on"] = False
+        lay = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in model.state_dict().items()]
+        path = os.path.join(OUT, f"state_dict_{tag}.json")
+        with open(path, "w") as f:
+            json.dump(lay, f)
+        anchors = model.detection_head.anchor_generator.anchors
+        np.save(os.path.join(OUT, "anchors.npy"), anchors.numpy())
+        print(f"  wrote {path} ({len(lay)} entries)")
+
+
+if __name__ == "__main__":
+    main()

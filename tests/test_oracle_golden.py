@@ -1,0 +1,173 @@
+"""Pin the CPU oracle (oracle/hv_oracle.py) against the reference's own outputs
+(tests/golden, produced by oracle/gen_golden.py from the reference with shims S1-S7).
+
+CPU only.  These tests are what makes the oracle trustworthy as the GPU parity checker.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import cases, hv_oracle as O, weights as W
+
+
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,it", cases.SK_CASES)
+def test_sinkhorn_oracle_matches_reference(fam, D, it):
+    g = golden(f"sk_{fam}_D{D}_it{it}")
+    raw = cases.sinkhorn_raw(D, it, fam)
+    hist = torch.zeros(it)
+    M = O.sinkhorn(raw, it, history=hist)
+    idx = [0, 1, D // 2, D - 1]
+    np.testing.assert_allclose(M[idx].numpy(), g["rows"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(M.sum(0).numpy(), g["col_sums"], rtol=1e-5)
+    np.testing.assert_allclose(hist.numpy(), g["history"], rtol=1e-4, atol=1e-7)
+    if "M" in g.files:
+        np.testing.assert_allclose(M.numpy(), g["M"], rtol=1e-5, atol=1e-8)
+
+
+def test_sinkhorn_oracle_batched_reference_cases():
+    for name, it in (("sk_batched_4x8x8", 20), ("sk_batched_2x5x7", 10)):
+        g = golden(name)
+        hist = torch.zeros(it)
+        M = O.sinkhorn(torch.from_numpy(g["raw"]), it, history=hist)
+        np.testing.assert_allclose(M.numpy(), g["M"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(hist.numpy(), g["history"], rtol=1e-4, atol=1e-7)
+
+
+def _mhc_sd(D, e, fam):
+    shapes = {
+        "H_pre_raw": (D, D * e), "H_post_raw": (D * e, D), "H_res_raw": (D, D),
+        "mlp.0.weight": (2 * D * e, D * e), "mlp.0.bias": (2 * D * e,),
+        "mlp.3.weight": (D * e, 2 * D * e), "mlp.3.bias": (D * e,),
+        "norm_pre.weight": (D,), "norm_pre.bias": (D,),
+        "norm_post.weight": (D,), "norm_post.bias": (D,),
+    }
+    return {k: W.make_tensor(k, s, fam) for k, s in shapes.items()}
+
+
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e", cases.MHC_CASES)
+def test_mhc_oracle_matches_reference(fam, D, e):
+    g = golden(f"mhc_{fam}_D{D}_e{e}")
+    sd = _mhc_sd(D, e, fam)
+    y = O.mhc(sd, "", cases.mhc_input(D, e), 20)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=2e-4)
+    # against the float64 reference run as well
+    sd64 = O.cast_state_dict(sd, torch.float64)
+    y64 = O.mhc(sd64, "", cases.mhc_input(D, e).double(), 20)
+    np.testing.assert_allclose(y64.float().numpy(), g["y64"], rtol=0, atol=2e-5)
+
+
+def _module_sd(names_shapes, fam):
+    return {n: W.make_tensor(n, s, fam) for n, s in names_shapes}
+
+
+def test_convmhc_blocks_match_reference():
+    for (cin, cout, k, s, HW) in [(3, 32, 3, 2, 32), (64, 64, 3, 1, 16), (64, 128, 3, 2, 16)]:
+        g = golden(f"convmhc_{cin}_{cout}_s{s}")
+        shapes = _convmhc_shapes("", cin, cout, k)
+        sd = _module_sd(shapes, "wc")
+        y = O.conv_mhc_layer(sd, "", torch.from_numpy(g["x"]), cin, cout, k, s, 20)
+        np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=5e-4)
+
+
+def _mhc_shapes(p, D, e):
+    return [(p + k, s) for k, s in [
+        ("H_pre_raw", (D, D * e)), ("H_post_raw", (D * e, D)), ("H_res_raw", (D, D)),
+        ("mlp.0.weight", (2 * D * e, D * e)), ("mlp.0.bias", (2 * D * e,)),
+        ("mlp.3.weight", (D * e, 2 * D * e)), ("mlp.3.bias", (D * e,)),
+        ("norm_pre.weight", (D,)), ("norm_pre.bias", (D,)),
+        ("norm_post.weight", (D,)), ("norm_post.bias", (D,))]]
+
+
+def _convmhc_shapes(p, cin, cout, k):
+    sh = [(p + "conv.weight", (cout, cin, k, k)), (p + "bn.weight", (cout,)),
+          (p + "bn.bias", (cout,)), (p + "bn.running_mean", (cout,)), (p + "bn.running_var", (cout,))]
+    sh += _mhc_shapes(p + "mhc.", cout, 4)
+    if cout >= 32:
+        sh += [(p + "channel_attention.1.weight", (cout // 4, cout, 1, 1)),
+               (p + "channel_attention.1.bias", (cout // 4,)),
+               (p + "channel_attention.3.weight", (cout, cout // 4, 1, 1)),
+               (p + "channel_attention.3.bias", (cout,))]
+    return sh
+
+
+def test_residual_block_matches_reference():
+    g = golden("residual_128")
+    c = 128
+    sh = (_convmhc_shapes("blocks.0.", c, c // 2, 1) + _convmhc_shapes("blocks.1.", c // 2, c, 3)
+          + _convmhc_shapes("projection.", c, c, 1))
+    sd = _module_sd(sh, "wc")
+    y = O.residual_mhc_layer(sd, "", torch.from_numpy(g["x"]), c, 20)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=5e-4)
+
+
+def test_encoder_block_matches_reference():
+    g = golden("encblock_256_n50")
+    D = 256
+    sh = []
+    for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+        sh += _mhc_shapes(f"attention.{n}.", D, 2)
+    sh += _mhc_shapes("residual_mhc1.", D, 2) + _mhc_shapes("residual_mhc2.", D, 2)
+    sh += [("norm1.scale", (D,)), ("norm2.scale", (D,)), ("mlp.0.weight", (4 * D, D)),
+           ("mlp.0.bias", (4 * D,)), ("mlp.3.weight", (D, 4 * D)), ("mlp.3.bias", (D,))]
+    sd = _module_sd(sh, "wc")
+    y = O.encoder_block(sd, "", torch.from_numpy(g["x"]), 20)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=5e-4)
+
+
+def test_decode_matches_reference():
+    g = golden("decode_s1")
+    out = O.decode(torch.from_numpy(g["pred"]), O.anchor_wh(1))
+    np.testing.assert_allclose(out["boxes"].numpy(), g["boxes"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(out["scores"].numpy(), g["scores"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(out["class_indices"].numpy(), g["class_indices"])
+
+
+def formula_state_dict(tag: str, fam: str):
+    """Reference-layout state dict filled from the weight formula (no reference import)."""
+    import json
+    import os
+    from conftest import GOLDEN
+    lay = json.load(open(os.path.join(GOLDEN, f"state_dict_{tag}.json")))
+    sd = {}
+    for name, shape, dt in lay:
+        t = W.make_tensor(name, tuple(shape), fam)
+        if t is None:
+            if name.endswith("anchors"):
+                t = torch.from_numpy(np.load(os.path.join(GOLDEN, "anchors.npy")))
+            else:
+                t = torch.zeros(shape, dtype=getattr(torch, dt))
+        sd[name] = t
+    return sd
+
+
+@pytest.mark.parametrize("tag,tiny,fam,S,B,sub", cases.MODEL_CASES[:3])
+def test_model_oracle_matches_reference(tag, tiny, fam, S, B, sub):
+    _check_model(tag, tiny, fam, S, B, sub)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("tag,tiny,fam,S,B,sub", cases.MODEL_CASES[3:])
+def test_model_oracle_matches_reference_large(tag, tiny, fam, S, B, sub):
+    _check_model(tag, tiny, fam, S, B, sub)
+
+
+def _check_model(tag, tiny, fam, S, B, sub):
+    g = golden(f"model_{tag}")
+    sd = formula_state_dict("tiny" if tiny else "base", fam)
+    cfg = O.TINY if tiny else O.BASE
+    with torch.no_grad():
+        out = O.system_forward(sd, cases.model_input(B, S), cfg)
+    for s in range(3):
+        step = sub if s == 0 else 1
+        pr = out["predictions"][f"scale_{s}"][:, :, ::step].numpy()
+        # the oracle vs the reference, both fp32 on CPU: bounded by the reference's own
+        # fp32-vs-fp64 error (up to 6.9e-4 from thread count alone)
+        np.testing.assert_allclose(pr, g[f"pred{s}"], rtol=0, atol=2e-3)
+        np.testing.assert_allclose(pr, g[f"pred{s}_f64"], rtol=0, atol=2e-3)
+        ci = out["decoded"][f"scale_{s}"]["class_indices"].numpy()
+        sure = g[f"margin{s}"] >= 1e-4
+        assert (ci[sure] == g[f"cls{s}_f64"][sure]).all()
+    np.testing.assert_allclose(out["final_features"].numpy(), g["final_features_f64"], rtol=0, atol=1e-4)
