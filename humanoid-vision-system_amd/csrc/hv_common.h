@@ -1,0 +1,80 @@
+// Shared device helpers for the HybridVision gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/hv_kernels.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+#define HV_WAVE 64
+
+__device__ __forceinline__ float bf2f(unsigned short v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// Round-to-nearest-even through the hardware convert (v_cvt_pk_bf16_f32 on gfx950).
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+// Storage-type adaptors: activations are either fp32 or bf16 (raw ushort bits).
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float load(const float* p, size_t i) { return p[i]; }
+  static __device__ __forceinline__ void store(float* p, size_t i, float v) { p[i] = v; }
+};
+template <> struct Elem<unsigned short> {
+  static __device__ __forceinline__ float load(const unsigned short* p, size_t i) { return bf2f(p[i]); }
+  static __device__ __forceinline__ void store(unsigned short* p, size_t i, float v) { p[i] = f2bf(v); }
+};
+
+__device__ __forceinline__ float hv_gelu(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float hv_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float hv_silu(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float hv_act(float v, int act) {
+  switch (act) {
+    case HV_ACT_RELU: return v > 0.f ? v : 0.f;
+    case HV_ACT_SILU: return hv_silu(v);
+    case HV_ACT_GELU: return hv_gelu(v);
+    case HV_ACT_LEAKY: return v > 0.f ? v : 0.1f * v;
+    case HV_ACT_SIGMOID: return hv_sigmoid(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `scratch` needs 16 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+#define HV_CHECK_LAUNCH() \
+  do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+static inline unsigned hv_cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

@@ -1,0 +1,646 @@
+// Normalisation, layout, pointwise, attention and decode kernels of the HybridVision path
+// (gfx950).  All activations are token-major (NHWC / [tokens, channels]); T is the storage
+// type (float or bf16 bits), arithmetic is fp32.
+#include "hv_common.h"
+
+namespace {
+
+using bf = unsigned short;
+
+#define HV_DISPATCH(dt, KERNEL_CALL)                 \
+  do {                                               \
+    if ((dt) == HV_BF16) { using T = bf; KERNEL_CALL; } \
+    else if ((dt) == HV_F32) { using T = float; KERNEL_CALL; } \
+    else return HV_EINVAL;                           \
+  } while (0)
+
+// ---------------------------------------------------------------- row statistics / norms
+// One wave per row; two-pass mean / variance from the row held in L1.
+template <typename T>
+__global__ void __launch_bounds__(256) k_row_stats(const T* __restrict__ x, long ldx, int rows,
+                                                   int cols, float eps, float* mean, float* rstd) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const T* p = x + (long)r * ldx;
+  float s = 0.f;
+  for (int j = lane; j < cols; j += 64) s += Elem<T>::load(p, j);
+  const float mu = wave_sum(s) / cols;
+  float v = 0.f;
+  for (int j = lane; j < cols; j += 64) { const float d = Elem<T>::load(p, j) - mu; v += d * d; }
+  v = wave_sum(v) / cols;
+  if (lane == 0) { mean[r] = mu; rstd[r] = rsqrtf(v + eps); }
+}
+
+template <typename TX, typename TY>
+__global__ void __launch_bounds__(256) k_layernorm(const TX* __restrict__ x, int rows, int cols,
+                                                   float eps, const float* gamma, const float* beta,
+                                                   TY* y, const void* res, int res_dt) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const TX* p = x + (long)r * cols;
+  float s = 0.f;
+  for (int j = lane; j < cols; j += 64) s += Elem<TX>::load(p, j);
+  const float mu = wave_sum(s) / cols;
+  float v = 0.f;
+  for (int j = lane; j < cols; j += 64) { const float d = Elem<TX>::load(p, j) - mu; v += d * d; }
+  const float rs = rsqrtf(wave_sum(v) / cols + eps);
+  TY* q = y + (long)r * cols;
+  for (int j = lane; j < cols; j += 64) {
+    float o = (Elem<TX>::load(p, j) - mu) * rs;
+    if (gamma) o = o * gamma[j] + beta[j];
+    if (res) o += res_dt == HV_BF16 ? bf2f(((const bf*)res)[(long)r * cols + j])
+                                    : ((const float*)res)[(long)r * cols + j];
+    Elem<TY>::store(q, j, o);
+  }
+}
+
+// RMSNorm (manifold_layers.py:449-456): x / sqrt(mean(x^2) + eps) * scale
+template <typename T>
+__global__ void __launch_bounds__(256) k_rmsnorm(const T* __restrict__ x, int rows, int cols,
+                                                 float eps, const float* scale, T* y) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const T* p = x + (long)r * cols;
+  float s = 0.f;
+  for (int j = lane; j < cols; j += 64) { const float a = Elem<T>::load(p, j); s += a * a; }
+  const float rms = sqrtf(wave_sum(s) / cols + eps);
+  for (int j = lane; j < cols; j += 64)
+    Elem<T>::store(y + (long)r * cols, j, Elem<T>::load(p, j) / rms * scale[j]);
+}
+
+// ---------------------------------------------------------------- mHC coefficient prep
+// gc[i,k] = g_i s(raw[i,k]) - mean_i(g_i s(raw[i,k])) ; u[k] = sum_i b_i s(raw[i,k])
+__global__ void __launch_bounds__(256) k_prep_pre(int D, int Hd, const float* __restrict__ raw,
+                                                  const float* gamma, const float* beta, float* gc,
+                                                  int gct, float* u) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= Hd) return;
+  float sg = 0.f, sb = 0.f;
+  for (int i = 0; i < D; ++i) {
+    const float s = 1.0f / (1.0f + expf(-raw[(long)i * Hd + k]));
+    sg += gamma[i] * s;
+    sb += beta[i] * s;
+  }
+  const float mean = sg / D;
+  u[k] = sb;
+  for (int i = 0; i < D; ++i) {
+    const float s = 1.0f / (1.0f + expf(-raw[(long)i * Hd + k]));
+    gc[gct ? (long)k * D + i : (long)i * Hd + k] = gamma[i] * s - mean;
+  }
+}
+
+// row means of H_res (rows 0..D-1) and H_post = 2 s(raw) (rows D..D+Hd-1); one wave per row
+__global__ void __launch_bounds__(256) k_prep_rowmean(int D, int Hd, const float* hres,
+                                                      const float* hpost_raw, float* rm) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= D + Hd) return;
+  float s = 0.f;
+  if (r < D) {
+    for (int j = lane; j < D; j += 64) s += hres[(long)r * D + j];
+  } else {
+    const float* p = hpost_raw + (long)(r - D) * D;
+    for (int j = lane; j < D; j += 64) s += 2.0f / (1.0f + expf(-p[j]));
+  }
+  s = wave_sum(s);
+  if (lane == 0) rm[r] = s / D;
+}
+
+// wct[j][i] = src[i][j] - rm[i], src = [H_res ; 2 s(H_post_raw)] ([D+Hd, D]); 32x32 LDS tiles
+__global__ void __launch_bounds__(256) k_prep_wct(int D, int Hd, const float* hres,
+                                                  const float* hpost_raw, const float* rm,
+                                                  float* wct) {
+  __shared__ float tile[32][33];
+  const int Kc = D + Hd;
+  const int i0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int i = i0 + r, j = j0 + tx;
+    float v = 0.f;
+    if (i < Kc && j < D) {
+      v = i < D ? hres[(long)i * D + j]
+                : 2.0f / (1.0f + expf(-hpost_raw[(long)(i - D) * D + j]));
+      v -= rm[i];
+    }
+    tile[r][tx] = v;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int j = j0 + r, i = i0 + tx;
+    if (j < D && i < Kc) wct[(long)j * Kc + i] = tile[tx][r];
+  }
+}
+
+// ---------------------------------------------------------------- casts / layout
+template <typename T>
+__global__ void k_cast(const float* __restrict__ x, long n, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) Elem<T>::store(y, i, x[i]);
+}
+
+template <typename T>
+__global__ void k_nchw_to_nhwc(const float* __restrict__ x, int n, int c, int h, int w, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)n * c * h * w;
+  if (i >= total) return;
+  const int ci = i % c;
+  const long p = i / c;                 // n*h*w index
+  const int b = p / ((long)h * w);
+  const long hw = p % ((long)h * w);
+  Elem<T>::store(y, i, x[((long)b * c + ci) * h * w + hw]);
+}
+
+template <typename T>
+__global__ void k_maxpool2x2(const T* __restrict__ x, int n, int h, int w, int c, T* y) {
+  const int oh = h / 2, ow = w / 2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)n * oh * ow * c;
+  if (i >= total) return;
+  const int ci = i % c;
+  long p = i / c;
+  const int ox = p % ow; p /= ow;
+  const int oy = p % oh;
+  const int b = p / oh;
+  const T* base = x + (((long)b * h + 2 * oy) * w + 2 * ox) * c + ci;
+  const float v = fmaxf(fmaxf(Elem<T>::load(base, 0), Elem<T>::load(base, c)),
+                        fmaxf(Elem<T>::load(base, (long)w * c), Elem<T>::load(base, (long)w * c + c)));
+  Elem<T>::store(y, i, v);
+}
+
+// channel sums over pixel chunks: part[n, chunk, c]; block = (64 channels) x 4 pixel lanes
+constexpr int CM_CHUNK = 1024;
+template <typename T>
+__global__ void __launch_bounds__(256) k_chan_partial(const T* __restrict__ x, int hw, int c,
+                                                      int nchunk, float* part) {
+  __shared__ float red[4][64];
+  const int cg = blockIdx.x, chunk = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = cg * 64 + lane;
+  float s = 0.f;
+  if (ch < c) {
+    const int p0 = chunk * CM_CHUNK, p1 = min(hw, p0 + CM_CHUNK);
+    const T* base = x + (long)b * hw * c + ch;
+    for (int p = p0 + wv; p < p1; p += 4) s += Elem<T>::load(base, (long)p * c);
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && ch < c)
+    part[((long)b * nchunk + chunk) * c + ch] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ void k_chan_final(const float* part, int n, int nchunk, int c, float inv, float* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * c) return;
+  const int b = i / c, ch = i % c;
+  float s = 0.f;
+  for (int k = 0; k < nchunk; ++k) s += part[((long)b * nchunk + k) * c + ch];
+  out[i] = s * inv;
+}
+
+// SE gate MLP (vision_backbone.py:77-83): one block per image.
+__global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int cr, const float* w1,
+                                                const float* b1, const float* w2, const float* b2,
+                                                float* gate) {
+  extern __shared__ float sh[];
+  float* p = sh;           // [c]
+  float* h = sh + c;       // [cr]
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < c; i += blockDim.x) p[i] = pooled[(long)b * c + i];
+  __syncthreads();
+  for (int o = threadIdx.x; o < cr; o += blockDim.x) {
+    float s = b1[o];
+    for (int i = 0; i < c; ++i) s += w1[(long)o * c + i] * p[i];
+    h[o] = hv_silu(s);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < c; o += blockDim.x) {
+    float s = b2[o];
+    for (int i = 0; i < cr; ++i) s += w2[(long)o * cr + i] * h[i];
+    gate[(long)b * c + o] = 1.0f / (1.0f + expf(-s));
+  }
+}
+
+template <typename T>
+__global__ void k_scale_residual(const T* __restrict__ x, const float* gate, const T* identity,
+                                 int hw, int c, long total, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int ch = i % c;
+  const long b = i / ((long)hw * c);
+  float v = Elem<T>::load(x, i) * gate[b * c + ch];
+  if (identity) v += Elem<T>::load(identity, i);
+  Elem<T>::store(y, i, v);
+}
+
+template <typename T>
+__global__ void k_upsample_add(const T* __restrict__ a, const T* __restrict__ bsrc, int n, int h,
+                               int w, int c, int hb, int wb, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)n * h * w * c;
+  if (i >= total) return;
+  const int ch = i % c;
+  long p = i / c;
+  const int x = p % w; p /= w;
+  const int yy = p % h;
+  const int b = p / h;
+  // nearest: src = floor(dst * in / out) (F.interpolate mode='nearest')
+  const int sy = min((int)((float)yy * ((float)hb / (float)h)), hb - 1);
+  const int sx = min((int)((float)x * ((float)wb / (float)w)), wb - 1);
+  const float v = Elem<T>::load(a, i) + Elem<T>::load(bsrc, (((long)b * hb + sy) * wb + sx) * c + ch);
+  Elem<T>::store(y, i, v);
+}
+
+template <typename T>
+__global__ void k_add_scaled(const T* a, const T* b, long n, float alpha, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) Elem<T>::store(y, i, (Elem<T>::load(a, i) + Elem<T>::load(b, i)) * alpha);
+}
+
+template <typename T>
+__global__ void k_add_rowvec(const T* x, const float* v, int p, int c, long total, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int ch = i % c;
+  const long b = i / ((long)p * c);
+  Elem<T>::store(y, i, Elem<T>::load(x, i) + v[b * c + ch]);
+}
+
+// F.interpolate(mode='linear', align_corners=False) of [L, D] -> [Lout, D]
+__global__ void k_interp_linear(const float* src, int L, int D, int Lout, float* dst) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Lout * D) return;
+  const int o = i / D, d = i % D;
+  const float scale = (float)L / (float)Lout;
+  float s = scale * ((float)o + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  const int x0 = (int)s;
+  const int x1 = x0 + (x0 < L - 1 ? 1 : 0);
+  const float l1 = s - (float)x0, l0 = 1.0f - l1;
+  dst[i] = l0 * src[(long)x0 * D + d] + l1 * src[(long)x1 * D + d];
+}
+
+// ---------------------------------------------------------------- transformer pieces
+template <typename T>
+__global__ void __launch_bounds__(256) k_vit_tokens(const T* x, const float* cls, const float* pos,
+                                                    const float* scale, int n, int tokens, int d, T* y) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int L = tokens + 1;
+  if (r >= n * L) return;
+  const int b = r / L, t = r % L;
+  float s = 0.f;
+  for (int j = lane; j < d; j += 64) {
+    const float v = (t == 0 ? cls[j] : Elem<T>::load(x, ((long)b * tokens + t - 1) * d + j)) +
+                    pos[(long)t * d + j];
+    s += v * v;
+  }
+  const float rms = sqrtf(wave_sum(s) / d + 1e-8f);
+  for (int j = lane; j < d; j += 64) {
+    const float v = (t == 0 ? cls[j] : Elem<T>::load(x, ((long)b * tokens + t - 1) * d + j)) +
+                    pos[(long)t * d + j];
+    Elem<T>::store(y, (long)r * d + j, v / rms * scale[j]);
+  }
+}
+
+// softmax(q k^T * scale) v: one thread per query, key/value tiles staged in LDS with an
+// online softmax; q/k/v/out are [n, L, heads*HD].
+template <typename T, int HD>
+__global__ void __launch_bounds__(128) k_attention(const T* q, const T* k, const T* v, T* out,
+                                                   int L, int heads, float sm_scale) {
+  constexpr int KT = 128;
+  __shared__ float ks[KT][HD], vs[KT][HD];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qi = blockIdx.x * 128 + threadIdx.x;
+  const int D = heads * HD;
+  const long base = (long)b * L * D + h * HD;
+  float qv[HD], o[HD];
+  const bool active = qi < L;
+#pragma unroll
+  for (int j = 0; j < HD; ++j) {
+    qv[j] = active ? Elem<T>::load(q, base + (long)qi * D + j) * sm_scale : 0.f;
+    o[j] = 0.f;
+  }
+  float mx = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < L; k0 += KT) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < KT * HD; e += 128) {
+      const int kk = e / HD, j = e % HD;
+      const bool in = k0 + kk < L;
+      ks[kk][j] = in ? Elem<T>::load(k, base + (long)(k0 + kk) * D + j) : 0.f;
+      vs[kk][j] = in ? Elem<T>::load(v, base + (long)(k0 + kk) * D + j) : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(KT, L - k0);
+    for (int kk = 0; kk < kn; ++kk) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < HD; ++j) s += qv[j] * ks[kk][j];
+      if (s > mx) {
+        const float f = expf(mx - s);
+        l *= f;
+#pragma unroll
+        for (int j = 0; j < HD; ++j) o[j] *= f;
+        mx = s;
+      }
+      const float p = expf(s - mx);
+      l += p;
+#pragma unroll
+      for (int j = 0; j < HD; ++j) o[j] += p * vs[kk][j];
+    }
+  }
+  if (active) {
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int j = 0; j < HD; ++j) Elem<T>::store(out, base + (long)qi * D + j, o[j] * inv);
+  }
+}
+
+template <typename T>
+__global__ void k_gather_rows(const T* x, long stride_rows, int n, int c, T* y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * c) return;
+  const int b = i / c, j = i % c;
+  y[i] = x[(long)b * stride_rows * c + j];
+}
+
+// ---------------------------------------------------------------- YOLO decode
+template <typename T>
+__global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logits, int n, int h, int w,
+                                                     int A, int nc, const float* anchor_wh,
+                                                     float* pred, float* boxes, float* scores,
+                                                     float* cscore, int64_t* cidx, float* obj) {
+  const long cell = (long)blockIdx.x * 256 + threadIdx.x;     // (b, a, y, x)
+  const long total = (long)n * A * h * w;
+  if (cell >= total) return;
+  const int x = cell % w;
+  long t = cell / w;
+  const int y = t % h; t /= h;
+  const int a = t % A;
+  const int b = t / A;
+  const int P = 5 + nc;
+  const T* src = logits + (((long)b * h + y) * w + x) * (long)(A * P) + (long)a * P;
+  float* pr = pred + cell * P;
+  for (int k = 0; k < P; ++k) pr[k] = Elem<T>::load(src, k);
+  const float sx = 1.0f / (1.0f + expf(-pr[0])), sy = 1.0f / (1.0f + expf(-pr[1]));
+  const float bx = ((float)x + sx) / (float)w, by = ((float)y + sy) / (float)h;
+  const float bw = anchor_wh[2 * a] * expf(pr[2]), bh = anchor_wh[2 * a + 1] * expf(pr[3]);
+  float* bo = boxes + cell * 4;
+  bo[0] = bx - bw / 2; bo[1] = by - bh / 2; bo[2] = bx + bw / 2; bo[3] = by + bh / 2;
+  const float o = 1.0f / (1.0f + expf(-pr[4]));
+  obj[cell] = o;
+  float best = -1.f;
+  int bi = 0;
+  float* sc = scores + cell * nc;
+  for (int k = 0; k < nc; ++k) {
+    const float s = o * (1.0f / (1.0f + expf(-pr[5 + k])));
+    sc[k] = s;
+    if (s > best) { best = s; bi = k; }
+  }
+  cscore[cell] = best;
+  cidx[cell] = bi;
+}
+
+}  // namespace
+
+// ============================================================== C ABI
+extern "C" int hv_row_stats(int dtype, const void* x, long ldx, int rows, int cols, float eps,
+                            float* mean, float* rstd, hv_stream_t stream) {
+  if (rows <= 0 || cols <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_row_stats<T><<<hv_cdiv(rows, 4), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, ldx, rows, cols, eps, mean, rstd)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_layernorm(int x_dtype, const void* x, int rows, int cols, float eps,
+                            const float* gamma, const float* beta, int y_dtype, void* y,
+                            const void* res_out, int res_dtype, hv_stream_t stream) {
+  if (rows <= 0 || cols <= 0) return HV_EINVAL;
+  const dim3 g(hv_cdiv(rows, 4));
+  hipStream_t s = (hipStream_t)stream;
+  if (x_dtype == HV_F32 && y_dtype == HV_F32)
+    k_layernorm<float, float><<<g, 256, 0, s>>>((const float*)x, rows, cols, eps, gamma, beta, (float*)y, res_out, res_dtype);
+  else if (x_dtype == HV_F32 && y_dtype == HV_BF16)
+    k_layernorm<float, bf><<<g, 256, 0, s>>>((const float*)x, rows, cols, eps, gamma, beta, (bf*)y, res_out, res_dtype);
+  else if (x_dtype == HV_BF16 && y_dtype == HV_BF16)
+    k_layernorm<bf, bf><<<g, 256, 0, s>>>((const bf*)x, rows, cols, eps, gamma, beta, (bf*)y, res_out, res_dtype);
+  else if (x_dtype == HV_BF16 && y_dtype == HV_F32)
+    k_layernorm<bf, float><<<g, 256, 0, s>>>((const bf*)x, rows, cols, eps, gamma, beta, (float*)y, res_out, res_dtype);
+  else
+    return HV_EINVAL;
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_rmsnorm(int dtype, const void* x, int rows, int cols, float eps,
+                          const float* scale, void* y, hv_stream_t stream) {
+  if (rows <= 0 || cols <= 0 || !scale) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_rmsnorm<T><<<hv_cdiv(rows, 4), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, rows, cols, eps, scale, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_mhc_prep(int D, int Hd, const float* h_pre_raw, const float* h_post_raw,
+                           const float* h_res, const float* gamma_pre, const float* beta_pre,
+                           float* gc, int gct, float* u, float* wct, float* rm, hv_stream_t stream) {
+  if (D <= 0 || Hd <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  k_prep_pre<<<hv_cdiv(Hd, 256), 256, 0, s>>>(D, Hd, h_pre_raw, gamma_pre, beta_pre, gc, gct, u);
+  k_prep_rowmean<<<hv_cdiv(D + Hd, 4), 256, 0, s>>>(D, Hd, h_res, h_post_raw, rm);
+  k_prep_wct<<<dim3(hv_cdiv(D + Hd, 32), hv_cdiv(D, 32)), 256, 0, s>>>(D, Hd, h_res, h_post_raw, rm, wct);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_cast(const float* x, long n, int y_dtype, void* y, hv_stream_t stream) {
+  if (n <= 0) return n == 0 ? HV_OK : HV_EINVAL;
+  HV_DISPATCH(y_dtype, (k_cast<T><<<hv_cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(x, n, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int y_dtype, void* y,
+                               hv_stream_t stream) {
+  const long total = (long)n * c * h * w;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(y_dtype, (k_nchw_to_nhwc<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                            x, n, c, h, w, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int c, void* y,
+                             hv_stream_t stream) {
+  const long total = (long)n * (h / 2) * (w / 2) * c;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_maxpool2x2<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, n, h, w, c, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_channel_mean_work_floats(int n, int hw, int c) {
+  return (size_t)n * ((hw + CM_CHUNK - 1) / CM_CHUNK) * c;
+}
+
+extern "C" int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out,
+                               float* work, hv_stream_t stream) {
+  if (n <= 0 || hw <= 0 || c <= 0 || !work) return HV_EINVAL;
+  const int nchunk = (hw + CM_CHUNK - 1) / CM_CHUNK;
+  hipStream_t s = (hipStream_t)stream;
+  HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(hv_cdiv(c, 64), nchunk, n), 256, 0, s>>>(
+                          (const T*)x, hw, c, nchunk, work)));
+  k_chan_final<<<hv_cdiv((long)n * c, 256), 256, 0, s>>>(work, n, nchunk, c, 1.0f / hw, out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
+                         const float* w2, const float* b2, float* gate, hv_stream_t stream) {
+  if (n <= 0 || c <= 0 || cr <= 0) return HV_EINVAL;
+  k_se_mlp<<<n, 256, (c + cr) * sizeof(float), (hipStream_t)stream>>>(pooled, c, cr, w1, b1, w2, b2, gate);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_scale_residual(int dtype, const void* x, const float* gate, const void* identity,
+                                 int n, int hw, int c, void* y, hv_stream_t stream) {
+  const long total = (long)n * hw * c;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_scale_residual<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, gate, (const T*)identity, hw, c, total, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_upsample_add(int dtype, const void* a, const void* b, int n, int h, int w, int c,
+                               int hb, int wb, void* y, hv_stream_t stream) {
+  const long total = (long)n * h * w * c;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_upsample_add<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)a, (const T*)b, n, h, w, c, hb, wb, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_add_scaled(int dtype, const void* a, const void* b, long count, float alpha,
+                             void* y, hv_stream_t stream) {
+  if (count <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_add_scaled<T><<<hv_cdiv(count, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)a, (const T*)b, count, alpha, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_add_rowvec(int dtype, const void* x, const float* v, int n, int p, int c, void* y,
+                             hv_stream_t stream) {
+  const long total = (long)n * p * c;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_add_rowvec<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, v, p, c, total, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_interp_linear(const float* src, int L, int D, int Lout, float* dst,
+                                hv_stream_t stream) {
+  if (L <= 0 || D <= 0 || Lout <= 0) return HV_EINVAL;
+  k_interp_linear<<<hv_cdiv((long)Lout * D, 256), 256, 0, (hipStream_t)stream>>>(src, L, D, Lout, dst);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_vit_tokens(int dtype, const void* x, const float* cls, const float* pos,
+                             const float* scale, int n, int tokens, int d, void* y,
+                             hv_stream_t stream) {
+  if (n <= 0 || tokens <= 0 || d <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_vit_tokens<T><<<hv_cdiv((long)n * (tokens + 1), 4), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, cls, pos, scale, n, tokens, d, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_attention(int dtype, const void* q, const void* k, const void* v, void* out,
+                            int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream) {
+  if (n <= 0 || L <= 0 || heads <= 0) return HV_EINVAL;
+  if (hd != 32) return HV_EUNSUPPORTED;
+  const dim3 g(hv_cdiv(L, 128), heads, n);
+  HV_DISPATCH(dtype, (k_attention<T, 32><<<g, 128, 0, (hipStream_t)stream>>>(
+                          (const T*)q, (const T*)k, (const T*)v, (T*)out, L, heads, sm_scale)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_gather_rows(int dtype, const void* x, long stride_rows, int n, int c, void* y,
+                              hv_stream_t stream) {
+  if (n <= 0 || c <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_gather_rows<T><<<hv_cdiv((long)n * c, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, stride_rows, n, c, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, int nc,
+                              const float* anchor_wh, float* predictions, float* boxes,
+                              float* scores, float* class_scores, int64_t* class_indices,
+                              float* objectness, hv_stream_t stream) {
+  const long total = (long)n * A * h * w;
+  if (total <= 0 || nc <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)logits, n, h, w, A, nc, anchor_wh, predictions, boxes, scores,
+                          class_scores, class_indices, objectness)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+// ---------------------------------------------------------------- parameter preparation
+namespace {
+// w [cout, cin, k, k] fp32 -> y [cout, k, k, cin] (implicit-GEMM B operand), optional row scale
+template <typename T>
+__global__ void k_conv_weight_prep(const float* __restrict__ w, int cout, int cin, int k,
+                                   const float* scale, T* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)cout * cin * k * k;
+  if (i >= total) return;
+  const int ci = i % cin;
+  long t = i / cin;
+  const int kw = t % k; t /= k;
+  const int kh = t % k;
+  const int co = t / k;
+  float v = w[(((long)co * cin + ci) * k + kh) * k + kw];
+  if (scale) v *= scale[co];
+  Elem<T>::store(y, i, v);
+}
+
+// eval BatchNorm (+ conv bias) folded to a per-channel affine:  s = g / sqrt(v + eps),
+// b' = beta + (bias - mean) * s   (vision_backbone.py:113, feature_fusion.py:44, yolo_head.py:122)
+__global__ void k_bn_fold(int c, const float* g, const float* beta, const float* mean,
+                          const float* var, const float* cbias, float eps, float* s_out,
+                          float* b_out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= c) return;
+  const float s = g ? g[i] / sqrtf(var[i] + eps) : 1.0f;
+  const float cb = cbias ? cbias[i] : 0.f;
+  s_out[i] = s;
+  b_out[i] = g ? beta[i] + (cb - mean[i]) * s : cb;
+}
+}  // namespace
+
+extern "C" int hv_conv_weight_prep(const float* w, int cout, int cin, int k, const float* scale,
+                                   int y_dtype, void* y, hv_stream_t stream) {
+  const long total = (long)cout * cin * k * k;
+  if (total <= 0) return HV_EINVAL;
+  HV_DISPATCH(y_dtype, (k_conv_weight_prep<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                            w, cout, cin, k, scale, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_bn_fold(int c, const float* gamma, const float* beta, const float* mean,
+                          const float* var, const float* conv_bias, float eps, float* scale_out,
+                          float* bias_out, hv_stream_t stream) {
+  if (c <= 0) return HV_EINVAL;
+  k_bn_fold<<<hv_cdiv(c, 256), 256, 0, (hipStream_t)stream>>>(c, gamma, beta, mean, var, conv_bias,
+                                                               eps, scale_out, bias_out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}

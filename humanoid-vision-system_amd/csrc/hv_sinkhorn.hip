@@ -1,0 +1,220 @@
+// Grouped Sinkhorn-Knopp projection for gfx950.
+//
+// Replaces SinkhornKnoppProjection.forward (reference src/models/manifold_layers.py:32-93).
+// The reference rescales the whole matrix in place 2*iters times and reads three host
+// scalars per iteration (.item(), :68,73,76).  Every step of that loop is a row or a
+// column scaling, so M_t = diag(a_t) K diag(b_t) with K = softmax(raw/tau)*m fixed:
+//     r_t  = a_t (.) (K b_t)            (row sums, :66)
+//     a_t+1 = a_t / (r_t + eps)         (:67)
+//     c_t  = b_t (.) (K^T a_t+1)        (column sums, :71)
+//     b_t+1 = b_t / (c_t + eps)         (:72)
+// K is read, never rewritten: each iteration is one fused "row dots + column partial
+// sums" pass over K (L2/MALL resident) and one tiny column-reduce pass.  Every matrix of
+// every mHC site of the model shares the same 2*iters+2 launches (a device table of
+// entries), nothing syncs with the host, and the a/b/r vectors of every iteration stay in
+// the workspace for the analytic backward.  Summation order is fixed -> bitwise
+// reproducible.
+#include "hv_common.h"
+
+namespace {
+
+constexpr int RB = 16;          // rows per block in the row pass (4 per wave)
+constexpr int MAXQ = 32;        // up to 64*32 = 2048 columns held per lane
+
+struct Work {                   // carve of hv_sinkhorn_entry::work
+  float* a;                     // [(iters+1), batch*n]
+  float* b;                     // [(iters+1), batch*m]
+  float* r;                     // [iters, batch*n]
+  float* part;                  // [batch, ceil(n/RB), m] column partials
+};
+
+__device__ __forceinline__ Work carve(const hv_sinkhorn_entry& e) {
+  Work w;
+  const long bn = (long)e.batch * e.n, bm = (long)e.batch * e.m;
+  w.a = e.work;
+  w.b = w.a + (long)(e.iters + 1) * bn;
+  w.r = w.b + (long)(e.iters + 1) * bm;
+  w.part = w.r + (long)e.iters * bn;
+  return w;
+}
+
+// Find the entry whose [start, start+len) range contains idx (entries sorted by start).
+template <int FIELD>
+__device__ __forceinline__ int find_entry(const hv_sinkhorn_entry* t, int count, int idx) {
+  int lo = 0, hi = count - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    int s = FIELD == 0 ? t[mid].row_start : (FIELD == 1 ? t[mid].row_block_start : t[mid].col_start);
+    if (s <= idx) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// K = softmax(raw / tau, -1) * m (manifold_layers.py:56-57); a_0 = b_0 = 1.
+__global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restrict__ tab,
+                                               int count, int total_rows) {
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= total_rows) return;
+  const int ei = find_entry<0>(tab, count, g);
+  const hv_sinkhorn_entry e = tab[ei];
+  const int row = g - e.row_start;               // row within batch*n
+  const float* src = e.raw + (long)row * e.m;
+  float* dst = e.out + (long)row * e.m;
+  const float inv_tau = 1.0f / e.tau;
+  float mx = -INFINITY;
+  for (int j = lane; j < e.m; j += 64) mx = fmaxf(mx, src[j] * inv_tau);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int j = lane; j < e.m; j += 64) s += __expf(src[j] * inv_tau - mx);
+  s = wave_sum(s);
+  const float k = (float)e.m / s;
+  for (int j = lane; j < e.m; j += 64) dst[j] = __expf(src[j] * inv_tau - mx) * k;
+  Work w = carve(e);
+  if (lane == 0) w.a[row] = 1.0f;
+}
+
+__global__ void __launch_bounds__(256) sk_init_cols(const hv_sinkhorn_entry* __restrict__ tab,
+                                                    int count, int total_cols) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= total_cols) return;
+  const hv_sinkhorn_entry e = tab[find_entry<2>(tab, count, g)];
+  carve(e).b[g - e.col_start] = 1.0f;
+}
+
+// Iteration t, pass 1: row dots -> r_t, a_t+1 ; column partial sums of a_t+1 (.) K.
+__global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restrict__ tab,
+                                               int count, int t) {
+  __shared__ float colpart[4][64 * MAXQ];
+  const int ei = find_entry<1>(tab, count, blockIdx.x);
+  const hv_sinkhorn_entry e = tab[ei];
+  if (t >= e.iters) return;
+  const Work w = carve(e);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nrb = (e.n + RB - 1) / RB;
+  const int lb = blockIdx.x - e.row_block_start;  // local row block
+  const int bidx = lb / nrb, rb = lb % nrb;
+  const int m = e.m, n = e.n;
+  const int nq = (m + 63) >> 6;
+  const float* K = e.out + (long)bidx * n * m;
+  const float* bt = w.b + (long)t * e.batch * m + (long)bidx * m;
+  const float* at = w.a + (long)t * e.batch * n + (long)bidx * n;
+  float* an = w.a + (long)(t + 1) * e.batch * n + (long)bidx * n;
+  float* rt = w.r + (long)t * e.batch * n + (long)bidx * n;
+
+  float bq[MAXQ], acc[MAXQ];
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q) {
+    const int j = lane + 64 * q;
+    bq[q] = (q < nq && j < m) ? bt[j] : 0.f;
+    acc[q] = 0.f;
+  }
+  for (int rr = 0; rr < RB / 4; ++rr) {
+    const int i = rb * RB + wv * (RB / 4) + rr;
+    if (i >= n) break;
+    const float* Ki = K + (long)i * m;
+    float kv[MAXQ];
+    float dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int j = lane + 64 * q;
+      kv[q] = (q < nq && j < m) ? Ki[j] : 0.f;
+      dot += kv[q] * bq[q];
+    }
+    dot = wave_sum(dot);
+    const float ai = at[i];
+    const float r = ai * dot;
+    const float a1 = ai / (r + e.eps);
+    if (lane == 0) { rt[i] = r; an[i] = a1; }
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) acc[q] += a1 * kv[q];
+  }
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q)
+    if (q < nq) colpart[wv][lane + 64 * q] = acc[q];
+  __syncthreads();
+  float* part = w.part + ((long)bidx * nrb + rb) * m;
+  for (int j = threadIdx.x; j < m; j += 256)
+    part[j] = (colpart[0][j] + colpart[1][j]) + (colpart[2][j] + colpart[3][j]);
+}
+
+// Iteration t, pass 2: c_t = b_t (.) sum(partials); b_t+1 = b_t / (c_t + eps).
+__global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restrict__ tab,
+                                               int count, int total_cols, int t) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= total_cols) return;
+  const int ei = find_entry<2>(tab, count, g);
+  const hv_sinkhorn_entry e = tab[ei];
+  if (t >= e.iters) return;
+  const Work w = carve(e);
+  const int c = g - e.col_start;           // within batch*m
+  const int bidx = c / e.m, j = c % e.m;
+  const int nrb = (e.n + RB - 1) / RB;
+  const float* part = w.part + (long)bidx * nrb * e.m + j;
+  float s = 0.f;
+  for (int r = 0; r < nrb; ++r) s += part[(long)r * e.m];
+  const long bm = (long)e.batch * e.m;
+  const float b = w.b[(long)t * bm + c];
+  const float cs = b * s;
+  w.b[(long)(t + 1) * bm + c] = b / (cs + e.eps);
+}
+
+// M = diag(a_T) K diag(b_T) in place; history[t] = |mean_i r_t,i - 1| (:76-77).
+__global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restrict__ tab,
+                                                int count, int total_rows) {
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= total_rows) return;
+  const int ei = find_entry<0>(tab, count, g);
+  const hv_sinkhorn_entry e = tab[ei];
+  const Work w = carve(e);
+  const int row = g - e.row_start;
+  const int bidx = row / e.n;
+  const long bn = (long)e.batch * e.n, bm = (long)e.batch * e.m;
+  const float ai = w.a[(long)e.iters * bn + row];
+  const float* bT = w.b + (long)e.iters * bm + (long)bidx * e.m;
+  float* M = e.out + (long)row * e.m;
+  for (int j = lane; j < e.m; j += 64) M[j] = ai * M[j] * bT[j];
+  if (row == 0 && e.history) {             // first row's wave reduces the history
+    for (int t = 0; t < e.iters; ++t) {
+      const float* rt = w.r + (long)t * bn;
+      float s = 0.f;
+      for (long i = lane; i < bn; i += 64) s += rt[i];
+      s = wave_sum(s);
+      if (lane == 0) e.history[t] = fabsf(s / (float)bn - 1.0f);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
+  const size_t bn = (size_t)batch * n, bm = (size_t)batch * m;
+  const size_t nrb = (size_t)(n + RB - 1) / RB;
+  return (size_t)(iters + 1) * bn + (size_t)(iters + 1) * bm + (size_t)iters * bn +
+         (size_t)batch * nrb * m;
+}
+
+extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count, int total_rows,
+                                         int total_row_blocks, int total_cols, int max_iters,
+                                         hv_stream_t stream) {
+  if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
+  sk_init_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols);
+  HV_CHECK_LAUNCH();
+  for (int t = 0; t < max_iters; ++t) {
+    sk_rows<<<total_row_blocks, 256, 0, s>>>(tab, count, t);
+    sk_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, t);
+  }
+  HV_CHECK_LAUNCH();
+  sk_final<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_abi_version(void) { return 1; }
+extern "C" void hv_struct_sizes(int* out2) {
+  out2[0] = (int)sizeof(hv_sinkhorn_entry);
+  out2[1] = (int)sizeof(hv_gemm_desc);
+}

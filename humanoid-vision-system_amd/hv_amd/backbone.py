@@ -1,0 +1,179 @@
+"""CNN backbone on the HIP path (reference src/models/vision_backbone.py).
+
+Activations stay NHWC end to end: the conv output is already the token-major [B*H*W, C]
+matrix the mHC layer consumes, so the reference's permute/reshape round trips
+(vision_backbone.py:121-123, 371-391) disappear.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .layers import ctx_scope, run_conv, to_nchw_view, to_nhwc
+from .manifold import ManifoldHyperConnection
+from .runtime import require_cuda, resolve_dtype
+
+
+class ConvMHCLayer(nn.Module):
+    """vision_backbone.py:10-134: conv -> BN -> act -> mHC(C_out) -> SE gate -> (+x)."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int = 3, stride: int = 1,
+                 padding: Optional[int] = None, groups: int = 1, expansion_rate: int = 4,
+                 use_mhc: bool = True, activation: str = "silu", sk_iterations: int = 20):
+        super().__init__()
+        if groups != 1:
+            raise NotImplementedError("grouped convolution is not on the HybridVision path")
+        self.in_channels, self.out_channels, self.stride, self.use_mhc = in_channels, out_channels, stride, use_mhc
+        padding = kernel_size // 2 if padding is None else padding
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False)
+        self.bn = nn.BatchNorm2d(out_channels)
+        acts = {"silu": nn.SiLU(), "relu": nn.ReLU(inplace=True), "gelu": nn.GELU()}
+        if activation not in acts:
+            raise ValueError(f"Unsupported activation: {activation}")
+        self.activation = acts[activation]
+        self.act_name = activation
+        self.mhc = ManifoldHyperConnection(out_channels, expansion_rate=expansion_rate,
+                                           sk_iterations=sk_iterations) if use_mhc else None
+        self.use_residual = in_channels == out_channels and stride == 1
+        if use_mhc and out_channels >= 32:
+            self.channel_attention = nn.Sequential(
+                nn.AdaptiveAvgPool2d(1), nn.Conv2d(out_channels, out_channels // 4, 1), self.activation,
+                nn.Conv2d(out_channels // 4, out_channels, 1), nn.Sigmoid())
+        else:
+            self.channel_attention = None
+        nn.init.kaiming_normal_(self.conv.weight, mode="fan_out", nonlinearity="relu")
+        nn.init.ones_(self.bn.weight)
+        nn.init.zeros_(self.bn.bias)
+
+    def forward_nhwc(self, x: torch.Tensor, extra_residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        y = run_conv(x, self.conv, self.bn, self.act_name, self)
+        if self.mhc is not None:
+            n, h, w, c = y.shape
+            y = self.mhc.forward_tokens(y.view(-1, c)).view(n, h, w, c)
+            if self.channel_attention is not None:
+                ca = self.channel_attention
+                gate = ops.se_mlp(ops.channel_mean(y), ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
+                y = ops.scale_residual(y, gate, x if self.use_residual else None)
+                if extra_residual is not None:
+                    y = ops.add_scaled(y, extra_residual, 1.0)
+                return y
+        if self.use_residual:
+            y = ops.add_scaled(y, x, 1.0)
+        if extra_residual is not None:
+            y = ops.add_scaled(y, extra_residual, 1.0)
+        return y
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        require_cuda(x, "ConvMHCLayer")
+        with ctx_scope(self) as ctx:
+            return to_nchw_view(self.forward_nhwc(to_nhwc(x, ctx.dtype)))
+
+
+class ResidualMHCLayer(nn.Module):
+    """vision_backbone.py:137-196 (bottleneck branch for channels >= 64)."""
+
+    def __init__(self, channels: int, num_blocks: int = 2, expansion_rate: int = 4, bottleneck: bool = True,
+                 sk_iterations: int = 20):
+        super().__init__()
+        self.channels, self.num_blocks = channels, num_blocks
+        kw = dict(expansion_rate=expansion_rate, sk_iterations=sk_iterations)
+        if bottleneck and channels >= 64:
+            self.blocks = nn.Sequential(ConvMHCLayer(channels, channels // 2, kernel_size=1, **kw),
+                                        ConvMHCLayer(channels // 2, channels, kernel_size=3, **kw))
+            self.projection = ConvMHCLayer(channels, channels, kernel_size=1, **kw)
+        else:
+            self.blocks = nn.Sequential(*[ConvMHCLayer(channels, channels, kernel_size=3, **kw)
+                                          for _ in range(num_blocks)])
+            self.projection = nn.Identity()
+
+    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        y = x
+        for b in self.blocks:
+            y = b.forward_nhwc(y)
+        if isinstance(self.projection, nn.Identity):
+            return ops.add_scaled(y, x, 1.0)
+        return self.projection.forward_nhwc(y, extra_residual=x)
+
+    def forward(self, x):
+        require_cuda(x, "ResidualMHCLayer")
+        with ctx_scope(self) as ctx:
+            return to_nchw_view(self.forward_nhwc(to_nhwc(x, ctx.dtype)))
+
+
+class HybridVisionBackbone(nn.Module):
+    """vision_backbone.py:199-413."""
+
+    def __init__(self, input_channels: int = 3, base_channels: int = 32, num_blocks: List[int] = (2, 3, 4, 2),
+                 use_mhc: bool = True, activation: str = "silu", dropout_rate: float = 0.1,
+                 sk_iterations: int = 20, verbose: bool = True):
+        super().__init__()
+        self.input_channels, self.base_channels, self.use_mhc = input_channels, base_channels, use_mhc
+        self.dropout_rate = dropout_rate
+        kw = dict(use_mhc=use_mhc, activation=activation, sk_iterations=sk_iterations)
+        self.stem = nn.Sequential(
+            ConvMHCLayer(input_channels, base_channels, 3, 2, 1, **kw),
+            ConvMHCLayer(base_channels, base_channels, 3, 1, 1, **kw),
+            ConvMHCLayer(base_channels, base_channels * 2, 3, 1, 1, **kw),
+            nn.MaxPool2d(kernel_size=2, stride=2))
+        cur = base_channels * 2
+        stage_channels = [cur, cur * 2, cur * 4, cur * 8]
+        self.stages = nn.ModuleList()
+        for i, (nl, co) in enumerate(zip(num_blocks, stage_channels)):
+            layers = [ConvMHCLayer(cur, co, kernel_size=3, stride=2 if i > 0 else 1, **kw)]
+            layers += [ResidualMHCLayer(co, num_blocks=2, expansion_rate=4, bottleneck=True,
+                                        sk_iterations=sk_iterations) for _ in range(1, nl)]
+            self.stages.append(nn.Sequential(*layers))
+            cur = co
+        mk = (lambda c: ManifoldHyperConnection(c, expansion_rate=4, sk_iterations=sk_iterations)) if use_mhc \
+            else (lambda c: nn.Identity())
+        self.enhance_large = mk(stage_channels[-1])
+        self.enhance_medium = mk(stage_channels[-2])
+        self.enhance_small = mk(stage_channels[-3])
+        self.dropout = nn.Dropout2d(dropout_rate) if dropout_rate > 0 else nn.Identity()
+        self.output_channels = {"stem": base_channels * 2, "stage_1": stage_channels[0],
+                                "stage_2": stage_channels[1], "stage_3": stage_channels[2],
+                                "stage_4": stage_channels[3]}
+        self.stride_factors = {"stem": 4, "stage_1": 4, "stage_2": 8, "stage_3": 16, "stage_4": 32}
+        if verbose:
+            print(f"Backbone initialized with channels: {self.output_channels}")
+
+    def forward_nhwc(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+        for lyr in list(self.stem)[:3]:
+            x = lyr.forward_nhwc(x)
+        x = ops.maxpool2x2(x)
+        raw = {"stem": x}
+        for i, st in enumerate(self.stages):
+            for lyr in st:
+                x = lyr.forward_nhwc(x)
+            raw[f"stage_{i + 1}"] = x
+
+        def enh(mod, f):
+            if isinstance(mod, nn.Identity):
+                return f
+            n, h, w, c = f.shape
+            return mod.forward_tokens(f.view(-1, c)).view(n, h, w, c)
+
+        return {"scale_small": enh(self.enhance_small, raw["stage_2"]),
+                "scale_medium": enh(self.enhance_medium, raw["stage_3"]),
+                "scale_large": enh(self.enhance_large, raw["stage_4"]),
+                "raw_features": raw}
+
+    def forward(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
+        require_cuda(x, "HybridVisionBackbone")
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("hv_amd: backbone training backward is not implemented yet")
+        with ctx_scope(self) as ctx:
+            out = self.forward_nhwc(to_nhwc(x, ctx.dtype))
+        res = {k: to_nchw_view(v) for k, v in out.items() if k != "raw_features"}
+        res["raw_features"] = {k: to_nchw_view(v) for k, v in out["raw_features"].items()}
+        return res
+
+    def get_output_channels(self) -> Dict[str, int]:
+        return {"scale_small": self.output_channels["stage_2"], "scale_medium": self.output_channels["stage_3"],
+                "scale_large": self.output_channels["stage_4"]}
+
+    def get_stride_factors(self) -> Dict[str, int]:
+        return {"scale_small": 8, "scale_medium": 16, "scale_large": 32}

@@ -1,0 +1,288 @@
+"""mHC layers on the HIP path: Sinkhorn projection, ManifoldHyperConnection, mHC attention,
+RMSNorm.  Parameter/buffer names and shapes mirror reference src/models/manifold_layers.py so
+reference checkpoints load unchanged.
+
+mHC forward (manifold_layers.py:223-280), eval mode, restated for MI355X:
+    z   = (x - mean) * rstd                                   LayerNorm core, applied on load
+    h1  = GELU(z A1 + c1)      A1 = Gc W1^T, c1 = u W1^T + b1  (folded; or z Gc + u, then W1)
+    h2  = GELU(h1 W2^T + b2)
+    yc  = [x | h2] Wc          Wc = [H_res - rowmean ; H_post - rowmean]
+    out = LN_post(yc)
+with G = diag(gamma_pre) sigmoid(H_pre_raw), Gc = G - colmean_i(G), u = beta_pre sigmoid(H_pre_raw).
+Centering is exact because LayerNorm subtracts the row mean (sum_i z_i = 0; LN_post(y) =
+LN_post(y - const_row)); it removes the ~1/D-uniform part of H_res and the ~1.0-uniform part
+of H_post, which is what makes the reference's bf16 path O(1)-wrong.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .runtime import RunCtx, current, require_cuda, resolve_dtype, use_ctx
+
+
+# ================================================================== Sinkhorn
+class SinkhornKnoppProjection(nn.Module):
+    """Reference manifold_layers.py:10-101 (shim S1: 2-D input = batch of one)."""
+
+    def __init__(self, num_iterations: int = 20, epsilon: float = 1e-8, tau: float = 1.0):
+        super().__init__()
+        self.num_iterations = num_iterations
+        self.epsilon = epsilon
+        self.tau = tau
+        self.register_buffer("convergence_history", torch.zeros(num_iterations))
+
+    def forward(self, matrix: torch.Tensor, return_history: bool = False):
+        require_cuda(matrix, "SinkhornKnoppProjection")
+        if matrix.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("hv_amd: Sinkhorn backward is not implemented yet (inference path)")
+        g = ops.SinkhornGroup([matrix.detach().float().contiguous()], [self.num_iterations],
+                              matrix.device, self.epsilon, self.tau)
+        out = g.run()[0]
+        out = out.squeeze(0) if matrix.dim() == 2 else out
+        self.convergence_history.copy_(g.hists[0][: self.num_iterations])
+        if not return_history:
+            return out
+        return out, self._history_dict(g)
+
+    def _history_dict(self, g: "ops.SinkhornGroup") -> Dict[str, Any]:
+        # reference :86-91: per-iteration means of the row sums and of the column sums
+        e = g.entries[0]
+        b, n, m, it = e.batch, e.n, e.m, e.iters
+        w = g.works[0]
+        a_sz, b_sz = (it + 1) * b * n, (it + 1) * b * m
+        bh = w[a_sz:a_sz + b_sz].view(it + 1, b * m)
+        rh = w[a_sz + b_sz:a_sz + b_sz + it * b * n].view(it, b * n)
+        cs = (bh[:-1] / bh[1:] - self.epsilon)
+        rows = rh.mean(dim=1).tolist()
+        cols = cs.mean(dim=1).tolist()
+        return {"row_sums": rows, "col_sums": cols, "final_row_error": rows[-1] - 1.0,
+                "final_col_error": cols[-1] - 1.0}
+
+    def get_convergence_metrics(self) -> Dict[str, Any]:
+        h = self.convergence_history
+        return {"mean_convergence": h.mean().item(), "max_convergence": h.max().item(),
+                "final_convergence": h[-1].item()}
+
+
+# ================================================================== mHC plan
+FOLD_MAX_D = 1024   # fold H_pre into W1 for every site but the D=1792 final fusion
+
+
+@dataclass
+class MhcPlan:
+    D: int
+    Hd: int
+    fold: bool
+    dtype: torch.dtype
+    b1: torch.Tensor          # fold: a1t [2Hd, D]; else gct [Hd, D]
+    c1: torch.Tensor          # fold: c1 [2Hd] fp32; else u [Hd] fp32
+    w1: Optional[torch.Tensor]
+    bias1: Optional[torch.Tensor]
+    w2: torch.Tensor
+    bias2: torch.Tensor
+    wct: torch.Tensor
+    g_post: torch.Tensor
+    b_post: torch.Tensor
+
+
+def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.dtype) -> MhcPlan:
+    D, Hd = m.input_dim, m.hidden_dim
+    fold = D <= FOLD_MAX_D
+    gc, u, wct = ops.mhc_prep(m.H_pre_raw, m.H_post_raw, h_res, m.norm_pre.weight, m.norm_pre.bias,
+                              gc_transposed=not fold)
+    w1 = ops.f32(m.mlp[0].weight)
+    b1 = ops.f32(m.mlp[0].bias)
+    if fold:
+        # A1^T = W1 Gc^T  [2Hd, D];  c1 = W1 u + b1
+        a1t = ops.gemm(ops.cast(w1, dtype), ops.cast(gc, dtype), out_dtype=dtype)
+        c1 = ops.gemm(u.view(1, Hd), w1, bias=b1, out_dtype=torch.float32).view(-1)
+        first, second, w1c, b1c = a1t, c1, None, None
+    else:
+        first, second, w1c, b1c = ops.cast(gc, dtype), u, ops.cast(w1, dtype), b1
+    return MhcPlan(D=D, Hd=Hd, fold=fold, dtype=dtype, b1=first, c1=second, w1=w1c, bias1=b1c,
+                   w2=ops.cast(ops.f32(m.mlp[3].weight), dtype), bias2=ops.f32(m.mlp[3].bias),
+                   wct=ops.cast(wct, dtype), g_post=ops.f32(m.norm_post.weight),
+                   b_post=ops.f32(m.norm_post.bias))
+
+
+def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Token chain on x2 [T, D] (compute dtype).  Returns LN_post(...) (+ residual) [T, D]."""
+    mean, rstd = ops.row_stats(x2, 1e-5)
+    if p.fold:
+        h1 = ops.gemm(x2, p.b1, bias=p.c1, act="gelu", a_mean=mean, a_rstd=rstd)
+    else:
+        e = ops.gemm(x2, p.b1, bias=p.c1, a_mean=mean, a_rstd=rstd)
+        h1 = ops.gemm(e, p.w1, bias=p.bias1, act="gelu")
+    h2 = ops.gemm(h1, p.w2, bias=p.bias2, act="gelu")
+    yc = ops.gemm(x2, p.wct, a2=h2, out_dtype=torch.float32)
+    return ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x2.dtype, residual=residual)
+
+
+def prepare_plans(mods, ctx: RunCtx) -> None:
+    """Grouped Sinkhorn for every mHC module of a model + per-site coefficient prep."""
+    mods = [m for m in mods if id(m) not in ctx.plans]
+    if not mods:
+        return
+    dev = mods[0].H_res_raw.device
+    raws = [m.H_res_raw.detach().float().contiguous() for m in mods]
+    group = ops.SinkhornGroup(raws, [m.sinkhorn.num_iterations for m in mods], dev,
+                              mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau)
+    outs = group.run(raws)
+    for m, h, hist in zip(mods, outs, group.hists):
+        m.sinkhorn.convergence_history.copy_(hist[: m.sinkhorn.num_iterations])
+        ctx.plans[id(m)] = build_plan(m, h[0], ctx.dtype)
+
+
+# ================================================================== mHC layer
+class ManifoldHyperConnection(nn.Module):
+    """Reference manifold_layers.py:104-346 (same parameters, buffers and init)."""
+
+    def __init__(self, input_dim: int, expansion_rate: int = 4, hidden_dim: Optional[int] = None,
+                 alpha: float = 0.01, sk_iterations: int = 20, use_mixed_precision: bool = True,
+                 dropout_rate: float = 0.1):
+        super().__init__()
+        self.input_dim = input_dim
+        self.expansion_rate = expansion_rate
+        self.hidden_dim = hidden_dim or input_dim * expansion_rate
+        self.alpha = alpha
+        self.use_mixed_precision = use_mixed_precision
+        self.dropout_rate = dropout_rate
+        D, Hd = input_dim, self.hidden_dim
+        self.H_pre_raw = nn.Parameter(torch.empty(D, Hd))
+        self.H_post_raw = nn.Parameter(torch.empty(Hd, D))
+        self.H_res_raw = nn.Parameter(torch.empty(D, D))
+        self.sinkhorn = SinkhornKnoppProjection(sk_iterations)
+        self.mlp = nn.Sequential(nn.Linear(Hd, 2 * Hd), nn.GELU(), nn.Dropout(dropout_rate),
+                                 nn.Linear(2 * Hd, Hd), nn.GELU(), nn.Dropout(dropout_rate))
+        self.norm_pre = nn.LayerNorm(D)
+        self.norm_post = nn.LayerNorm(D)
+        self.dropout = nn.Dropout(dropout_rate)
+        self.register_buffer("gradient_norms", torch.zeros(3))
+        self.register_buffer("eigenvalues", torch.zeros(D))
+        self.register_buffer("signal_ratio_history", torch.zeros(1000))
+        self.signal_ratio_idx = 0
+        self.hv_precision = "bf16" if use_mixed_precision else "fp32"
+        self._frozen = None
+        for p in (self.H_pre_raw, self.H_post_raw, self.H_res_raw):   # :194-196
+            nn.init.xavier_uniform_(p, gain=0.1)
+        for lyr in (self.mlp[0], self.mlp[3]):                         # :199-203
+            nn.init.xavier_uniform_(lyr.weight, gain=math.sqrt(2))
+            nn.init.zeros_(lyr.bias)
+
+    @property
+    def dtype(self):
+        return torch.bfloat16 if self.use_mixed_precision else torch.float32
+
+    def constrained_matrices(self):
+        """(H_pre, H_post, H_res) (manifold_layers.py:205-221); the Sinkhorn runs on the GPU."""
+        require_cuda(self.H_res_raw, "constrained_matrices")
+        H_pre = torch.sigmoid(self.H_pre_raw)
+        H_post = 2 * torch.sigmoid(self.H_post_raw)
+        H_res = self.sinkhorn(self.H_res_raw)
+        return H_pre, H_post, H_res
+
+    def plan(self) -> MhcPlan:
+        ctx = current()
+        if ctx is not None:
+            p = ctx.plans.get(id(self))
+            if p is None:
+                prepare_plans([self], ctx)
+                p = ctx.plans[id(self)]
+            return p
+        own = RunCtx(dtype=resolve_dtype(self))
+        prepare_plans([self], own)
+        return own.plans[id(self)]
+
+    def forward_tokens(self, x2: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x2: [T, D] token-major in the compute dtype."""
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("hv_amd: mHC training backward is not implemented yet")
+        return mhc_apply(x2, self.plan(), residual)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        require_cuda(x, "ManifoldHyperConnection")
+        shape = x.shape
+        dt = resolve_dtype(self)
+        x2 = x.reshape(-1, shape[-1])
+        in_dtype = x2.dtype
+        x2 = x2.to(dt).contiguous()
+        y = self.forward_tokens(x2)
+        return y.view(shape).to(in_dtype if in_dtype in (torch.float32, torch.bfloat16) else dt)
+
+    def get_stability_metrics(self) -> Dict[str, Any]:
+        """manifold_layers.py:318-341 (host reads happen here, never in forward)."""
+        ev = self.eigenvalues
+        metrics = {"max_eigenvalue": ev.max().item(), "min_eigenvalue": ev.min().item(),
+                   "eigenvalue_range": (ev.max() - ev.min()).item(),
+                   "sk_convergence": self.sinkhorn.get_convergence_metrics()}
+        if self.signal_ratio_idx > 0:
+            h = self.signal_ratio_history[: min(self.signal_ratio_idx, 1000)]
+            metrics.update({"signal_ratio_mean": h.mean().item(), "signal_ratio_std": h.std().item(),
+                            "signal_ratio_min": h.min().item(), "signal_ratio_max": h.max().item()})
+        if hasattr(self, "monitoring_metrics"):
+            metrics.update(self.monitoring_metrics)
+        return metrics
+
+    def extra_repr(self) -> str:
+        return (f"input_dim={self.input_dim}, hidden_dim={self.hidden_dim}, "
+                f"expansion={self.expansion_rate}, alpha={self.alpha}")
+
+
+# ================================================================== attention / norms
+class MultiHeadManifoldAttention(nn.Module):
+    """Reference manifold_layers.py:349-434: four mHC projections around softmax(QK^T/sqrt(hd))V."""
+
+    def __init__(self, embed_dim: int, num_heads: int = 8, dropout: float = 0.1, use_mhc: bool = True,
+                 sk_iterations: int = 20):
+        super().__init__()
+        assert embed_dim % num_heads == 0
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.head_dim = embed_dim // num_heads
+        self.use_mhc = use_mhc
+        if not use_mhc:
+            raise NotImplementedError("hv_amd implements the use_mhc=True attention (the reference default)")
+        kw = dict(expansion_rate=2, sk_iterations=sk_iterations)
+        self.q_proj = ManifoldHyperConnection(embed_dim, **kw)
+        self.k_proj = ManifoldHyperConnection(embed_dim, **kw)
+        self.v_proj = ManifoldHyperConnection(embed_dim, **kw)
+        self.out_proj = ManifoldHyperConnection(embed_dim, **kw)
+        self.dropout = nn.Dropout(dropout)
+        self.scaling = self.head_dim ** -0.5
+
+    def forward_tokens(self, x: torch.Tensor, n: int) -> torch.Tensor:
+        """Self-attention on x [n*L, D] (compute dtype); returns out_proj(attn) [n*L, D]."""
+        L = x.shape[0] // n
+        q = self.q_proj.forward_tokens(x).view(n, L, -1)
+        k = self.k_proj.forward_tokens(x).view(n, L, -1)
+        v = self.v_proj.forward_tokens(x).view(n, L, -1)
+        o = ops.attention(q, k, v, self.num_heads)
+        return self.out_proj.forward_tokens(o.view(n * L, -1))
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
+        require_cuda(query, "MultiHeadManifoldAttention")
+        if key is not query or value is not query or key_padding_mask is not None or need_weights:
+            raise NotImplementedError("hv_amd attention implements the self-attention call of "
+                                      "TransformerEncoderBlock (vit_encoder_decoder.py:191)")
+        n, L, D = query.shape
+        dt = resolve_dtype(self.q_proj)
+        x = query.reshape(n * L, D).to(dt).contiguous()
+        return self.forward_tokens(x, n).view(n, L, D).to(query.dtype), None
+
+
+class RMSNorm(nn.Module):
+    """Reference manifold_layers.py:437-456."""
+
+    def __init__(self, dim: int, eps: float = 1e-8):
+        super().__init__()
+        self.scale = nn.Parameter(torch.ones(dim))
+        self.eps = eps
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        require_cuda(x, "RMSNorm")
+        return ops.rmsnorm(x.contiguous(), ops.f32(self.scale), self.eps)

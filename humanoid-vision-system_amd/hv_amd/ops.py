@@ -1,0 +1,466 @@
+"""Torch-tensor wrappers over the libhvs C ABI.
+
+Every function launches HIP kernels on the current torch stream and returns freshly
+allocated (caching-allocator) tensors; there is no CPU or eager-PyTorch fallback.
+Activations are token-major: images are NHWC tensors [n, h, w, c] (contiguous), token
+sequences are [rows, c].
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import check, dtype_code, ptr, stream_ptr
+
+Tensor = torch.Tensor
+
+
+def _cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("hv_amd ops require CUDA(HIP) tensors; there is no CPU path")
+
+
+def _contig(t: Tensor, name: str) -> Tensor:
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+# ---------------------------------------------------------------------------- GEMM
+def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional[Tensor] = None,
+         act: str = "none", alpha: float = 1.0, residual: Optional[Tensor] = None,
+         a_mean: Optional[Tensor] = None, a_rstd: Optional[Tensor] = None,
+         a2: Optional[Tensor] = None, out_dtype: Optional[torch.dtype] = None,
+         out: Optional[Tensor] = None, residual_mod: int = 0) -> Tensor:
+    """C = act((a' @ b^T) * alpha * scale + bias) + residual.
+
+    a: [M, K1] (row stride may exceed K1), b: [N, K] with K = K1 (+ K2 if a2 [M, K2] given).
+    a_mean/a_rstd: per-row LayerNorm statistics applied to a while it is loaded.
+    """
+    _cuda(a, b)
+    if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm expects 2-D row-major operands")
+    if a.dtype != b.dtype or (a2 is not None and a2.dtype != a.dtype):
+        raise TypeError("gemm operands must share a dtype")
+    M, K1 = a.shape
+    K = K1 + (a2.shape[1] if a2 is not None else 0)
+    N = b.shape[0]
+    if b.shape[1] != K:
+        raise ValueError(f"gemm K mismatch: a {tuple(a.shape)} a2 {None if a2 is None else tuple(a2.shape)} b {tuple(b.shape)}")
+    od = out_dtype or a.dtype
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=od)
+    d = L.GemmDesc()
+    d.dtype = dtype_code(a.dtype)
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda = a.data_ptr(), a.stride(0)
+    if a2 is not None:
+        if a2.shape[0] != M or a2.stride(1) != 1:
+            raise ValueError("a2 must be [M, K2] row-major")
+        d.A2, d.lda2, d.k1 = a2.data_ptr(), a2.stride(0), K1
+    d.B, d.ldb = b.data_ptr(), b.stride(0)
+    d.C, d.ldc, d.c_dtype = out.data_ptr(), out.stride(0), dtype_code(out.dtype)
+    d.a_mean, d.a_rstd = ptr(a_mean), ptr(a_rstd)
+    d.scale, d.bias = ptr(scale), ptr(bias)
+    d.act = L.ACT[act]
+    d.alpha = alpha
+    if residual is not None:
+        d.residual, d.ldr, d.r_dtype = residual.data_ptr(), residual.stride(0), dtype_code(residual.dtype)
+        d.r_mod = residual_mod
+    check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm M={M} N={N} K={K}")
+    return out
+
+
+def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, bias=None,
+           act: str = "none", residual: Optional[Tensor] = None,
+           out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    """Implicit-GEMM convolution. x: NHWC [n, h, w, c]; w: [cout, k*k*c] (from conv_weight_prep)."""
+    _cuda(x, w)
+    _contig(x, "conv input")
+    n, h, wd, c = x.shape
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (wd + 2 * pad - k) // stride + 1
+    cout = w.shape[0]
+    out = torch.empty((n, oh, ow, cout), device=x.device, dtype=out_dtype or x.dtype)
+    d = L.GemmDesc()
+    d.dtype = dtype_code(x.dtype)
+    d.M, d.N, d.K = n * oh * ow, cout, k * k * c
+    if w.shape[1] != d.K:
+        raise ValueError(f"conv weight K {w.shape[1]} != {d.K}")
+    d.A, d.lda = x.data_ptr(), c
+    d.B, d.ldb = w.data_ptr(), w.stride(0)
+    d.C, d.ldc, d.c_dtype = out.data_ptr(), cout, dtype_code(out.dtype)
+    d.scale, d.bias = ptr(scale), ptr(bias)
+    d.act = L.ACT[act]
+    d.alpha = 1.0
+    if residual is not None:
+        _contig(residual, "residual")
+        d.residual, d.ldr, d.r_dtype = residual.data_ptr(), cout, dtype_code(residual.dtype)
+    d.conv_n, d.conv_h, d.conv_w, d.conv_c = n, h, wd, c
+    d.conv_k, d.conv_stride, d.conv_pad, d.conv_oh, d.conv_ow = k, stride, pad, oh, ow
+    check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(conv {c}->{cout} k{k} s{stride})")
+    return out
+
+
+# ---------------------------------------------------------------------------- parameters
+def conv_weight_prep(w: Tensor, dtype: torch.dtype, scale: Optional[Tensor] = None) -> Tensor:
+    """[cout, cin, k, k] fp32 -> [cout, k*k*cin] (K padded to a 16-byte multiple)."""
+    _cuda(w)
+    w = w.detach().float().contiguous()
+    cout, cin, k, _ = w.shape
+    kk = k * k * cin
+    epc = 8 if dtype == torch.bfloat16 else 4
+    kp = (kk + epc - 1) // epc * epc
+    if kp == kk:
+        out = torch.empty((cout, kk), device=w.device, dtype=dtype)
+        check(L.lib().hv_conv_weight_prep(w.data_ptr(), cout, cin, k, ptr(scale), dtype_code(dtype),
+                                          out.data_ptr(), stream_ptr()), "hv_conv_weight_prep")
+        return out
+    tmp = torch.empty((cout, kk), device=w.device, dtype=dtype)
+    check(L.lib().hv_conv_weight_prep(w.data_ptr(), cout, cin, k, ptr(scale), dtype_code(dtype),
+                                      tmp.data_ptr(), stream_ptr()), "hv_conv_weight_prep")
+    out = torch.zeros((cout, kp), device=w.device, dtype=dtype)
+    out[:, :kk].copy_(tmp)
+    return out[:, :kk]
+
+
+def bn_fold(c: int, device, gamma=None, beta=None, mean=None, var=None, conv_bias=None,
+            eps: float = 1e-5):
+    s = torch.empty(c, device=device, dtype=torch.float32)
+    b = torch.empty(c, device=device, dtype=torch.float32)
+    f = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+    gamma, beta, mean, var, conv_bias = map(f, (gamma, beta, mean, var, conv_bias))
+    check(L.lib().hv_bn_fold(c, ptr(gamma), ptr(beta), ptr(mean), ptr(var), ptr(conv_bias), eps,
+                             s.data_ptr(), b.data_ptr(), stream_ptr()), "hv_bn_fold")
+    return s, b
+
+
+def cast(x: Tensor, dtype: torch.dtype) -> Tensor:
+    _cuda(x)
+    x = x.detach()
+    if x.dtype != torch.float32:
+        raise TypeError("cast expects fp32 input")
+    x = x.contiguous()
+    if dtype == torch.float32:
+        return x
+    y = torch.empty(x.shape, device=x.device, dtype=dtype)
+    check(L.lib().hv_cast(x.data_ptr(), x.numel(), dtype_code(dtype), y.data_ptr(), stream_ptr()), "hv_cast")
+    return y
+
+
+def f32(t: Optional[Tensor]) -> Optional[Tensor]:
+    return None if t is None else t.detach().float().contiguous()
+
+
+# ---------------------------------------------------------------------------- norms
+def row_stats(x: Tensor, eps: float = 1e-5):
+    _cuda(x)
+    rows, cols = x.shape
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    check(L.lib().hv_row_stats(dtype_code(x.dtype), x.data_ptr(), x.stride(0), rows, cols, eps,
+                               mean.data_ptr(), rstd.data_ptr(), stream_ptr()), "hv_row_stats")
+    return mean, rstd
+
+
+def layernorm(x: Tensor, gamma: Optional[Tensor], beta: Optional[Tensor], eps: float = 1e-5,
+              out_dtype: Optional[torch.dtype] = None, residual: Optional[Tensor] = None) -> Tensor:
+    _cuda(x)
+    _contig(x, "layernorm input")
+    rows, cols = x.reshape(-1, x.shape[-1]).shape
+    y = torch.empty(x.shape, device=x.device, dtype=out_dtype or x.dtype)
+    if residual is not None:
+        _contig(residual, "residual")
+    check(L.lib().hv_layernorm(dtype_code(x.dtype), x.data_ptr(), rows, cols, eps, ptr(gamma), ptr(beta),
+                               dtype_code(y.dtype), y.data_ptr(), ptr(residual),
+                               dtype_code(residual.dtype) if residual is not None else 0, stream_ptr()),
+          "hv_layernorm")
+    return y
+
+
+def rmsnorm(x: Tensor, scale: Tensor, eps: float = 1e-8) -> Tensor:
+    _cuda(x)
+    _contig(x, "rmsnorm input")
+    cols = x.shape[-1]
+    y = torch.empty_like(x)
+    check(L.lib().hv_rmsnorm(dtype_code(x.dtype), x.data_ptr(), x.numel() // cols, cols, eps,
+                             scale.data_ptr(), y.data_ptr(), stream_ptr()), "hv_rmsnorm")
+    return y
+
+
+# ---------------------------------------------------------------------------- sinkhorn
+class SinkhornGroup:
+    """A device table of Sinkhorn problems launched together (hv_sinkhorn_group_forward).
+
+    Buffers (outputs, workspaces, the table itself) are allocated once per group and reused
+    on every run, so the table's pointers stay valid.
+    """
+
+    def __init__(self, raws, iters, device, eps: float = 1e-8, tau: float = 1.0):
+        self.raws = list(raws)
+        self.iters = list(iters)
+        lib = L.lib()
+        n_e = len(self.raws)
+        self.outs, self.hists, self.works = [], [], []
+        entries = (L.SinkhornEntry * n_e)()
+        rs = rbs = cs = 0
+        for i, (raw, it) in enumerate(zip(self.raws, self.iters)):
+            if raw.dim() == 2:
+                b, n, m = 1, raw.shape[0], raw.shape[1]
+            else:
+                b, n, m = raw.shape
+            if m > 2048:
+                raise ValueError("hv sinkhorn supports up to 2048 columns")
+            out = torch.empty((b, n, m), device=device, dtype=torch.float32)
+            hist = torch.zeros(max(it, 1), device=device, dtype=torch.float32)
+            work = torch.empty(lib.hv_sinkhorn_work_floats(b, n, m, it), device=device, dtype=torch.float32)
+            self.outs.append(out)
+            self.hists.append(hist)
+            self.works.append(work)
+            e = entries[i]
+            e.raw = 0  # filled per run (raw may be re-materialised)
+            e.out, e.history, e.work = out.data_ptr(), hist.data_ptr(), work.data_ptr()
+            e.batch, e.n, e.m, e.iters, e.eps, e.tau = b, n, m, it, eps, tau
+            e.row_start, e.row_block_start, e.col_start = rs, rbs, cs
+            rs += b * n
+            rbs += b * ((n + 15) // 16)
+            cs += b * m
+        self.entries = entries
+        self.totals = (rs, rbs, cs)
+        self.table = None
+        self._raw_ptrs = None
+        self.device = device
+
+    def run(self, raws=None):
+        raws = self.raws if raws is None else raws
+        rp = tuple(r.data_ptr() for r in raws)
+        if rp != self._raw_ptrs:
+            for e, p in zip(self.entries, rp):
+                e.raw = p
+            host = torch.frombuffer(bytearray(bytes(self.entries)), dtype=torch.uint8)
+            self.table = host.to(self.device)
+            self._raw_ptrs = rp
+        rs, rbs, cs = self.totals
+        check(L.lib().hv_sinkhorn_group_forward(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
+                                                max(self.iters), stream_ptr()), "hv_sinkhorn_group_forward")
+        return self.outs
+
+
+def sinkhorn(raw: Tensor, iters: int, eps: float = 1e-8, tau: float = 1.0):
+    """One Sinkhorn-Knopp projection ([n, m] or [b, n, m]); returns (M, history)."""
+    _cuda(raw)
+    r = raw.detach().float().contiguous()
+    g = SinkhornGroup([r], [iters], raw.device, eps, tau)
+    out = g.run([r])[0]
+    return (out.squeeze(0) if raw.dim() == 2 else out), g.hists[0][:iters]
+
+
+# ---------------------------------------------------------------------------- mHC prep
+def mhc_prep(h_pre_raw, h_post_raw, h_res, gamma_pre, beta_pre, gc_transposed: bool):
+    D, Hd = h_pre_raw.shape
+    dev = h_pre_raw.device
+    gc = torch.empty((Hd, D) if gc_transposed else (D, Hd), device=dev, dtype=torch.float32)
+    u = torch.empty(Hd, device=dev, dtype=torch.float32)
+    wct = torch.empty((D, D + Hd), device=dev, dtype=torch.float32)
+    rm = torch.empty(D + Hd, device=dev, dtype=torch.float32)
+    args = [f32(h_pre_raw), f32(h_post_raw), h_res.contiguous(), f32(gamma_pre), f32(beta_pre)]
+    check(L.lib().hv_mhc_prep(D, Hd, *[a.data_ptr() for a in args], gc.data_ptr(), int(gc_transposed),
+                              u.data_ptr(), wct.data_ptr(), rm.data_ptr(), stream_ptr()), "hv_mhc_prep")
+    return gc, u, wct
+
+
+# ---------------------------------------------------------------------------- pointwise
+def nchw_to_nhwc(x: Tensor, dtype: torch.dtype) -> Tensor:
+    _cuda(x)
+    x = x.float().contiguous()
+    n, c, h, w = x.shape
+    y = torch.empty((n, h, w, c), device=x.device, dtype=dtype)
+    check(L.lib().hv_nchw_to_nhwc(x.data_ptr(), n, c, h, w, dtype_code(dtype), y.data_ptr(), stream_ptr()),
+          "hv_nchw_to_nhwc")
+    return y
+
+
+def maxpool2x2(x: Tensor) -> Tensor:
+    n, h, w, c = x.shape
+    y = torch.empty((n, h // 2, w // 2, c), device=x.device, dtype=x.dtype)
+    check(L.lib().hv_maxpool2x2(dtype_code(x.dtype), _contig(x, "x").data_ptr(), n, h, w, c, y.data_ptr(),
+                                stream_ptr()), "hv_maxpool2x2")
+    return y
+
+
+def channel_mean(x: Tensor) -> Tensor:
+    """NHWC [n, h, w, c] (or [n, p, c]) -> fp32 [n, c]."""
+    _contig(x, "x")
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    out = torch.empty((n, c), device=x.device, dtype=torch.float32)
+    work = torch.empty(L.lib().hv_channel_mean_work_floats(n, hw, c), device=x.device, dtype=torch.float32)
+    check(L.lib().hv_channel_mean(dtype_code(x.dtype), x.data_ptr(), n, hw, c, out.data_ptr(), work.data_ptr(),
+                                  stream_ptr()), "hv_channel_mean")
+    return out
+
+
+def se_mlp(pooled: Tensor, w1, b1, w2, b2) -> Tensor:
+    n, c = pooled.shape
+    cr = w1.shape[0]
+    gate = torch.empty_like(pooled)
+    w1, b1, w2, b2 = map(f32, (w1, b1, w2, b2))
+    check(L.lib().hv_se_mlp(pooled.data_ptr(), n, c, cr, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                            b2.data_ptr(), gate.data_ptr(), stream_ptr()), "hv_se_mlp")
+    return gate
+
+
+def scale_residual(x: Tensor, gate: Tensor, identity: Optional[Tensor]) -> Tensor:
+    _contig(x, "x")
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    if gate.shape != (n, c) or gate.dtype != torch.float32 or not gate.is_contiguous():
+        raise ValueError("scale_residual: gate must be contiguous fp32 [n, c]")
+    y = torch.empty_like(x)
+    if identity is not None:
+        _contig(identity, "identity")
+        if identity.shape != x.shape or identity.dtype != x.dtype:
+            raise ValueError("scale_residual: identity must match x")
+    check(L.lib().hv_scale_residual(dtype_code(x.dtype), x.data_ptr(), gate.data_ptr(), ptr(identity), n, hw, c,
+                                    y.data_ptr(), stream_ptr()), "hv_scale_residual")
+    return y
+
+
+def upsample_add(a: Tensor, b: Tensor) -> Tensor:
+    n, h, w, c = a.shape
+    hb, wb = b.shape[1], b.shape[2]
+    if b.shape[0] != n or b.shape[3] != c or a.dtype != b.dtype:
+        raise ValueError("upsample_add: batch/channel/dtype mismatch")
+    y = torch.empty_like(a)
+    check(L.lib().hv_upsample_add(dtype_code(a.dtype), _contig(a, "a").data_ptr(), _contig(b, "b").data_ptr(),
+                                  n, h, w, c, hb, wb, y.data_ptr(), stream_ptr()), "hv_upsample_add")
+    return y
+
+
+def add_scaled(a: Tensor, b: Tensor, alpha: float) -> Tensor:
+    if a.shape != b.shape or a.dtype != b.dtype:
+        raise ValueError(f"add_scaled: {tuple(a.shape)}/{a.dtype} vs {tuple(b.shape)}/{b.dtype}")
+    y = torch.empty_like(a)
+    check(L.lib().hv_add_scaled(dtype_code(a.dtype), _contig(a, "a").data_ptr(), _contig(b, "b").data_ptr(),
+                                a.numel(), alpha, y.data_ptr(), stream_ptr()), "hv_add_scaled")
+    return y
+
+
+def add_rowvec(x: Tensor, v: Tensor) -> Tensor:
+    n, c = x.shape[0], x.shape[-1]
+    p = x.numel() // (n * c)
+    v = f32(v)
+    if v.shape != (n, c):
+        raise ValueError(f"add_rowvec: v {tuple(v.shape)} != {(n, c)}")
+    y = torch.empty_like(x)
+    check(L.lib().hv_add_rowvec(dtype_code(x.dtype), _contig(x, "x").data_ptr(), v.data_ptr(), n, p, c,
+                                y.data_ptr(), stream_ptr()), "hv_add_rowvec")
+    return y
+
+
+def interp_linear(src: Tensor, lout: int) -> Tensor:
+    """[L, D] fp32 -> [lout, D] (F.interpolate mode='linear', align_corners=False, on dim 0)."""
+    src = f32(src)
+    Ls, D = src.shape
+    dst = torch.empty((lout, D), device=src.device, dtype=torch.float32)
+    check(L.lib().hv_interp_linear(src.data_ptr(), Ls, D, lout, dst.data_ptr(), stream_ptr()), "hv_interp_linear")
+    return dst
+
+
+def vit_tokens(x: Tensor, cls: Tensor, pos: Tensor, scale: Tensor) -> Tensor:
+    """x [n, t, d] -> RMSNorm(cat(cls, x) + pos) [n, t+1, d]."""
+    n, t, d = x.shape
+    cls, pos, scale = f32(cls), f32(pos), f32(scale)      # keep temporaries alive over the launch
+    if cls.numel() != d or pos.shape != (t + 1, d) or scale.numel() != d:
+        raise ValueError("vit_tokens: cls/pos/scale shape mismatch")
+    y = torch.empty((n, t + 1, d), device=x.device, dtype=x.dtype)
+    check(L.lib().hv_vit_tokens(dtype_code(x.dtype), _contig(x, "x").data_ptr(), cls.data_ptr(),
+                                pos.data_ptr(), scale.data_ptr(), n, t, d, y.data_ptr(), stream_ptr()),
+          "hv_vit_tokens")
+    return y
+
+
+def attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
+    n, Lq, D = q.shape
+    hd = D // heads
+    o = torch.empty_like(q)
+    check(L.lib().hv_attention(dtype_code(q.dtype), _contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
+                               _contig(v, "v").data_ptr(), o.data_ptr(), n, Lq, heads, hd, hd ** -0.5,
+                               stream_ptr()), "hv_attention")
+    return o
+
+
+def gather_rows(x: Tensor, stride_rows: int) -> Tensor:
+    """Row 0 of every group of `stride_rows` rows: x [n*stride_rows, c] -> [n, c]."""
+    c = x.shape[-1]
+    rows = x.numel() // c
+    if rows % stride_rows:
+        raise ValueError("gather_rows: row count is not a multiple of stride_rows")
+    n = rows // stride_rows
+    y = torch.empty((n, c), device=x.device, dtype=x.dtype)
+    check(L.lib().hv_gather_rows(dtype_code(x.dtype), _contig(x, "x").data_ptr(), stride_rows, n, c,
+                                 y.data_ptr(), stream_ptr()), "hv_gather_rows")
+    return y
+
+
+def yolo_decode(logits: Tensor, A: int, nc: int, anchor_wh: Tensor):
+    """logits NHWC [n, h, w, A*(5+nc)] -> reference YOLODecoder outputs (shim S5 layout)."""
+    n, h, w, _ = logits.shape
+    dev = logits.device
+    P = 5 + nc
+    pred = torch.empty((n, A, h, w, P), device=dev, dtype=torch.float32)
+    boxes = torch.empty((n, A, h, w, 4), device=dev, dtype=torch.float32)
+    scores = torch.empty((n, A, h, w, nc), device=dev, dtype=torch.float32)
+    cs = torch.empty((n, A, h, w), device=dev, dtype=torch.float32)
+    ci = torch.empty((n, A, h, w), device=dev, dtype=torch.int64)
+    obj = torch.empty((n, A, h, w, 1), device=dev, dtype=torch.float32)
+    awh = f32(anchor_wh)
+    if awh.numel() != 2 * A or logits.shape[-1] != A * P:
+        raise ValueError("yolo_decode: anchor / channel count mismatch")
+    check(L.lib().hv_yolo_decode(dtype_code(logits.dtype), _contig(logits, "logits").data_ptr(), n, h, w, A, nc,
+                                 awh.data_ptr(), pred.data_ptr(), boxes.data_ptr(), scores.data_ptr(),
+                                 cs.data_ptr(), ci.data_ptr(), obj.data_ptr(), stream_ptr()), "hv_yolo_decode")
+    return {"boxes": boxes, "scores": scores, "class_scores": cs, "class_indices": ci,
+            "objectness": obj, "raw_predictions": pred}, pred
+
+
+# ---------------------------------------------------------------------------- debug tracing
+def _install_sync_check():
+    """HV_SYNC_CHECK=1: synchronise after every op and report the first one that faults."""
+    import functools
+    import os
+    import sys
+    if os.environ.get("HV_SYNC_CHECK") != "1":
+        return
+    mod = sys.modules[__name__]
+    for name in ("gemm", "conv2d", "conv_weight_prep", "bn_fold", "cast", "row_stats", "layernorm", "rmsnorm",
+                 "sinkhorn", "mhc_prep", "nchw_to_nhwc", "maxpool2x2", "channel_mean", "se_mlp",
+                 "scale_residual", "upsample_add", "add_scaled", "add_rowvec", "interp_linear", "vit_tokens",
+                 "attention", "gather_rows", "yolo_decode"):
+        fn = getattr(mod, name)
+
+        def wrap(fn=fn, name=name):
+            @functools.wraps(fn)
+            def inner(*a, **k):
+                desc = [tuple(t.shape) if isinstance(t, torch.Tensor) else t for t in a]
+                print(f"[hv] {name} {desc}", flush=True)
+                r = fn(*a, **k)
+                torch.cuda.synchronize()
+                return r
+            return inner
+        setattr(mod, name, wrap())
+    run0 = SinkhornGroup.run
+
+    def run(self, raws=None):
+        print(f"[hv] sinkhorn_group n={len(self.entries)} totals={self.totals}", flush=True)
+        r = run0(self, raws)
+        torch.cuda.synchronize()
+        return r
+    SinkhornGroup.run = run
+
+
+_install_sync_check()

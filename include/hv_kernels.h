@@ -1,0 +1,193 @@
+/*
+ * hv_kernels.h -- C ABI of the MI355X (gfx950) HybridVision hot-path library (libhvs.so).
+ *
+ * The reference (nazimurahman/humanoid-vision-system) has no FFI layer: its hot path is
+ * stock PyTorch ops called from the src/models nn.Modules.  These entry points are what
+ * those modules bind to instead (the Python side is humanoid-vision-system_amd/hv_amd,
+ * see INTEGRATION.md).  Each entry point names the reference function it replaces.
+ *
+ * Conventions
+ *   - plain device pointers + sizes; no torch types.  Activations are token-major
+ *     (NHWC / [tokens, channels]) and either fp32 or bf16 (raw 16-bit storage).
+ *   - the caller owns every buffer (PyTorch caching allocator); kernels never allocate.
+ *   - every call is asynchronous on `stream`, performs no host synchronisation and is
+ *     hipGraph-capturable.
+ *   - return value: 0 on success, a hipError_t (>0) from the launch, or a negative
+ *     argument-error code (HV_EINVAL / HV_EUNSUPPORTED).
+ */
+#ifndef HV_KERNELS_H
+#define HV_KERNELS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hv_stream_t; /* == hipStream_t */
+
+enum { HV_F32 = 0, HV_BF16 = 1 };
+enum { HV_ACT_NONE = 0, HV_ACT_RELU = 1, HV_ACT_SILU = 2, HV_ACT_GELU = 3,
+       HV_ACT_LEAKY = 4 /* slope 0.1 */, HV_ACT_SIGMOID = 5 };
+enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
+
+int hv_abi_version(void);
+/* sizeof(hv_sinkhorn_entry), sizeof(hv_gemm_desc): lets bindings verify their mirrors */
+void hv_struct_sizes(int* out2);
+
+/* ------------------------------------------------------------------------------------
+ * Sinkhorn-Knopp projection, grouped.
+ * Replaces SinkhornKnoppProjection.forward (reference src/models/manifold_layers.py:32-93,
+ * called from ManifoldHyperConnection.constrained_matrices :205-221).
+ * M = softmax(raw / tau, -1) * m, then `iters` x (row-normalise, column-normalise) with
+ * eps; history[t] = |mean(row sums at iteration t) - 1|.  All matrices of a table run in
+ * the same 2*iters+2 launches.  The table lives in device memory (hv_sinkhorn_entry[count]);
+ * row_block_start / col_start are exclusive prefix sums filled by the host.
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_sinkhorn_entry {
+  const float* raw;   /* [batch, n, m] fp32 */
+  float* out;         /* [batch, n, m] fp32 (also holds the softmax kernel K during the run) */
+  float* history;     /* [iters] or NULL */
+  float* work;        /* hv_sinkhorn_work_floats(batch, n, m, iters) floats */
+  int batch, n, m, iters;
+  float eps, tau;
+  int row_block_start; /* prefix over entries of batch*ceil(n/16) */
+  int col_start;       /* prefix over entries of batch*m */
+  int row_start;       /* prefix over entries of batch*n */
+  int pad_;
+} hv_sinkhorn_entry;
+
+size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters);
+int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* dev_table, int count,
+                              int total_rows, int total_row_blocks, int total_cols,
+                              int max_iters, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * MFMA GEMM with fused prologue/epilogue:  C[M,N] = epi( A'[M,K] . B[N,K]^T )
+ * Replaces the conv2d / linear / matmul calls of the reference hot path
+ * (vision_backbone.py:42-49,112-114; feature_fusion.py:33-49,65; yolo_head.py:120-127,139;
+ *  manifold_layers.py:253-263; vit_encoder_decoder.py:94-97,146-152).
+ * A' = A (dense), LayerNorm-normalised A (a_mean/a_rstd per row), an implicit im2col of an
+ * NHWC image (conv_k > 0), or the K-concatenation [A | A2] (a2 != NULL, split at k1).
+ * epi: v = acc*alpha; v *= scale[n]; v += bias[n]; v = act(v); v += residual[m, n]; store.
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_gemm_desc {
+  int dtype;          /* HV_F32 or HV_BF16: storage type of A, A2 and B (fp32 accumulate) */
+  int M, N, K;
+  const void* A; long lda;
+  const void* A2; long lda2; int k1;   /* optional second K segment */
+  const void* B; long ldb;             /* [N, K], K contiguous */
+  void* C; long ldc; int c_dtype;      /* output storage type */
+  const float* a_mean;                 /* LN prologue (optional) */
+  const float* a_rstd;
+  const float* scale;                  /* [N] optional */
+  const float* bias;                   /* [N] optional */
+  int act;
+  float alpha;
+  const void* residual; long ldr; int r_dtype;  /* optional */
+  int r_mod;          /* > 0: residual row index = m % r_mod (broadcast over images) */
+  /* implicit-GEMM convolution: A is an NHWC image [conv_n, conv_h, conv_w, conv_c];
+     K = conv_k*conv_k*conv_c ordered (kh, kw, c); M = conv_n*conv_oh*conv_ow */
+  int conv_n, conv_h, conv_w, conv_c, conv_k, conv_stride, conv_pad, conv_oh, conv_ow;
+} hv_gemm_desc;
+
+int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
+ * RMSNorm :449-456 eps 1e-8).
+ * ------------------------------------------------------------------------------------ */
+int hv_row_stats(int dtype, const void* x, long ldx, int rows, int cols, float eps,
+                 float* mean, float* rstd, hv_stream_t stream);
+/* y = LN(x [+ res_in]) * gamma + beta [+ res_out];  x may be fp32 or bf16 */
+int hv_layernorm(int x_dtype, const void* x, int rows, int cols, float eps,
+                 const float* gamma, const float* beta,
+                 int y_dtype, void* y, const void* res_out, int res_dtype, hv_stream_t stream);
+int hv_rmsnorm(int dtype, const void* x, int rows, int cols, float eps, const float* scale,
+               void* y, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * mHC coefficient preparation (parameter-only; manifold_layers.py:205-221 + the algebraic
+ * fold documented in DESIGN.md): writes fp32
+ *   gc[D, Hd]   = (gamma_pre (.) sigmoid(H_pre_raw)) centred over the input index
+ *                 (stored [Hd, D] when gc_transposed)
+ *   u[Hd]       = beta_pre . sigmoid(H_pre_raw)
+ *   wct[D, D+Hd]= [H_res - rowmean | 2 sigmoid(H_post_raw) - rowmean]^T
+ * ------------------------------------------------------------------------------------ */
+int hv_mhc_prep(int D, int Hd, const float* h_pre_raw, const float* h_post_raw,
+                const float* h_res, const float* gamma_pre, const float* beta_pre,
+                float* gc, int gc_transposed /* 1: gc is [Hd, D] */, float* u, float* wct,
+                float* row_mean_ws, hv_stream_t stream);
+
+/* conv weight [cout, cin, k, k] fp32 -> implicit-GEMM operand [cout, k, k, cin] (fp32|bf16),
+   optionally scaled per output channel */
+int hv_conv_weight_prep(const float* w, int cout, int cin, int k, const float* scale,
+                        int y_dtype, void* y, hv_stream_t stream);
+/* eval BatchNorm (+ conv bias) -> per-channel scale/bias (gamma == NULL: bias passthrough) */
+int hv_bn_fold(int c, const float* gamma, const float* beta, const float* mean, const float* var,
+               const float* conv_bias, float eps, float* scale_out, float* bias_out,
+               hv_stream_t stream);
+
+/* elementwise cast fp32 -> (fp32|bf16) */
+int hv_cast(const float* x, long n, int y_dtype, void* y, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Pointwise / layout kernels of the CNN + FPN path (NHWC).
+ * ------------------------------------------------------------------------------------ */
+/* NCHW fp32 image -> NHWC (fp32|bf16) */
+int hv_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int y_dtype, void* y,
+                    hv_stream_t stream);
+/* MaxPool2d(2, 2) (vision_backbone.py:248) */
+int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int c, void* y,
+                  hv_stream_t stream);
+/* global average pool over H*W -> fp32 [n, c]  (vision_backbone.py:78; hybrid_vision.py:387) */
+size_t hv_channel_mean_work_floats(int n, int hw, int c);
+int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out, float* work,
+                    hv_stream_t stream);
+/* squeeze-excite MLP: s = sigmoid(W2 silu(W1 pooled + b1) + b2)  (vision_backbone.py:77-83) */
+int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
+              const float* w2, const float* b2, float* gate, hv_stream_t stream);
+/* y = x * gate[n, c] (+ identity)  (vision_backbone.py:126-132) */
+int hv_scale_residual(int dtype, const void* x, const float* gate, const void* identity,
+                      int n, int hw, int c, void* y, hv_stream_t stream);
+/* y = a + nearest_upsample(b) with integer factor (feature_fusion.py:116-146) */
+int hv_upsample_add(int dtype, const void* a, const void* b, int n, int h, int w, int c,
+                    int hb, int wb, void* y, hv_stream_t stream);
+/* y = (a + b) * alpha  (hybrid_vision.py:256-258) */
+int hv_add_scaled(int dtype, const void* a, const void* b, long count, float alpha, void* y,
+                  hv_stream_t stream);
+/* y[n, p, c] = x[n, p, c] + v[n, c]  (broadcast per image; vit_encoder_decoder.py:175-183) */
+int hv_add_rowvec(int dtype, const void* x, const float* v, int n, int p, int c, void* y,
+                  hv_stream_t stream);
+/* linear interpolation of a [L, D] table to [Lout, D] (F.interpolate mode='linear') */
+int hv_interp_linear(const float* src, int L, int D, int Lout, float* dst, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Transformer pieces (vit_encoder_decoder.py:77-108, manifold_layers.py:404-427)
+ * ------------------------------------------------------------------------------------ */
+/* y[b, 0] = cls + pos[0]; y[b, 1+i] = x[b, i] + pos[1+i];  then RMSNorm(scale) */
+int hv_vit_tokens(int dtype, const void* x, const float* cls, const float* pos, const float* scale,
+                  int n, int tokens, int d, void* y, hv_stream_t stream);
+/* out = softmax(q k^T * sm_scale) v per (batch, head); q/k/v/out token-major [n, L, heads*hd] */
+int hv_attention(int dtype, const void* q, const void* k, const void* v, void* out,
+                 int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream);
+/* y[b, c] = x[b, 0, c]  (strided row gather) */
+int hv_gather_rows(int dtype, const void* x, long stride_rows, int n, int c, void* y,
+                   hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * YOLO decode (yolo_head.py:196-201 permute + YOLODecoder.forward :220-294, shims S4/S5).
+ * logits: NHWC [n, h, w, A*(5+nc)] (fp32|bf16).  Writes fp32 predictions [n, A, h, w, 5+nc],
+ * boxes [n, A, h, w, 4] (xyxy, normalised), scores [.., nc], class_scores, objectness,
+ * int64 class_indices.
+ * ------------------------------------------------------------------------------------ */
+int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, int nc,
+                   const float* anchor_wh /* [A, 2] */, float* predictions, float* boxes,
+                   float* scores, float* class_scores, int64_t* class_indices,
+                   float* objectness, hv_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HV_KERNELS_H */

@@ -28,3 +28,26 @@ def gpu_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def formula_state_dict(tag: str, fam: str):
+    """Reference-layout state dict (tests/golden/state_dict_<tag>.json) filled from the weight
+    formula (oracle/weights.py) -- no reference import needed."""
+    import json
+    import torch
+    from oracle import weights as W
+    lay = json.load(open(os.path.join(GOLDEN, f"state_dict_{tag}.json")))
+    sd = {}
+    for name, shape, dt in lay:
+        t = W.make_tensor(name, tuple(shape), fam)
+        if t is None:
+            if name.endswith("anchors"):
+                t = torch.from_numpy(np.load(os.path.join(GOLDEN, "anchors.npy")))
+            else:
+                t = torch.zeros(shape, dtype=getattr(torch, dt))
+        sd[name] = t
+    return sd
+
+
+MODEL_CFG = {"tiny": dict(num_blocks=[1, 1, 1, 1], vit_depth=1, sk_iters=5, verbose=False),
+             "base": dict(verbose=False)}

@@ -1,0 +1,220 @@
+"""GPU parity of the individual HIP kernels (through the libhvs C ABI) against plain PyTorch
+fp32 references of the same op computed on the CPU, and against the oracle fixtures."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from oracle import cases
+
+pytestmark = pytest.mark.gpu
+
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+# bf16 operands are rounded to 8 significant bits; tolerance relative to the output scale
+TOL = {"fp32": 2e-5, "bf16": 2e-2}
+
+
+def _ops():
+    from hv_amd import ops
+    return ops
+
+
+def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+# ------------------------------------------------------------------------------ Sinkhorn
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,it", cases.SK_CASES)
+def test_sinkhorn_matches_reference_fixture(gpu_device, fam, D, it):
+    ops = _ops()
+    g = golden(f"sk_{fam}_D{D}_it{it}")
+    raw = cases.sinkhorn_raw(D, it, fam).to(gpu_device)
+    M, hist = ops.sinkhorn(raw, it)
+    M = M.cpu()
+    idx = [0, 1, D // 2, D - 1]
+    np.testing.assert_allclose(M[idx].numpy(), g["rows"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(M.sum(0).numpy(), g["col_sums"], rtol=2e-5)
+    np.testing.assert_allclose(M.sum(1).numpy(), g["row_sums"], rtol=2e-5)
+    np.testing.assert_allclose(hist.cpu().numpy(), g["history"], rtol=1e-3, atol=2e-7)
+    if "M" in g.files:
+        np.testing.assert_allclose(M.numpy(), g["M"], rtol=2e-5, atol=1e-8)
+
+
+def test_sinkhorn_batched_reference_cases(gpu_device):
+    ops = _ops()
+    for name, it in (("sk_batched_4x8x8", 20), ("sk_batched_2x5x7", 10)):
+        g = golden(name)
+        M, hist = ops.sinkhorn(torch.from_numpy(g["raw"]).to(gpu_device), it)
+        np.testing.assert_allclose(M.cpu().numpy(), g["M"], rtol=2e-5, atol=1e-7)
+        np.testing.assert_allclose(hist.cpu().numpy(), g["history"], rtol=1e-3, atol=2e-7)
+
+
+def test_sinkhorn_grouped_equals_single(gpu_device):
+    """All mHC sites share one launch set: grouped results must equal one-at-a-time runs."""
+    ops = _ops()
+    raws = [cases.sinkhorn_raw(D, 20, "wc").to(gpu_device) for D in (32, 64, 256, 512, 1792)]
+    grp = ops.SinkhornGroup(raws, [20, 5, 20, 20, 20], gpu_device)
+    outs = [o.clone() for o in grp.run(raws)]
+    for r, it, o in zip(raws, [20, 5, 20, 20, 20], outs):
+        M, _ = ops.sinkhorn(r, it)
+        assert torch.equal(M, o[0])
+
+
+def test_sinkhorn_reference_properties(gpu_device):
+    """test_models.py:33-56 / :85-100: doubly stochastic within rtol 1e-4, deterministic."""
+    from hv_amd import SinkhornKnoppProjection
+    sk = SinkhornKnoppProjection(num_iterations=20).to(gpu_device)
+    x = torch.randn(4, 8, 8, generator=torch.Generator().manual_seed(0)).to(gpu_device)
+    p = sk(x)
+    assert torch.all(p >= 0)
+    rs, cs = p.sum(2), p.sum(1)
+    assert torch.allclose(rs, torch.ones_like(rs), rtol=1e-4)
+    assert torch.allclose(cs, torch.ones_like(cs), rtol=1e-4)
+    assert torch.equal(sk(x), p)
+    _, h = sk(x, return_history=True)
+    assert len(h["row_sums"]) == 20 and abs(h["final_col_error"]) < 1e-4
+
+
+# ------------------------------------------------------------------------------ GEMM
+GEMM_SHAPES = [(1, 64, 32), (7, 33, 40), (64, 256, 128), (130, 200, 96), (300, 64, 1024), (1000, 512, 256),
+               (257, 1000, 64)]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_gemm_epilogue_vs_torch(gpu_device, prec, M, N, K):
+    ops = _ops()
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(N, K, generator=g) / K ** 0.5
+    bias = torch.randn(N, generator=g)
+    scale = torch.rand(N, generator=g) + 0.5
+    res = torch.randn(M, N, generator=g)
+    dt = DT[prec]
+    ad, bd = a.to(dt), b.to(dt)
+    ref = F.gelu((ad.float() @ bd.float().T) * 0.5 * scale + bias) + res
+    out = ops.gemm(ad.to(gpu_device), bd.to(gpu_device), bias=bias.to(gpu_device), scale=scale.to(gpu_device),
+                   act="gelu", alpha=0.5, residual=res.to(gpu_device), out_dtype=torch.float32)
+    assert rel_err(out, ref) < TOL[prec]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_gemm_ln_prologue_and_concat(gpu_device, prec):
+    ops = _ops()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(5)
+    T, D, H, N = 200, 64, 96, 48
+    x = (torch.randn(T, D, generator=g) * 3 + 1).to(dt)
+    h = torch.randn(T, H, generator=g).to(dt)
+    b = (torch.randn(N, D, generator=g) / 8).to(dt)
+    bc = (torch.randn(N, D + H, generator=g) / 8).to(dt)
+    xd = x.to(gpu_device)
+    mean, rstd = ops.row_stats(xd, 1e-5)
+    z = F.layer_norm(x.float(), (D,), eps=1e-5)
+    out = ops.gemm(xd, b.to(gpu_device), a_mean=mean, a_rstd=rstd, out_dtype=torch.float32)
+    assert rel_err(out, z.to(dt).float() @ b.float().T) < TOL[prec]
+    out2 = ops.gemm(xd, bc.to(gpu_device), a2=h.to(gpu_device), out_dtype=torch.float32)
+    assert rel_err(out2, torch.cat([x, h], 1).float() @ bc.float().T) < TOL[prec]
+
+
+def test_gemm_residual_mod(gpu_device):
+    ops = _ops()
+    a = torch.randn(6 * 10, 32)
+    b = torch.randn(16, 32)
+    pos = torch.randn(10, 16)
+    out = ops.gemm(a.to(gpu_device), b.to(gpu_device), residual=pos.to(gpu_device), residual_mod=10)
+    ref = a @ b.T + pos.repeat(6, 1)
+    assert rel_err(out, ref) < 1e-5
+
+
+CONV_CASES = [(3, 32, 3, 2, 1, 33), (32, 32, 3, 1, 1, 20), (32, 64, 3, 2, 1, 17), (64, 32, 1, 1, 0, 9),
+              (128, 96, 3, 1, 1, 7), (16, 8, 3, 1, 1, 5)]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("cin,cout,k,s,p,hw", CONV_CASES)
+def test_conv_implicit_gemm_vs_torch(gpu_device, prec, cin, cout, k, s, p, hw):
+    ops = _ops()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(cin * 100 + cout + k + s)
+    x = torch.randn(2, cin, hw, hw + 3, generator=g).to(dt).float()
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(dt).float()
+    sc, bi = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)
+    ref = F.silu(F.conv2d(x, w, None, s, p) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1))
+    xd = ops.nchw_to_nhwc(x.to(gpu_device), dt)
+    wd = ops.conv_weight_prep(w.to(gpu_device), dt)
+    out = ops.conv2d(xd, wd, k, s, p, scale=sc.to(gpu_device), bias=bi.to(gpu_device), act="silu",
+                     out_dtype=torch.float32)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < TOL[prec]
+
+
+# ------------------------------------------------------------------------------ pointwise / norms
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_norms_and_pointwise_vs_torch(gpu_device, prec):
+    ops = _ops()
+    dt = DT[prec]
+    tol = TOL[prec]
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 12, 10, 64, generator=g).to(dt)
+    xd = x.to(gpu_device)
+    gam, bet = torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g)
+    y = ops.layernorm(xd.view(-1, 64).float().contiguous(), gam.to(gpu_device), bet.to(gpu_device), 1e-5)
+    assert rel_err(y, F.layer_norm(x.float().view(-1, 64), (64,), gam, bet, 1e-5)) < 1e-5
+    sc = torch.rand(64, generator=g) + 0.5
+    r = ops.rmsnorm(xd, sc.to(gpu_device))
+    xf = x.float()
+    assert rel_err(r, xf / torch.sqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-8) * sc) < tol
+    mp = ops.maxpool2x2(xd)
+    assert rel_err(mp, F.max_pool2d(xf.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)) < tol
+    cm = ops.channel_mean(xd)
+    assert rel_err(cm, xf.mean(dim=(1, 2))) < 1e-5
+    b = torch.randn(2, 6, 5, 64, generator=g).to(dt)
+    up = ops.upsample_add(xd, b.to(gpu_device))
+    ref = xf + F.interpolate(b.float().permute(0, 3, 1, 2), size=(12, 10), mode="nearest").permute(0, 2, 3, 1)
+    assert rel_err(up, ref) < tol
+    gate = torch.rand(2, 64, generator=g)
+    sr = ops.scale_residual(xd, gate.to(gpu_device), xd)
+    assert rel_err(sr, xf * gate.view(2, 1, 1, 64) + xf) < tol
+    w1, b1 = torch.randn(16, 64, 1, 1, generator=g) / 8, torch.randn(16, generator=g)
+    w2, b2 = torch.randn(64, 16, 1, 1, generator=g) / 4, torch.randn(64, generator=g)
+    pooled = torch.randn(2, 64, generator=g)
+    gt = ops.se_mlp(pooled.to(gpu_device), w1.to(gpu_device), b1.to(gpu_device), w2.to(gpu_device), b2.to(gpu_device))
+    ref = torch.sigmoid(F.linear(F.silu(F.linear(pooled, w1.view(16, 64), b1)), w2.view(64, 16), b2))
+    assert rel_err(gt, ref) < 1e-5
+    t = torch.randn(3 * 7, 64, generator=g).to(dt)
+    assert torch.equal(ops.gather_rows(t.to(gpu_device), 7).cpu(), t.view(3, 7, 64)[:, 0])
+    v = torch.randn(2, 64, generator=g)
+    assert rel_err(ops.add_rowvec(xd, v.to(gpu_device)), xf + v.view(2, 1, 1, 64)) < tol
+    pe = torch.randn(256, 32, generator=g)
+    for lout in (49, 400, 1024, 256):
+        ref = F.interpolate(pe.T.unsqueeze(0), size=(lout,), mode="linear").squeeze(0).T
+        assert rel_err(ops.interp_linear(pe.to(gpu_device), lout), ref) < 1e-6
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("L", [1, 50, 257, 401])
+def test_attention_vs_torch(gpu_device, prec, L):
+    ops = _ops()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(L)
+    q, k, v = (torch.randn(2, L, 256, generator=g).to(dt) for _ in range(3))
+    o = ops.attention(q.to(gpu_device), k.to(gpu_device), v.to(gpu_device), 8)
+    qh, kh, vh = (t.float().view(2, L, 8, 32).transpose(1, 2) for t in (q, k, v))
+    ref = (torch.softmax(qh @ kh.transpose(-1, -2) * 32 ** -0.5, -1) @ vh).transpose(1, 2).reshape(2, L, 256)
+    assert rel_err(o, ref) < TOL[prec]
+
+
+def test_decode_matches_reference_fixture(gpu_device):
+    ops = _ops()
+    g = golden("decode_s1")
+    pred = torch.from_numpy(g["pred"])                     # [2, 3, 7, 9, 85]
+    from oracle import hv_oracle as O
+    lg = pred.permute(0, 2, 3, 1, 4).reshape(2, 7, 9, 3 * 85).contiguous()
+    dec, pr = ops.yolo_decode(lg.to(gpu_device), 3, 80, O.anchor_wh(1).float().to(gpu_device))
+    np.testing.assert_array_equal(pr.cpu().numpy(), g["pred"])
+    np.testing.assert_allclose(dec["boxes"].cpu().numpy(), g["boxes"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dec["scores"].cpu().numpy(), g["scores"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(dec["class_indices"].cpu().numpy(), g["class_indices"])

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import formula_state_dict, golden
 from oracle import cases, hv_oracle as O, weights as W
 
 
@@ -123,24 +123,6 @@ def test_decode_matches_reference():
     np.testing.assert_allclose(out["boxes"].numpy(), g["boxes"], rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(out["scores"].numpy(), g["scores"], rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(out["class_indices"].numpy(), g["class_indices"])
-
-
-def formula_state_dict(tag: str, fam: str):
-    """Reference-layout state dict filled from the weight formula (no reference import)."""
-    import json
-    import os
-    from conftest import GOLDEN
-    lay = json.load(open(os.path.join(GOLDEN, f"state_dict_{tag}.json")))
-    sd = {}
-    for name, shape, dt in lay:
-        t = W.make_tensor(name, tuple(shape), fam)
-        if t is None:
-            if name.endswith("anchors"):
-                t = torch.from_numpy(np.load(os.path.join(GOLDEN, "anchors.npy")))
-            else:
-                t = torch.zeros(shape, dtype=getattr(torch, dt))
-        sd[name] = t
-    return sd
 
 
 @pytest.mark.parametrize("tag,tiny,fam,S,B,sub", cases.MODEL_CASES[:3])
