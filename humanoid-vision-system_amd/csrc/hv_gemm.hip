@@ -326,6 +326,13 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
 
 }  // namespace
 
+int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
+
+static int g_force_regstage = 0;
+static int hv_gemm_force_regstage() { return g_force_regstage; }
+// 1: route every GEMM through the register-staged kernel (A/B testing of the two paths)
+extern "C" void hv_gemm_set_path(int regstage_only) { g_force_regstage = regstage_only; }
+
 extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (!dp) return HV_EINVAL;
   const hv_gemm_desc& d = *dp;
@@ -342,6 +349,10 @@ extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (d.ldb % epc) return HV_EUNSUPPORTED;
   if (((uintptr_t)d.A | (uintptr_t)d.B) & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+  if (!hv_gemm_force_regstage()) {
+    const int rc = hv_gemm_glds(d, s);
+    if (rc != HV_EUNSUPPORTED) return rc;
+  }
   if (d.dtype == HV_BF16) return launch_typed<unsigned short>(d, s);
   if (d.dtype == HV_F32) return launch_typed<float>(d, s);
   return HV_EINVAL;

@@ -1,0 +1,265 @@
+// Fused mHC token chain for small D (gfx950, bf16 MFMA), replacing the six launches of the
+// unfused path (row stats, 3 GEMMs, LayerNorm) for the backbone's high-token-count sites:
+//
+//   z   = (x - mean) * rstd                    (LN_pre core; gamma/beta folded into A1/c1)
+//   h1  = GELU(z A1 + c1)          [BM x 2HD]  produced KC columns at a time, never stored
+//   h2  = GELU(h1 W2^T + b2)       [BM x HD]   accumulated in registers over the 2HD chunks
+//   y   = [x | h2] Wc              [BM x D]    Wc = centred [H_res ; H_post]
+//   out = LN_post(y) * g2 + b2'                computed from the GEMM3 accumulators in registers
+//
+// Reference: ManifoldHyperConnection.forward (manifold_layers.py:223-280); the algebra
+// (fold + centring) is documented in hv_amd/manifold.py and DESIGN.md.  Per token tile only x
+// (D*2 bytes/token) is read and out written: the [T, 2HD] and [T, HD] intermediates of the
+// unfused chain never reach HBM.
+//
+// Weights are not staged through LDS: every weight element a workgroup needs is consumed by
+// exactly one lane as an MFMA B fragment, so each lane loads its 16-byte fragments straight
+// from L2 into a 2-chunk-deep register ring (loads for chunk c+2 are issued while chunk c
+// computes).  LDS holds only the x/z tile, a double-buffered h1 chunk (one barrier per
+// chunk) and h2.  GELU uses an erf with |err| <= 1.5e-7 (A&S 7.1.26), far below bf16 rounding.
+#include "hv_common.h"
+
+namespace {
+
+template <int D, int HD, int NW>
+struct Cfg {
+  static constexpr int NT = 64 * NW;
+  static constexpr int BM = 4096 * NW / HD;       // acc2: BM x HD/NW per wave = 16 tiles (64 regs)
+  static constexpr int KC = 32;                   // 2HD chunk per step (one MFMA k-step)
+  static constexpr int NCH = 2 * HD / KC;
+  static constexpr int XS = D * 2 + 16;           // x / z row stride (bytes), == 16 mod 64
+  static constexpr int H1S = KC * 2 + 16;
+  static constexpr int H2S = HD * 2 + 16;
+  static constexpr int OFF_X = 0;
+  static constexpr int OFF_Z = BM * XS;
+  static constexpr int OFF_H1 = 2 * BM * XS;      // 2 buffers
+  static constexpr int OFF_H2 = OFF_H1 + 2 * BM * H1S;
+  static constexpr int LDS = OFF_H2 + BM * H2S;
+  // tiling
+  static constexpr int T1W = (BM / 16) * (KC / 16) / NW;   // GEMM1 tiles per wave
+  static constexpr int C2 = HD / NW / 16;                  // GEMM2 column tiles per wave
+  static constexpr int R2 = BM / 16;                       // GEMM2 row tiles
+  static constexpr int RT3 = (BM / 16) / NW;               // GEMM3 row tiles per wave
+  static constexpr int CT3 = D / 16;                       // GEMM3 column tiles
+  static constexpr int KS3 = (D + HD) / 32;                // GEMM3 k-steps
+  static_assert(R2 * C2 == 16, "acc2 tiling");
+  static_assert(T1W >= 1 && (BM / 16) * (KC / 16) % NW == 0, "gemm1 tiling");
+  static_assert(RT3 >= 1, "gemm3 tiling");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+__device__ __forceinline__ uint4 lds16(const unsigned char* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint4 gl16(const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ __forceinline__ f32x4 mfma(uint4 a, uint4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                 c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float u = x * 0.70710678118654752f;
+  const float a = fabsf(u);
+  const float t = 1.0f / (1.0f + 0.3275911f * a);
+  const float p = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t + 0.254829592f) * t;
+  const float e = 1.0f - p * __expf(-a * a);
+  return 0.5f * x * (1.0f + copysignf(e, u));
+}
+
+template <int D, int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
+    const unsigned short* __restrict__ x, int T,
+    const unsigned short* __restrict__ a1t,   // [2HD, D]
+    const float* __restrict__ c1,             // [2HD]
+    const unsigned short* __restrict__ w2,    // [HD, 2HD]
+    const float* __restrict__ b2,             // [HD]
+    const unsigned short* __restrict__ wct,   // [D, D+HD]
+    const float* __restrict__ g_post, const float* __restrict__ b_post,
+    unsigned short* __restrict__ out) {
+  using C = Cfg<D, HD, NW>;
+  constexpr int BM = C::BM, KC = C::KC;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const long t0 = (long)blockIdx.x * BM;
+
+  // ---------------- weight-fragment ring (registers), 2 chunks deep
+  uint4 fb1[2][C::T1W][D / 32];      // GEMM1 B fragments (rows of A1^T)
+  uint4 fb2[2][C::C2];               // GEMM2 B fragments (rows of W2)
+  float cb1[2][C::T1W];              // c1 bias per GEMM1 tile column
+  auto load_chunk = [&](int slot, int ch) {
+#pragma unroll
+    for (int i = 0; i < C::T1W; ++i) {
+      const int t = w * C::T1W + i, ct = t % (KC / 16);
+      const int n = ch * KC + ct * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) fb1[slot][i][ks] = gl16(a1t + (long)n * D + ks * 32 + fg * 8);
+      cb1[slot][i] = c1[n];
+    }
+#pragma unroll
+    for (int b = 0; b < C::C2; ++b)
+      fb2[slot][b] = gl16(w2 + (long)(w * (HD / NW) + b * 16 + fr) * (2 * HD) + ch * KC + fg * 8);
+  };
+  load_chunk(0, 0);
+  load_chunk(1, 1);
+
+  // ---------------- phase 0: x tile -> LDS; LN_pre stats -> z (bf16)
+  {
+    constexpr int CH = D / 8;
+    for (int c = tid; c < BM * CH; c += C::NT) {
+      const int r = c / CH, k = c % CH;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (t0 + r < T) v = gl16(x + (t0 + r) * D + k * 8);
+      *reinterpret_cast<uint4*>(smem + C::OFF_X + r * C::XS + k * 16) = v;
+    }
+  }
+  __syncthreads();
+  for (int r = w; r < BM; r += NW) {
+    const unsigned short* xr = (const unsigned short*)(smem + C::OFF_X + r * C::XS);
+    const float v = lane < D ? bf2f(xr[lane]) : 0.f;
+    const float v2 = (D > 64 && lane + 64 < D) ? bf2f(xr[lane + 64]) : 0.f;
+    const float mu = wave_sum(v + v2) / D;
+    const float d1 = lane < D ? v - mu : 0.f, d2 = (D > 64 && lane + 64 < D) ? v2 - mu : 0.f;
+    const float rs = rsqrtf(wave_sum(d1 * d1 + d2 * d2) / D + 1e-5f);
+    unsigned short* zr = (unsigned short*)(smem + C::OFF_Z + r * C::XS);
+    if (lane < D) zr[lane] = f2bf(d1 * rs);
+    if (D > 64 && lane + 64 < D) zr[lane + 64] = f2bf(d2 * rs);
+  }
+  __syncthreads();
+
+  // ---------------- phase 1: 2HD chunks
+  f32x4 acc2[C::R2][C::C2];
+#pragma unroll
+  for (int a = 0; a < C::R2; ++a)
+#pragma unroll
+    for (int b = 0; b < C::C2; ++b) acc2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    const int slot = ch & 1;
+    unsigned char* h1 = smem + C::OFF_H1 + slot * BM * C::H1S;
+    // GEMM1 + bias + GELU -> h1[slot]
+#pragma unroll
+    for (int i = 0; i < C::T1W; ++i) {
+      const int t = w * C::T1W + i, rt = t / (KC / 16), ct = t % (KC / 16);
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks)
+        acc = mfma(lds16(smem + C::OFF_Z + (rt * 16 + fr) * C::XS + ks * 64 + fg * 16), fb1[slot][i][ks], acc);
+      const float bias = cb1[slot][i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(unsigned short*)(h1 + (rt * 16 + fg * 4 + j) * C::H1S + (ct * 16 + fr) * 2) = f2bf(gelu_fast(acc[j] + bias));
+    }
+    __syncthreads();
+    // GEMM2: acc2 += h1[slot] . W2 chunk^T
+    uint4 fa[C::R2];
+#pragma unroll
+    for (int a = 0; a < C::R2; ++a) fa[a] = lds16(h1 + (a * 16 + fr) * C::H1S + fg * 16);
+#pragma unroll
+    for (int b = 0; b < C::C2; ++b)
+#pragma unroll
+      for (int a = 0; a < C::R2; ++a) acc2[a][b] = mfma(fa[a], fb2[slot][b], acc2[a][b]);
+    if (ch + 2 < C::NCH) load_chunk(slot, ch + 2);
+  }
+
+  // ---------------- phase 2: h2 = GELU(acc2 + b2) -> LDS
+#pragma unroll
+  for (int b = 0; b < C::C2; ++b) {
+    const int col = w * (HD / NW) + b * 16 + fr;
+    const float bias = b2[col];
+#pragma unroll
+    for (int a = 0; a < C::R2; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(unsigned short*)(smem + C::OFF_H2 + (a * 16 + fg * 4 + j) * C::H2S + col * 2) =
+            f2bf(gelu_fast(acc2[a][b][j] + bias));
+  }
+  __syncthreads();
+
+  // ---------------- phase 3: y = [x | h2] Wc  (wave owns RT3 row tiles x all D columns)
+  f32x4 acc3[C::RT3][C::CT3];
+#pragma unroll
+  for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+    for (int c = 0; c < C::CT3; ++c) acc3[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 fw[2][C::CT3];
+  auto load_wc = [&](int slot, int ks) {
+#pragma unroll
+    for (int c = 0; c < C::CT3; ++c) fw[slot][c] = gl16(wct + (long)(c * 16 + fr) * (D + HD) + ks * 32 + fg * 8);
+  };
+  load_wc(0, 0);
+  load_wc(1, 1);
+#pragma unroll
+  for (int ks = 0; ks < C::KS3; ++ks) {
+    const int slot = ks & 1;
+#pragma unroll
+    for (int r = 0; r < C::RT3; ++r) {
+      const int row = (w * C::RT3 + r) * 16 + fr;
+      const uint4 fa = ks < D / 32 ? lds16(smem + C::OFF_X + row * C::XS + ks * 64 + fg * 16)
+                                   : lds16(smem + C::OFF_H2 + row * C::H2S + (ks - D / 32) * 64 + fg * 16);
+#pragma unroll
+      for (int c = 0; c < C::CT3; ++c) acc3[r][c] = mfma(fa, fw[slot][c], acc3[r][c]);
+    }
+    if (ks + 2 < C::KS3) load_wc(slot, ks + 2);
+  }
+
+  // ---------------- phase 4: LN_post from the accumulators (row = 16 lanes x CT3 tiles)
+  float gp[C::CT3], bp[C::CT3];
+#pragma unroll
+  for (int c = 0; c < C::CT3; ++c) { gp[c] = g_post[c * 16 + fr]; bp[c] = b_post[c * 16 + fr]; }
+#pragma unroll
+  for (int r = 0; r < C::RT3; ++r) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < C::CT3; ++c) s += acc3[r][c][j];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+      const float mu = s / D;
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < C::CT3; ++c) { const float dd = acc3[r][c][j] - mu; q += dd * dd; }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+      const float rs = rsqrtf(q / D + 1e-5f);
+      const long row = t0 + (w * C::RT3 + r) * 16 + fg * 4 + j;
+      if (row < T) {
+#pragma unroll
+        for (int c = 0; c < C::CT3; ++c)
+          out[row * D + c * 16 + fr] = f2bf((acc3[r][c][j] - mu) * rs * gp[c] + bp[c]);
+      }
+    }
+  }
+}
+
+template <int D, int HD, int NW>
+int launch(const hv_mhc_fused_args* a, hipStream_t s) {
+  using C = Cfg<D, HD, NW>;
+  auto k = mhc_fused_kernel<D, HD, NW>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  k<<<hv_cdiv(a->T, C::BM), C::NT, C::LDS, s>>>(
+      (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
+      a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (unsigned short*)a->out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+}  // namespace
+
+extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype) {
+  if (dtype != HV_BF16) return 0;
+  return (D == 32 && Hd == 128) || (D == 64 && Hd == 256);
+}
+
+extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
+  if (!a || a->T <= 0) return HV_EINVAL;
+  if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype)) return HV_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->D == 32) return launch<32, 128, 4>(a, s);
+  return launch<64, 256, 8>(a, s);
+}

@@ -70,23 +70,61 @@ __global__ void __launch_bounds__(256) k_rmsnorm(const T* __restrict__ x, int ro
 
 // ---------------------------------------------------------------- mHC coefficient prep
 // gc[i,k] = g_i s(raw[i,k]) - mean_i(g_i s(raw[i,k])) ; u[k] = sum_i b_i s(raw[i,k])
-__global__ void __launch_bounds__(256) k_prep_pre(int D, int Hd, const float* __restrict__ raw,
-                                                  const float* gamma, const float* beta, float* gc,
-                                                  int gct, float* u) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+// Two passes over 64x64 tiles (grid = Hd/64 x D/64): column partial sums, then centre + write.
+constexpr int PT = 64;
+__global__ void __launch_bounds__(256) k_prep_pre_sum(int D, int Hd, const float* __restrict__ raw,
+                                                      const float* gamma, const float* beta,
+                                                      float* part /* [2][nrb][Hd] */) {
+  __shared__ float red[2][4][PT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * PT + lane, rb = blockIdx.y, nrb = gridDim.y;
+  float sg = 0.f, sb = 0.f;
+  if (k < Hd) {
+    for (int r = w; r < PT; r += 4) {
+      const int i = rb * PT + r;
+      if (i >= D) break;
+      const float s = 1.0f / (1.0f + expf(-raw[(long)i * Hd + k]));
+      sg += gamma[i] * s;
+      sb += beta[i] * s;
+    }
+  }
+  red[0][w][lane] = sg;
+  red[1][w][lane] = sb;
+  __syncthreads();
+  if (w == 0 && k < Hd) {
+    part[(long)rb * Hd + k] = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+    part[(long)(nrb + rb) * Hd + k] = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_prep_pre_write(int D, int Hd, const float* __restrict__ raw,
+                                                        const float* gamma, const float* part, float* gc,
+                                                        int gct, float* u) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * PT + lane, rb = blockIdx.y, nrb = gridDim.y;
   if (k >= Hd) return;
   float sg = 0.f, sb = 0.f;
-  for (int i = 0; i < D; ++i) {
-    const float s = 1.0f / (1.0f + expf(-raw[(long)i * Hd + k]));
-    sg += gamma[i] * s;
-    sb += beta[i] * s;
-  }
+  for (int r = 0; r < nrb; ++r) { sg += part[(long)r * Hd + k]; sb += part[(long)(nrb + r) * Hd + k]; }
   const float mean = sg / D;
-  u[k] = sb;
-  for (int i = 0; i < D; ++i) {
+  if (rb == 0 && w == 0) u[k] = sb;
+  for (int r = w; r < PT; r += 4) {
+    const int i = rb * PT + r;
+    if (i >= D) break;
     const float s = 1.0f / (1.0f + expf(-raw[(long)i * Hd + k]));
     gc[gct ? (long)k * D + i : (long)i * Hd + k] = gamma[i] * s - mean;
   }
+}
+
+// y[n] = sum_k W[n, k] x[k] + b[n]  (fp32 GEMV, one wave per output)
+__global__ void __launch_bounds__(256) k_gemv(const float* __restrict__ W, const float* __restrict__ x,
+                                              const float* b, int N, int K, float* y) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  const float* row = W + (long)n * K;
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += row[k] * x[k];
+  s = wave_sum(s);
+  if (lane == 0) y[n] = s + (b ? b[n] : 0.f);
 }
 
 // row means of H_res (rows 0..D-1) and H_post = 2 s(raw) (rows D..D+Hd-1); one wave per row
@@ -367,7 +405,10 @@ __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logit
                                                      int A, int nc, const float* anchor_wh,
                                                      float* pred, float* boxes, float* scores,
                                                      float* cscore, int64_t* cidx, float* obj) {
-  const long cell = (long)blockIdx.x * 256 + threadIdx.x;     // (b, a, y, x)
+  // one wave per cell (b, a, y, x): lanes cover the 5+nc logits, coalesced loads/stores,
+  // argmax by a wave reduction (first index wins ties, like a sequential scan)
+  const long cell = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const long total = (long)n * A * h * w;
   if (cell >= total) return;
   const int x = cell % w;
@@ -378,24 +419,36 @@ __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logit
   const int P = 5 + nc;
   const T* src = logits + (((long)b * h + y) * w + x) * (long)(A * P) + (long)a * P;
   float* pr = pred + cell * P;
-  for (int k = 0; k < P; ++k) pr[k] = Elem<T>::load(src, k);
-  const float sx = 1.0f / (1.0f + expf(-pr[0])), sy = 1.0f / (1.0f + expf(-pr[1]));
-  const float bx = ((float)x + sx) / (float)w, by = ((float)y + sy) / (float)h;
-  const float bw = anchor_wh[2 * a] * expf(pr[2]), bh = anchor_wh[2 * a + 1] * expf(pr[3]);
-  float* bo = boxes + cell * 4;
-  bo[0] = bx - bw / 2; bo[1] = by - bh / 2; bo[2] = bx + bw / 2; bo[3] = by + bh / 2;
-  const float o = 1.0f / (1.0f + expf(-pr[4]));
-  obj[cell] = o;
+  const float o = 1.0f / (1.0f + expf(-Elem<T>::load(src, 4)));
   float best = -1.f;
-  int bi = 0;
-  float* sc = scores + cell * nc;
-  for (int k = 0; k < nc; ++k) {
-    const float s = o * (1.0f / (1.0f + expf(-pr[5 + k])));
-    sc[k] = s;
-    if (s > best) { best = s; bi = k; }
+  int bi = 0x7fffffff;
+  for (int k = lane; k < P; k += 64) {
+    const float v = Elem<T>::load(src, k);
+    pr[k] = v;
+    if (k >= 5) {
+      const float s = o * (1.0f / (1.0f + expf(-v)));
+      scores[cell * nc + (k - 5)] = s;
+      if (s > best) { best = s; bi = k - 5; }
+    }
   }
-  cscore[cell] = best;
-  cidx[cell] = bi;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ob = __shfl_xor(best, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) {
+    const float v0 = Elem<T>::load(src, 0), v1 = Elem<T>::load(src, 1);
+    const float v2 = Elem<T>::load(src, 2), v3 = Elem<T>::load(src, 3);
+    const float sx = 1.0f / (1.0f + expf(-v0)), sy = 1.0f / (1.0f + expf(-v1));
+    const float bx = ((float)x + sx) / (float)w, by = ((float)y + sy) / (float)h;
+    const float bw = anchor_wh[2 * a] * expf(v2), bh = anchor_wh[2 * a + 1] * expf(v3);
+    float* bo = boxes + cell * 4;
+    bo[0] = bx - bw / 2; bo[1] = by - bh / 2; bo[2] = bx + bw / 2; bo[3] = by + bh / 2;
+    obj[cell] = o;
+    cscore[cell] = best;
+    cidx[cell] = bi;
+  }
 }
 
 }  // namespace
@@ -444,7 +497,12 @@ extern "C" int hv_mhc_prep(int D, int Hd, const float* h_pre_raw, const float* h
                            float* gc, int gct, float* u, float* wct, float* rm, hv_stream_t stream) {
   if (D <= 0 || Hd <= 0) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  k_prep_pre<<<hv_cdiv(Hd, 256), 256, 0, s>>>(D, Hd, h_pre_raw, gamma_pre, beta_pre, gc, gct, u);
+  const dim3 g(hv_cdiv(Hd, PT), hv_cdiv(D, PT));
+  // column partials live in the tail of `wct` (written last, after its own pass)
+  float* part = wct + (long)D * (D + Hd) - 2L * g.y * Hd;
+  if (2L * g.y * Hd > (long)D * (D + Hd)) return HV_EUNSUPPORTED;
+  k_prep_pre_sum<<<g, 256, 0, s>>>(D, Hd, h_pre_raw, gamma_pre, beta_pre, part);
+  k_prep_pre_write<<<g, 256, 0, s>>>(D, Hd, h_pre_raw, gamma_pre, part, gc, gct, u);
   k_prep_rowmean<<<hv_cdiv(D + Hd, 4), 256, 0, s>>>(D, Hd, h_res, h_post_raw, rm);
   k_prep_wct<<<dim3(hv_cdiv(D + Hd, 32), hv_cdiv(D, 32)), 256, 0, s>>>(D, Hd, h_res, h_post_raw, rm, wct);
   HV_CHECK_LAUNCH();
@@ -585,7 +643,7 @@ extern "C" int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w
                               float* objectness, hv_stream_t stream) {
   const long total = (long)n * A * h * w;
   if (total <= 0 || nc <= 0) return HV_EINVAL;
-  HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+  HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 4), 256, 0, (hipStream_t)stream>>>(
                           (const T*)logits, n, h, w, A, nc, anchor_wh, predictions, boxes, scores,
                           class_scores, class_indices, objectness)));
   HV_CHECK_LAUNCH();
@@ -641,6 +699,14 @@ extern "C" int hv_bn_fold(int c, const float* gamma, const float* beta, const fl
   if (c <= 0) return HV_EINVAL;
   k_bn_fold<<<hv_cdiv(c, 256), 256, 0, (hipStream_t)stream>>>(c, gamma, beta, mean, var, conv_bias,
                                                                eps, scale_out, bias_out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_gemv(const float* W, const float* x, const float* b, int N, int K, float* y,
+                       hv_stream_t stream) {
+  if (N <= 0 || K <= 0) return HV_EINVAL;
+  k_gemv<<<hv_cdiv(N, 4), 256, 0, (hipStream_t)stream>>>(W, x, b, N, K, y);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -47,17 +47,27 @@ class GemmDesc(C.Structure):
                 ("conv_oh", i32), ("conv_ow", i32)]
 
 
+class MhcFusedArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("D", i32), ("Hd", i32), ("T", i32),
+                ("x", vp), ("a1t", vp), ("c1", vp), ("w2", vp), ("b2", vp), ("wct", vp),
+                ("g_post", vp), ("b_post", vp), ("out", vp)]
+
+
 _SIGS = {
+    "hv_mhc_fused_supported": ([i32, i32, i32], i32),
+    "hv_mhc_fused": ([vp, vp], i32),
     "hv_abi_version": ([], i32),
     "hv_struct_sizes": ([vp], None),
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_forward": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "hv_gemm": ([vp, vp], i32),
+    "hv_gemm_set_path": ([i32], None),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),
     "hv_layernorm": ([i32, vp, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp], i32),
     "hv_rmsnorm": ([i32, vp, i32, i32, f32, vp, vp, vp], i32),
     "hv_mhc_prep": ([i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp], i32),
     "hv_cast": ([vp, i64, i32, vp, vp], i32),
+    "hv_gemv": ([vp, vp, vp, i32, i32, vp, vp], i32),
     "hv_conv_weight_prep": ([vp, i32, i32, i32, vp, i32, vp, vp], i32),
     "hv_bn_fold": ([i32, vp, vp, vp, vp, vp, f32, vp, vp, vp], i32),
     "hv_nchw_to_nhwc": ([vp, i32, i32, i32, i32, i32, vp, vp], i32),

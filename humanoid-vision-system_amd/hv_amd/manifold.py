@@ -72,6 +72,7 @@ class SinkhornKnoppProjection(nn.Module):
 
 # ================================================================== mHC plan
 FOLD_MAX_D = 1024   # fold H_pre into W1 for every site but the D=1792 final fusion
+USE_FUSED = True    # one-launch kernel for the small-D sites (hv_mhc_fused); False = unfused chain
 
 
 @dataclass
@@ -101,7 +102,7 @@ def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.d
     if fold:
         # A1^T = W1 Gc^T  [2Hd, D];  c1 = W1 u + b1
         a1t = ops.gemm(ops.cast(w1, dtype), ops.cast(gc, dtype), out_dtype=dtype)
-        c1 = ops.gemm(u.view(1, Hd), w1, bias=b1, out_dtype=torch.float32).view(-1)
+        c1 = ops.gemv(w1, u, b1)
         first, second, w1c, b1c = a1t, c1, None, None
     else:
         first, second, w1c, b1c = ops.cast(gc, dtype), u, ops.cast(w1, dtype), b1
@@ -113,6 +114,9 @@ def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.d
 
 def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token chain on x2 [T, D] (compute dtype).  Returns LN_post(...) (+ residual) [T, D]."""
+    if (USE_FUSED and p.fold and residual is None and x2.is_contiguous()
+            and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)):
+        return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post)
     mean, rstd = ops.row_stats(x2, 1e-5)
     if p.fold:
         h1 = ops.gemm(x2, p.b1, bias=p.c1, act="gelu", a_mean=mean, a_rstd=rstd)

@@ -156,6 +156,37 @@ def f32(t: Optional[Tensor]) -> Optional[Tensor]:
     return None if t is None else t.detach().float().contiguous()
 
 
+def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype) -> bool:
+    return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype)))
+
+
+def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post) -> Tensor:
+    """One-launch mHC token chain (bf16) for x [T, D]; see hv_mhc_fused in hv_kernels.h."""
+    _contig(x, "x")
+    T, D = x.shape
+    Hd = w2.shape[0]
+    if a1t.shape != (2 * Hd, D) or w2.shape != (Hd, 2 * Hd) or wct.shape != (D, D + Hd):
+        raise ValueError("mhc_fused: coefficient shapes do not match x")
+    for t in (a1t, w2, wct):
+        _contig(t, "coefficient")
+    out = torch.empty_like(x)
+    a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
+                       b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), out.data_ptr())
+    check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
+    return out
+
+
+def gemv(w: Tensor, x: Tensor, b: Optional[Tensor] = None) -> Tensor:
+    """fp32 y = w @ x + b for w [N, K], x [K]."""
+    w, x, b = f32(w), f32(x), f32(b)
+    N, K = w.shape
+    if x.numel() != K or (b is not None and b.numel() != N):
+        raise ValueError("gemv shape mismatch")
+    y = torch.empty(N, device=w.device, dtype=torch.float32)
+    check(L.lib().hv_gemv(w.data_ptr(), x.data_ptr(), ptr(b), N, K, y.data_ptr(), stream_ptr()), "hv_gemv")
+    return y
+
+
 # ---------------------------------------------------------------------------- norms
 def row_stats(x: Tensor, eps: float = 1e-5):
     _cuda(x)

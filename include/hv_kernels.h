@@ -93,6 +93,8 @@ typedef struct hv_gemm_desc {
 } hv_gemm_desc;
 
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
+/* path selection for A/B tests: 1 = register-staged kernel only, 0 = default (LDS-DMA when eligible) */
+void hv_gemm_set_path(int regstage_only);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
@@ -128,6 +130,30 @@ int hv_conv_weight_prep(const float* w, int cout, int cin, int k, const float* s
 int hv_bn_fold(int c, const float* gamma, const float* beta, const float* mean, const float* var,
                const float* conv_bias, float eps, float* scale_out, float* bias_out,
                hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Fused mHC token chain (ManifoldHyperConnection.forward, manifold_layers.py:223-280) for
+ * the small-D backbone sites: LN_pre, folded GEMM1 + GELU, GEMM2 + GELU, [x|h2] Wc, LN_post
+ * in one launch, intermediates on chip.  bf16 only; (D, Hd) in {(32,128), (64,256)}.
+ * Operands are the folded coefficients of hv_mhc_prep + the fold GEMM.
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_mhc_fused_args {
+  int dtype, D, Hd, T;
+  const void* x;        /* [T, D] */
+  const void* a1t;      /* [2Hd, D]  = W1 Gc^T */
+  const float* c1;      /* [2Hd]     = W1 u + b1 */
+  const void* w2;       /* [Hd, 2Hd] */
+  const float* b2;      /* [Hd] */
+  const void* wct;      /* [D, D+Hd] centred [H_res ; H_post]^T */
+  const float* g_post;  /* [D] */
+  const float* b_post;  /* [D] */
+  void* out;            /* [T, D] */
+} hv_mhc_fused_args;
+int hv_mhc_fused_supported(int D, int Hd, int dtype);
+int hv_mhc_fused(const hv_mhc_fused_args* args, hv_stream_t stream);
+
+/* y[N] = W[N, K] x[K] + b  (fp32; folded mHC bias c1 = W1 u + b1) */
+int hv_gemv(const float* W, const float* x, const float* b, int N, int K, float* y, hv_stream_t stream);
 
 /* elementwise cast fp32 -> (fp32|bf16) */
 int hv_cast(const float* x, long n, int y_dtype, void* y, hv_stream_t stream);

@@ -130,6 +130,37 @@ def test_gemm_residual_mod(gpu_device):
     assert rel_err(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,conv", [(4096, 512, 1024, False), (333, 1000, 576, False),
+                                         (2 * 40 * 40, 256, 9 * 64, True), (2 * 20 * 20, 96, 9 * 128, True)])
+def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
+    """The global_load_lds kernel (K % 64 == 0, bf16) against the register-staged kernel."""
+    ops = _ops()
+    from hv_amd import _lib
+    g = torch.Generator().manual_seed(M + N)
+    if conv:
+        c = K // 9
+        hw = int(round((M // 2) ** 0.5))
+        x = torch.randn(2, hw, hw, c, generator=g).to(torch.bfloat16).to(gpu_device)
+        w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(gpu_device)
+        run = lambda: ops.conv2d(x, w, 3, 1, 1, out_dtype=torch.float32)  # noqa: E731
+        ref = F.conv2d(x.float().cpu().permute(0, 3, 1, 2), w.float().cpu().view(N, 3, 3, c).permute(0, 3, 1, 2),
+                       None, 1, 1).permute(0, 2, 3, 1)
+    else:
+        a = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu_device)
+        b = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(gpu_device)
+        bias = torch.randn(N, generator=g).to(gpu_device)
+        run = lambda: ops.gemm(a, b, bias=bias, act="relu", out_dtype=torch.float32)  # noqa: E731
+        ref = F.relu(a.float().cpu() @ b.float().cpu().T + bias.cpu())
+    fast = run()
+    _lib.lib().hv_gemm_set_path(1)
+    try:
+        slow = run()
+    finally:
+        _lib.lib().hv_gemm_set_path(0)
+    assert rel_err(fast, slow) < 1e-5
+    assert rel_err(fast, ref) < 1e-4
+
+
 CONV_CASES = [(3, 32, 3, 2, 1, 33), (32, 32, 3, 1, 1, 20), (32, 64, 3, 2, 1, 17), (64, 32, 1, 1, 0, 9),
               (128, 96, 3, 1, 1, 7), (16, 8, 3, 1, 1, 5)]
 

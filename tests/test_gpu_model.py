@@ -57,6 +57,26 @@ def test_mhc_bf16_agreement(gpu_device, D, e):
     assert rel_l2(y, g["y64"]) < 5e-2
 
 
+@pytest.mark.parametrize("D,T", [(32, 64), (32, 1000), (64, 64), (64, 777)])
+def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, T):
+    """hv_mhc_fused (one launch, on-chip intermediates) vs the six-launch chain, both bf16."""
+    from hv_amd import ManifoldHyperConnection
+    from hv_amd import manifold as MF
+    m = ManifoldHyperConnection(D, expansion_rate=4, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    x = torch.randn(T, D, generator=torch.Generator().manual_seed(T)).to(gpu_device)
+    MF.USE_FUSED = True
+    y1 = m(x).float().cpu().numpy()
+    MF.USE_FUSED = False
+    try:
+        y0 = m(x).float().cpu().numpy()
+    finally:
+        MF.USE_FUSED = True
+    assert rel_l2(y1, y0) < 1e-2
+    assert np.abs(y1 - y0).max() < 0.1
+
+
 def test_convmhc_and_blocks_fp32(gpu_device):
     from hv_amd import ConvMHCLayer, ResidualMHCLayer, TransformerEncoderBlock
     for (cin, cout, k, s, HW) in [(3, 32, 3, 2, 32), (64, 64, 3, 1, 16), (64, 128, 3, 2, 16)]:
