@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="time host-launched steps instead of HIP-graph replays")
     return ap.parse_args()
 
 
@@ -130,15 +132,25 @@ def main():
     x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=None)
 
     with torch.no_grad():
-        for _ in range(a.warmup):
+        for _ in range(2):
             model(x)
+        # eager reference timing (host-launched kernels), reported beside the graph number
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(3):
+            model(x)
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - te) / 3 * 1e3
+        step = model.capture(x).replay if a.graph else (lambda: model(x))
+        for _ in range(a.warmup):
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            model(x)
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -155,21 +167,30 @@ def main():
 
     lat = None
     if rank == 0 and not a.no_latency:
-        x1 = x[:1].contiguous()
-        model.freeze()
-        ts = []
-        with torch.no_grad():
-            for i in range(25):
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                model(x1)
-                torch.cuda.synchronize()
-                if i >= 5:
-                    ts.append((time.perf_counter() - t1) * 1e3)
+        # streaming config E: single 640x640 frame, hipGraph-captured forward; the frame is copied
+        # into the graph's input buffer inside the timed interval
+        lat = {}
+        frames = torch.randn(8, 1, 3, a.size, a.size, device=dev)
+        for mode in ("recompute", "frozen"):
+            model.freeze(mode == "frozen")
+            with torch.no_grad():
+                runner = model.capture(frames[0])
+                ts = []
+                for i in range(60):
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    runner(frames[i % 8])
+                    torch.cuda.synchronize()
+                    if i >= 10:
+                        ts.append((time.perf_counter() - t1) * 1e3)
+            del runner
+            ts.sort()
+            lat[mode] = {"p50_ms": round(ts[len(ts) // 2], 3), "p95_ms": round(ts[int(len(ts) * 0.95) - 1], 3),
+                         "p99_ms": round(ts[-1], 3)}
         model.freeze(False)
-        ts.sort()
-        lat = {"p50_ms": round(ts[len(ts) // 2], 3), "p95_ms": round(ts[int(len(ts) * 0.95) - 1], 3),
-               "batch": 1, "mode": "eager, coefficients frozen (eval cache)"}
+        lat["batch"] = 1
+        lat["note"] = ("hipGraph replay; 'recompute' re-runs Sinkhorn + coefficient prep per frame like the "
+                       "reference, 'frozen' reuses them until a parameter changes (eval streaming)")
 
     imgs = world * a.batch * a.steps
     value = imgs / elapsed
@@ -190,6 +211,9 @@ def main():
                          "launches_per_step": n_l, "avg_launch_ms": round(avg_ms, 4),
                          "avg_flop_per_launch": avg_flop},
             "model_tflops_reference_graph": round(GFLOP_PER_IMG_640 * value / 1e3, 2) if a.size == 640 else None,
+            "step_mode": "hipGraph replay of the full forward (Sinkhorn + coefficient prep recomputed every step)"
+                         if a.graph else "eager",
+            "eager_ms_per_step": round(eager_ms, 3),
             "latency": lat,
             "cpu_baseline": base,
         }

@@ -1,11 +1,11 @@
-// Fused mHC token chain for small D (gfx950, bf16 MFMA), replacing the six launches of the
-// unfused path (row stats, 3 GEMMs, LayerNorm) for the backbone's high-token-count sites:
+// Fused mHC token chain (gfx950, bf16 MFMA), replacing the six launches of the unfused path
+// (row stats, 3 GEMMs, LayerNorm) for every site with D <= 256 and hidden width <= 512:
 //
 //   z   = (x - mean) * rstd                    (LN_pre core; gamma/beta folded into A1/c1)
 //   h1  = GELU(z A1 + c1)          [BM x 2HD]  produced KC columns at a time, never stored
 //   h2  = GELU(h1 W2^T + b2)       [BM x HD]   accumulated in registers over the 2HD chunks
 //   y   = [x | h2] Wc              [BM x D]    Wc = centred [H_res ; H_post]
-//   out = LN_post(y) * g2 + b2'                computed from the GEMM3 accumulators in registers
+//   out = LN_post(y) * g2 + b2' (+ residual)   computed from the GEMM3 accumulators
 //
 // Reference: ManifoldHyperConnection.forward (manifold_layers.py:223-280); the algebra
 // (fold + centring) is documented in hv_amd/manifold.py and DESIGN.md.  Per token tile only x
@@ -14,9 +14,9 @@
 //
 // Weights are not staged through LDS: every weight element a workgroup needs is consumed by
 // exactly one lane as an MFMA B fragment, so each lane loads its 16-byte fragments straight
-// from L2 into a 2-chunk-deep register ring (loads for chunk c+2 are issued while chunk c
-// computes).  LDS holds only the x/z tile, a double-buffered h1 chunk (one barrier per
-// chunk) and h2.  GELU uses an erf with |err| <= 1.5e-7 (A&S 7.1.26), far below bf16 rounding.
+// from L2 into a 2-slot register ring (chunk c+1 is in flight while chunk c computes).  LDS
+// holds the x/z tile, a double-buffered h1 chunk (one barrier per chunk), h2 and a small
+// LayerNorm exchange.  GELU uses an erf with |err| <= 1.5e-7 (A&S 7.1.26), far below bf16.
 #include "hv_common.h"
 
 namespace {
@@ -27,24 +27,29 @@ struct Cfg {
   static constexpr int BM = 4096 * NW / HD;       // acc2: BM x HD/NW per wave = 16 tiles (64 regs)
   static constexpr int KC = 32;                   // 2HD chunk per step (one MFMA k-step)
   static constexpr int NCH = 2 * HD / KC;
+  static constexpr int NV = (D + 63) / 64;        // row values per lane in row-wise passes
   static constexpr int XS = D * 2 + 16;           // x / z row stride (bytes), == 16 mod 64
   static constexpr int H1S = KC * 2 + 16;
   static constexpr int H2S = HD * 2 + 16;
+  // GEMM1: (BM/16) x (KC/16) tiles over NW waves
+  static constexpr int T1W = (BM / 16) * (KC / 16) / NW;
+  // GEMM2: wave owns HD/NW columns x all BM rows
+  static constexpr int R2 = BM / 16, C2 = HD / NW / 16;
+  // GEMM3: (BM/16) row tiles x (D/16) col tiles; CG column groups per row tile
+  static constexpr int CG = NW > BM / 16 ? NW / (BM / 16) : 1;
+  static constexpr int RT3 = (BM / 16) * CG / NW;
+  static constexpr int CT3 = (D / 16) / CG;
+  static constexpr int KS3 = (D + HD) / 32;
+  // LDS carve
   static constexpr int OFF_X = 0;
   static constexpr int OFF_Z = BM * XS;
   static constexpr int OFF_H1 = 2 * BM * XS;      // 2 buffers
   static constexpr int OFF_H2 = OFF_H1 + 2 * BM * H1S;
-  static constexpr int LDS = OFF_H2 + BM * H2S;
-  // tiling
-  static constexpr int T1W = (BM / 16) * (KC / 16) / NW;   // GEMM1 tiles per wave
-  static constexpr int C2 = HD / NW / 16;                  // GEMM2 column tiles per wave
-  static constexpr int R2 = BM / 16;                       // GEMM2 row tiles
-  static constexpr int RT3 = (BM / 16) / NW;               // GEMM3 row tiles per wave
-  static constexpr int CT3 = D / 16;                       // GEMM3 column tiles
-  static constexpr int KS3 = (D + HD) / 32;                // GEMM3 k-steps
+  static constexpr int OFF_RED = OFF_H2 + BM * H2S;   // [BM][CG] floats
+  static constexpr int LDS = OFF_RED + BM * CG * 4;
   static_assert(R2 * C2 == 16, "acc2 tiling");
   static_assert(T1W >= 1 && (BM / 16) * (KC / 16) % NW == 0, "gemm1 tiling");
-  static_assert(RT3 >= 1, "gemm3 tiling");
+  static_assert(RT3 >= 1 && CT3 >= 1 && (D / 16) % CG == 0, "gemm3 tiling");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -74,6 +79,7 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
     const float* __restrict__ b2,             // [HD]
     const unsigned short* __restrict__ wct,   // [D, D+HD]
     const float* __restrict__ g_post, const float* __restrict__ b_post,
+    const unsigned short* __restrict__ res,   // optional [T, D], added after LN_post
     unsigned short* __restrict__ out) {
   using C = Cfg<D, HD, NW>;
   constexpr int BM = C::BM, KC = C::KC;
@@ -82,7 +88,7 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   const int fr = lane & 15, fg = lane >> 4;
   const long t0 = (long)blockIdx.x * BM;
 
-  // ---------------- weight-fragment ring (registers), 2 chunks deep
+  // ---------------- weight-fragment ring (registers), 2 slots
   uint4 fb1[2][C::T1W][D / 32];      // GEMM1 B fragments (rows of A1^T)
   uint4 fb2[2][C::C2];               // GEMM2 B fragments (rows of W2)
   float cb1[2][C::T1W];              // c1 bias per GEMM1 tile column
@@ -102,7 +108,7 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   load_chunk(0, 0);
   load_chunk(1, 1);
 
-  // ---------------- phase 0: x tile -> LDS; LN_pre stats -> z (bf16)
+  // ---------------- phase 0: x tile -> LDS; LN_pre -> z (bf16)
   {
     constexpr int CH = D / 8;
     for (int c = tid; c < BM * CH; c += C::NT) {
@@ -115,14 +121,29 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   __syncthreads();
   for (int r = w; r < BM; r += NW) {
     const unsigned short* xr = (const unsigned short*)(smem + C::OFF_X + r * C::XS);
-    const float v = lane < D ? bf2f(xr[lane]) : 0.f;
-    const float v2 = (D > 64 && lane + 64 < D) ? bf2f(xr[lane + 64]) : 0.f;
-    const float mu = wave_sum(v + v2) / D;
-    const float d1 = lane < D ? v - mu : 0.f, d2 = (D > 64 && lane + 64 < D) ? v2 - mu : 0.f;
-    const float rs = rsqrtf(wave_sum(d1 * d1 + d2 * d2) / D + 1e-5f);
+    float v[C::NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      const int j = lane + 64 * i;
+      v[i] = j < D ? bf2f(xr[j]) : 0.f;
+      s += v[i];
+    }
+    const float mu = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      const int j = lane + 64 * i;
+      v[i] = j < D ? v[i] - mu : 0.f;
+      q += v[i] * v[i];
+    }
+    const float rs = rsqrtf(wave_sum(q) / D + 1e-5f);
     unsigned short* zr = (unsigned short*)(smem + C::OFF_Z + r * C::XS);
-    if (lane < D) zr[lane] = f2bf(d1 * rs);
-    if (D > 64 && lane + 64 < D) zr[lane + 64] = f2bf(d2 * rs);
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      const int j = lane + 64 * i;
+      if (j < D) zr[j] = f2bf(v[i] * rs);
+    }
   }
   __syncthreads();
 
@@ -137,7 +158,6 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   for (int ch = 0; ch < C::NCH; ++ch) {
     const int slot = ch & 1;
     unsigned char* h1 = smem + C::OFF_H1 + slot * BM * C::H1S;
-    // GEMM1 + bias + GELU -> h1[slot]
 #pragma unroll
     for (int i = 0; i < C::T1W; ++i) {
       const int t = w * C::T1W + i, rt = t / (KC / 16), ct = t % (KC / 16);
@@ -151,7 +171,6 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
         *(unsigned short*)(h1 + (rt * 16 + fg * 4 + j) * C::H1S + (ct * 16 + fr) * 2) = f2bf(gelu_fast(acc[j] + bias));
     }
     __syncthreads();
-    // GEMM2: acc2 += h1[slot] . W2 chunk^T
     uint4 fa[C::R2];
 #pragma unroll
     for (int a = 0; a < C::R2; ++a) fa[a] = lds16(h1 + (a * 16 + fr) * C::H1S + fg * 16);
@@ -176,7 +195,8 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   }
   __syncthreads();
 
-  // ---------------- phase 3: y = [x | h2] Wc  (wave owns RT3 row tiles x all D columns)
+  // ---------------- phase 3: y = [x | h2] Wc ; wave = (row-tile group, column group)
+  const int rg = w / C::CG, cg = w % C::CG;
   f32x4 acc3[C::RT3][C::CT3];
 #pragma unroll
   for (int r = 0; r < C::RT3; ++r)
@@ -185,7 +205,8 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   uint4 fw[2][C::CT3];
   auto load_wc = [&](int slot, int ks) {
 #pragma unroll
-    for (int c = 0; c < C::CT3; ++c) fw[slot][c] = gl16(wct + (long)(c * 16 + fr) * (D + HD) + ks * 32 + fg * 8);
+    for (int c = 0; c < C::CT3; ++c)
+      fw[slot][c] = gl16(wct + (long)((cg * C::CT3 + c) * 16 + fr) * (D + HD) + ks * 32 + fg * 8);
   };
   load_wc(0, 0);
   load_wc(1, 1);
@@ -194,7 +215,7 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
     const int slot = ks & 1;
 #pragma unroll
     for (int r = 0; r < C::RT3; ++r) {
-      const int row = (w * C::RT3 + r) * 16 + fr;
+      const int row = (rg * C::RT3 + r) * 16 + fr;
       const uint4 fa = ks < D / 32 ? lds16(smem + C::OFF_X + row * C::XS + ks * 64 + fg * 16)
                                    : lds16(smem + C::OFF_H2 + row * C::H2S + (ks - D / 32) * 64 + fg * 16);
 #pragma unroll
@@ -203,12 +224,12 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
     if (ks + 2 < C::KS3) load_wc(slot, ks + 2);
   }
 
-  // ---------------- phase 4: LN_post from the accumulators (row = 16 lanes x CT3 tiles)
-  float gp[C::CT3], bp[C::CT3];
+  // ---------------- phase 4: LN_post from the accumulators
+  // row (r, j) of this wave = 16 lanes (same fg) x CT3 tiles, x CG waves when CG > 1
+  float* red = (float*)(smem + C::OFF_RED);
+  float mu[C::RT3][4], rs[C::RT3][4];
 #pragma unroll
-  for (int c = 0; c < C::CT3; ++c) { gp[c] = g_post[c * 16 + fr]; bp[c] = b_post[c * 16 + fr]; }
-#pragma unroll
-  for (int r = 0; r < C::RT3; ++r) {
+  for (int r = 0; r < C::RT3; ++r)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float s = 0.f;
@@ -216,21 +237,77 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
       for (int c = 0; c < C::CT3; ++c) s += acc3[r][c][j];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-      const float mu = s / D;
+      mu[r][j] = s;
+    }
+  if constexpr (C::CG > 1) {
+#pragma unroll
+    for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (fr == 0) red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + cg] = mu[r][j];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < C::CG; ++g) s += red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + g];
+        mu[r][j] = s;
+      }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mu[r][j] *= 1.0f / D;
       float q = 0.f;
 #pragma unroll
-      for (int c = 0; c < C::CT3; ++c) { const float dd = acc3[r][c][j] - mu; q += dd * dd; }
+      for (int c = 0; c < C::CT3; ++c) { const float dd = acc3[r][c][j] - mu[r][j]; q += dd * dd; }
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
-      const float rs = rsqrtf(q / D + 1e-5f);
-      const long row = t0 + (w * C::RT3 + r) * 16 + fg * 4 + j;
+      rs[r][j] = q;
+    }
+  if constexpr (C::CG > 1) {
+#pragma unroll
+    for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (fr == 0) red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + cg] = rs[r][j];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < C::CG; ++g) s += red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + g];
+        rs[r][j] = s;
+      }
+  }
+  float gp[C::CT3], bp[C::CT3];
+#pragma unroll
+  for (int c = 0; c < C::CT3; ++c) {
+    gp[c] = g_post[(cg * C::CT3 + c) * 16 + fr];
+    bp[c] = b_post[(cg * C::CT3 + c) * 16 + fr];
+  }
+#pragma unroll
+  for (int r = 0; r < C::RT3; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float inv = rsqrtf(rs[r][j] * (1.0f / D) + 1e-5f);
+      const long row = t0 + (rg * C::RT3 + r) * 16 + fg * 4 + j;
       if (row < T) {
 #pragma unroll
-        for (int c = 0; c < C::CT3; ++c)
-          out[row * D + c * 16 + fr] = f2bf((acc3[r][c][j] - mu) * rs * gp[c] + bp[c]);
+        for (int c = 0; c < C::CT3; ++c) {
+          const int col = (cg * C::CT3 + c) * 16 + fr;
+          float v = (acc3[r][c][j] - mu[r][j]) * inv * gp[c] + bp[c];
+          if (res) v += bf2f(res[row * D + col]);
+          out[row * D + col] = f2bf(v);
+        }
       }
     }
-  }
 }
 
 template <int D, int HD, int NW>
@@ -244,22 +321,31 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
   }
   k<<<hv_cdiv(a->T, C::BM), C::NT, C::LDS, s>>>(
       (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
-      a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (unsigned short*)a->out);
+      a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
+      (unsigned short*)a->out);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
+
+int g_fused_wide = 0;
 
 }  // namespace
 
 extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype) {
   if (dtype != HV_BF16) return 0;
-  return (D == 32 && Hd == 128) || (D == 64 && Hd == 256);
+  // (256, 512) is instantiated but not dispatched by default: at D = 256 the per-tile weight
+  // re-stream (1.9 MB per 64 tokens) makes it slower than the unfused GEMM chain.
+  return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
+         (D == 256 && Hd == 512 && g_fused_wide);
 }
+extern "C" void hv_mhc_fused_enable_wide(int on) { g_fused_wide = on; }
 
 extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   if (!a || a->T <= 0) return HV_EINVAL;
   if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype)) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (a->D == 32) return launch<32, 128, 4>(a, s);
-  return launch<64, 256, 8>(a, s);
+  if (a->D == 64) return launch<64, 256, 8>(a, s);
+  if (a->D == 128) return launch<128, 512, 8>(a, s);
+  return launch<256, 512, 8>(a, s);
 }

@@ -50,12 +50,13 @@ class GemmDesc(C.Structure):
 class MhcFusedArgs(C.Structure):
     _fields_ = [("dtype", i32), ("D", i32), ("Hd", i32), ("T", i32),
                 ("x", vp), ("a1t", vp), ("c1", vp), ("w2", vp), ("b2", vp), ("wct", vp),
-                ("g_post", vp), ("b_post", vp), ("out", vp)]
+                ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp)]
 
 
 _SIGS = {
     "hv_mhc_fused_supported": ([i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
+    "hv_mhc_fused_enable_wide": ([i32], None),
     "hv_abi_version": ([], i32),
     "hv_struct_sizes": ([vp], None),
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),

@@ -264,6 +264,36 @@ class YOLODetectionHead(nn.Module):
         return inter / (a1 + a2 - inter + 1e-6)
 
 
+# ====================================================================== graphs
+class GraphRunner:
+    """One HybridVisionSystem forward captured as a HIP graph (torch.cuda.CUDAGraph over the
+    HIP runtime).  Every kernel of the step -- grouped Sinkhorn, coefficient folds, the token
+    path, decode -- is recorded once and replayed with no host launch overhead."""
+
+    def __init__(self, model: "HybridVisionSystem", example: torch.Tensor, task: str = "detection"):
+        require_cuda(example, "GraphRunner")
+        self.model = model
+        self.static_in = example.detach().clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):                   # allocate workspaces, upload tables, set attributes
+                model(self.static_in, task=task)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_out = model(self.static_in, task=task)
+
+    def replay(self) -> Dict[str, Any]:
+        self.graph.replay()
+        return self.static_out
+
+    def __call__(self, x: torch.Tensor) -> Dict[str, Any]:
+        self.static_in.copy_(x)
+        return self.replay()
+
+
 # ====================================================================== system
 class HybridVisionSystem(nn.Module):
     """hybrid_vision.py:17-485.  Accepts the real constructor ``(config)`` and the call-site
@@ -316,6 +346,7 @@ class HybridVisionSystem(nn.Module):
                     nn.init.zeros_(m.bias)
         self._mhc_modules = [m for m in self.modules() if isinstance(m, ManifoldHyperConnection)]
         self._frozen: Optional[Tuple[Any, RunCtx]] = None
+        self._sk_cache: Dict[str, Any] = {}
 
     # ---- precision / caching controls
     def set_precision(self, precision: str) -> "HybridVisionSystem":
@@ -333,8 +364,13 @@ class HybridVisionSystem(nn.Module):
 
     def _make_ctx(self) -> RunCtx:
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
-        prepare_plans(self._mhc_modules, ctx)
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache)
         return ctx
+
+    def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":
+        """Capture one full forward (coefficient prep included unless frozen) into a HIP
+        graph; the returned runner copies its input into the captured buffer and replays."""
+        return GraphRunner(self, example, task)
 
     def _ctx(self) -> RunCtx:
         if self._frozen is None:

@@ -1,0 +1,289 @@
+"""Inference engine with the reference API (src/inference/engine.py:33-671), MI355X edition.
+
+Same public surface -- InferenceConfig fields, InferenceEngine(config, model=None) (and the
+call-site form InferenceEngine(model=..., config=..., device=...) of scripts/inference.py:427),
+infer / inference / infer_batch / async_infer / get_performance_stats / get_stability_report /
+reset_stats, AsyncInferenceEngine.infer_async / infer_sync -- with these differences:
+  * the model forward runs on the HIP kernels of hv_amd (bf16 activations, fp32
+    coefficients) instead of torch.cuda.amp fp16 autocast; use_half_precision selects bf16;
+  * streaming (batch 1) can replay a hipGraph of the whole forward with the coefficients
+    frozen (config.use_graphs), and stability metrics are read lazily (no per-frame host
+    syncs over 76 modules unless collect_stability is set);
+  * the reference preprocessor's stale-cache defect is not reproduced.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from collections import deque
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, List, Optional, Union
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+logger = logging.getLogger(__name__)
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+@dataclass
+class InferenceConfig:
+    """engine.py:33-63 (+ use_graphs / collect_stability)."""
+    device: str = "cuda"
+    use_half_precision: bool = True
+    use_tensorrt: bool = False
+    tensorrt_precision: str = "FP16"
+    batch_size: int = 1
+    max_batch_size: int = 16
+    warmup_iterations: int = 10
+    enable_batching: bool = True
+    model_path: str = ""
+    input_height: int = 416
+    input_width: int = 416
+    num_classes: int = 80
+    confidence_threshold: float = 0.25
+    iou_threshold: float = 0.45
+    enable_profiling: bool = False
+    log_interval: int = 100
+    memory_monitoring: bool = True
+    max_latency_ms: int = 50
+    target_fps: int = 30
+    use_graphs: bool = False
+    collect_stability: bool = False
+
+
+def preprocess_image(img: np.ndarray, height: int, width: int, device) -> torch.Tensor:
+    """uint8 HWC BGR -> normalised fp32 CHW (preprocessing.py:181-232 semantics: BGR->RGB,
+    bilinear resize, /255, ImageNet mean/std).  Resize runs on the device."""
+    t = torch.from_numpy(np.ascontiguousarray(img[..., ::-1])).to(device)
+    t = t.permute(2, 0, 1).unsqueeze(0).float() / 255.0
+    if t.shape[-2:] != (height, width):
+        t = F.interpolate(t, size=(height, width), mode="bilinear", align_corners=False)
+    mean = torch.tensor(IMAGENET_MEAN, device=device).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=device).view(1, 3, 1, 1)
+    return ((t - mean) / std)[0]
+
+
+class InferenceEngine:
+    """engine.py:72-562."""
+
+    def __init__(self, config: Optional[InferenceConfig] = None, model: Optional[torch.nn.Module] = None,
+                 device: Optional[str] = None, **kw):
+        if config is None:
+            config = InferenceConfig()
+        elif isinstance(config, dict):
+            config = InferenceConfig(**{k: v for k, v in config.items() if k in InferenceConfig.__dataclass_fields__})
+        if device is not None:
+            config.device = str(device)
+        self.config = config
+        self.device = torch.device(config.device)
+        self.use_half = config.use_half_precision and self.device.type == "cuda"
+        self.model = model
+        if model is None and config.model_path:
+            self._load_model()
+        elif model is not None:
+            self.model = model.to(self.device)
+        if self.model is not None:
+            self.model.eval()
+            if hasattr(self.model, "set_precision"):
+                self.model.set_precision("bf16" if self.use_half else "fp32")
+        self.inference_times: deque = deque(maxlen=100)
+        self.memory_usage: deque = deque(maxlen=100)
+        self.stability_metrics: List[Dict[str, Any]] = []
+        self.batch_queue: queue.Queue = queue.Queue(maxsize=config.max_batch_size)
+        self.batch_thread: Optional[threading.Thread] = None
+        self.batch_running = False
+        self._lock = threading.Lock()
+        self._runner = None
+        if config.warmup_iterations > 0 and self.model is not None:
+            self._warmup()
+
+    # ------------------------------------------------------------------ setup
+    def _load_model(self):
+        ckpt = torch.load(self.config.model_path, map_location="cpu", weights_only=True)
+        sd = ckpt.get("model_state_dict", ckpt.get("state_dict", ckpt)) if isinstance(ckpt, dict) else None
+        if self.model is None or sd is None:
+            raise RuntimeError("InferenceEngine: pass a model instance; checkpoints load as state_dicts only")
+        self.model.load_state_dict(sd)
+        self.model = self.model.to(self.device).eval()
+
+    def _warmup(self):
+        x = torch.randn(self.config.batch_size, 3, self.config.input_height, self.config.input_width,
+                        device=self.device)
+        with torch.no_grad():
+            for _ in range(self.config.warmup_iterations):
+                self.model(x, task="detection")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        if self.config.use_graphs and hasattr(self.model, "capture"):
+            self.model.freeze(True)
+            self._runner = self.model.capture(x[:1].contiguous())
+
+    def _to_tensor(self, image: Union[np.ndarray, torch.Tensor]) -> torch.Tensor:
+        if isinstance(image, np.ndarray):
+            return preprocess_image(image, self.config.input_height, self.config.input_width, self.device)
+        return image.to(self.device)
+
+    def preprocess_batch(self, images: List[np.ndarray]) -> torch.Tensor:
+        return torch.stack([self._to_tensor(i) for i in images])
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def infer(self, image: Union[np.ndarray, torch.Tensor]) -> Dict[str, Any]:
+        """engine.py:251-317."""
+        start = time.perf_counter()
+        x = self._to_tensor(image)
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        with self._lock:
+            if self._runner is not None and tuple(x.shape) == tuple(self._runner.static_in.shape):
+                outputs = self._runner(x)
+            else:
+                outputs = self.model(x, task="detection")
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+        ms = (time.perf_counter() - start) * 1e3
+        self.inference_times.append(ms)
+        if self.device.type == "cuda":
+            self.memory_usage.append(torch.cuda.memory_allocated() / 1024 ** 2)
+        res = {"outputs": outputs, "inference_time_ms": ms, "batch_size": x.shape[0],
+               "input_shape": x.shape, "device": str(self.device)}
+        if self.config.collect_stability and hasattr(self.model, "get_stability_metrics"):
+            st = self.model.get_stability_metrics()
+            self.stability_metrics.append(st)
+            res["stability_metrics"] = st
+        return res
+
+    inference = infer   # call-site alias (scripts/inference.py:121)
+
+    @torch.no_grad()
+    def infer_batch(self, images: List[Union[np.ndarray, torch.Tensor]]) -> List[Dict[str, Any]]:
+        """engine.py:319-387."""
+        t0 = time.perf_counter()
+        batch = torch.stack([self._to_tensor(i) for i in images])
+        with self._lock:
+            outputs = self.model(batch, task="detection")
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        results = []
+        for i in range(len(images)):
+            per = {}
+            for k, v in outputs.items():
+                if isinstance(v, torch.Tensor):
+                    per[k] = v[i:i + 1]
+                elif isinstance(v, dict):
+                    per[k] = {kk: (vv[i:i + 1] if isinstance(vv, torch.Tensor) else vv) for kk, vv in v.items()}
+                else:
+                    per[k] = v
+            results.append({"outputs": per, "batch_index": i, "batch_inference_time_ms": ms / len(images),
+                            "total_inference_time_ms": ms})
+        return results
+
+    # ------------------------------------------------------------------ async (engine.py:389-471)
+    def start_async_inference(self):
+        if self.batch_thread is not None:
+            logger.warning("Async inference already running")
+            return
+        self.batch_running = True
+        self.batch_thread = threading.Thread(target=self._async_loop, daemon=True)
+        self.batch_thread.start()
+
+    def stop_async_inference(self):
+        self.batch_running = False
+        if self.batch_thread:
+            self.batch_thread.join(timeout=5.0)
+            self.batch_thread = None
+
+    def _async_loop(self):
+        buf, stamps = [], []
+        while self.batch_running:
+            try:
+                item = self.batch_queue.get(timeout=0.1)
+                buf.append(item)
+                stamps.append(time.time())
+            except queue.Empty:
+                if not buf:
+                    continue
+            ready = len(buf) >= self.config.batch_size or (buf and time.time() - stamps[0] > 0.033)
+            if ready:
+                try:
+                    for r, it in zip(self.infer_batch([b["image"] for b in buf]), buf):
+                        if it.get("callback"):
+                            it["callback"](r)
+                except Exception as e:  # noqa: BLE001 -- the reference logs and keeps serving
+                    logger.error(f"Error in async inference loop: {e}")
+                buf.clear()
+                stamps.clear()
+
+    def async_infer(self, image: np.ndarray, callback: Optional[Callable] = None):
+        if not self.batch_running:
+            raise RuntimeError("Async inference not started")
+        self.batch_queue.put({"image": image, "callback": callback, "timestamp": time.time()})
+
+    # ------------------------------------------------------------------ stats (engine.py:473-562)
+    def get_performance_stats(self) -> Dict[str, Any]:
+        if not self.inference_times:
+            return {}
+        t = list(self.inference_times)
+        stats = {"inference_time": {"mean": float(np.mean(t)), "std": float(np.std(t)), "min": float(np.min(t)),
+                                    "max": float(np.max(t)), "p95": float(np.percentile(t, 95)),
+                                    "p99": float(np.percentile(t, 99)), "latest": t[-1]},
+                 "throughput_fps": 1000.0 / float(np.mean(t)), "total_inferences": len(t)}
+        if self.memory_usage:
+            m = list(self.memory_usage)
+            stats["memory_usage_mb"] = {"mean": float(np.mean(m)), "max": float(np.max(m)), "current": m[-1]}
+        stats["latency_constraint_met"] = stats["inference_time"]["p95"] <= self.config.max_latency_ms
+        return stats
+
+    def get_stability_report(self) -> Dict[str, Any]:
+        if not self.stability_metrics:
+            return {}
+        rep = {"eigenvalues": [], "signal_ratios": [], "gradient_norms": [],
+               "total_checks": len(self.stability_metrics)}
+        for m in self.stability_metrics[-100:]:
+            rep["eigenvalues"] += [v for k, v in m.items() if k.endswith("max_eigenvalue")]
+            rep["signal_ratios"] += [v for k, v in m.items() if k.endswith("signal_ratio_mean")]
+        if rep["eigenvalues"]:
+            e = rep["eigenvalues"]
+            rep["eigenvalue_stats"] = {"mean": float(np.mean(e)), "std": float(np.std(e)), "max": float(np.max(e))}
+            rep["is_stable"] = all(v <= 1.0 + 1e-3 for v in e)
+        if rep["signal_ratios"]:
+            rep["signal_ratio_stats"] = {"mean": float(np.mean(rep["signal_ratios"])),
+                                         "std": float(np.std(rep["signal_ratios"]))}
+        return rep
+
+    def reset_stats(self):
+        self.inference_times.clear()
+        self.memory_usage.clear()
+        self.stability_metrics.clear()
+
+
+class AsyncInferenceEngine(InferenceEngine):
+    """engine.py:564-671: asyncio front-end over a thread pool (kernels are stream-ordered and
+    the engine serialises model calls, so concurrent requests are safe)."""
+
+    def __init__(self, config: Optional[InferenceConfig] = None, model: Optional[torch.nn.Module] = None, **kw):
+        super().__init__(config, model, **kw)
+        self.executor = ThreadPoolExecutor(max_workers=4)
+        self.request_counter = 0
+
+    async def infer_async(self, image: np.ndarray) -> Dict[str, Any]:
+        self.request_counter += 1
+        loop = asyncio.get_event_loop()
+        return await loop.run_in_executor(self.executor, self.infer, image)
+
+    def infer_sync(self, image: np.ndarray) -> Dict[str, Any]:
+        try:
+            loop = asyncio.get_event_loop()
+        except RuntimeError:
+            loop = asyncio.new_event_loop()
+            asyncio.set_event_loop(loop)
+        return loop.run_until_complete(self.infer_async(image))

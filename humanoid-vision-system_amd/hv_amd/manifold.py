@@ -114,9 +114,9 @@ def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.d
 
 def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token chain on x2 [T, D] (compute dtype).  Returns LN_post(...) (+ residual) [T, D]."""
-    if (USE_FUSED and p.fold and residual is None and x2.is_contiguous()
-            and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)):
-        return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post)
+    if (USE_FUSED and p.fold and x2.is_contiguous() and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)
+            and (residual is None or residual.dtype == x2.dtype)):
+        return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post, residual)
     mean, rstd = ops.row_stats(x2, 1e-5)
     if p.fold:
         h1 = ops.gemm(x2, p.b1, bias=p.c1, act="gelu", a_mean=mean, a_rstd=rstd)
@@ -128,16 +128,30 @@ def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = N
     return ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x2.dtype, residual=residual)
 
 
-def prepare_plans(mods, ctx: RunCtx) -> None:
+def sinkhorn_group_for(mods, cache: Optional[dict] = None) -> "ops.SinkhornGroup":
+    """The device table of Sinkhorn problems for these modules (reused while the parameter
+    storage and iteration counts are unchanged, so a captured graph can replay it)."""
+    key = tuple((m.H_res_raw.data_ptr(), tuple(m.H_res_raw.shape), m.sinkhorn.num_iterations) for m in mods)
+    if cache is not None and cache.get("key") == key:
+        return cache["group"]
+    raws = [m.H_res_raw.detach() for m in mods]
+    if any(r.dtype != torch.float32 or not r.is_contiguous() for r in raws):
+        raise TypeError("H_res_raw must be contiguous fp32")
+    group = ops.SinkhornGroup(raws, [m.sinkhorn.num_iterations for m in mods], raws[0].device,
+                              mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau)
+    group.run(raws)                      # uploads the table once
+    if cache is not None:
+        cache["key"], cache["group"] = key, group
+    return group
+
+
+def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None) -> None:
     """Grouped Sinkhorn for every mHC module of a model + per-site coefficient prep."""
     mods = [m for m in mods if id(m) not in ctx.plans]
     if not mods:
         return
-    dev = mods[0].H_res_raw.device
-    raws = [m.H_res_raw.detach().float().contiguous() for m in mods]
-    group = ops.SinkhornGroup(raws, [m.sinkhorn.num_iterations for m in mods], dev,
-                              mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau)
-    outs = group.run(raws)
+    group = sinkhorn_group_for(mods, cache)
+    outs = group.run()
     for m, h, hist in zip(mods, outs, group.hists):
         m.sinkhorn.convergence_history.copy_(hist[: m.sinkhorn.num_iterations])
         ctx.plans[id(m)] = build_plan(m, h[0], ctx.dtype)

@@ -160,7 +160,7 @@ def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype) -> bool:
     return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype)))
 
 
-def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post) -> Tensor:
+def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optional[Tensor] = None) -> Tensor:
     """One-launch mHC token chain (bf16) for x [T, D]; see hv_mhc_fused in hv_kernels.h."""
     _contig(x, "x")
     T, D = x.shape
@@ -169,9 +169,12 @@ def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post) -> Tensor:
         raise ValueError("mhc_fused: coefficient shapes do not match x")
     for t in (a1t, w2, wct):
         _contig(t, "coefficient")
+    if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype or not residual.is_contiguous()):
+        raise ValueError("mhc_fused: residual must match x")
     out = torch.empty_like(x)
     a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
-                       b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), out.data_ptr())
+                       b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), ptr(residual),
+                       out.data_ptr())
     check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
     return out
 

@@ -134,7 +134,8 @@ int hv_bn_fold(int c, const float* gamma, const float* beta, const float* mean, 
 /* ------------------------------------------------------------------------------------
  * Fused mHC token chain (ManifoldHyperConnection.forward, manifold_layers.py:223-280) for
  * the small-D backbone sites: LN_pre, folded GEMM1 + GELU, GEMM2 + GELU, [x|h2] Wc, LN_post
- * in one launch, intermediates on chip.  bf16 only; (D, Hd) in {(32,128), (64,256)}.
+ * in one launch, intermediates on chip.  bf16 only;
+ * (D, Hd) in {(32,128), (64,256), (128,512), (256,512)}.
  * Operands are the folded coefficients of hv_mhc_prep + the fold GEMM.
  * ------------------------------------------------------------------------------------ */
 typedef struct hv_mhc_fused_args {
@@ -147,9 +148,12 @@ typedef struct hv_mhc_fused_args {
   const void* wct;      /* [D, D+Hd] centred [H_res ; H_post]^T */
   const float* g_post;  /* [D] */
   const float* b_post;  /* [D] */
+  const void* residual; /* optional [T, D], added after LN_post (transformer residual stream) */
   void* out;            /* [T, D] */
 } hv_mhc_fused_args;
 int hv_mhc_fused_supported(int D, int Hd, int dtype);
+/* 1: also dispatch (256, 512) to the fused kernel (off by default: slower than unfused) */
+void hv_mhc_fused_enable_wide(int on);
 int hv_mhc_fused(const hv_mhc_fused_args* args, hv_stream_t stream);
 
 /* y[N] = W[N, K] x[K] + b  (fp32; folded mHC bias c1 = W1 u + b1) */

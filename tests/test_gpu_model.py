@@ -57,22 +57,31 @@ def test_mhc_bf16_agreement(gpu_device, D, e):
     assert rel_l2(y, g["y64"]) < 5e-2
 
 
-@pytest.mark.parametrize("D,T", [(32, 64), (32, 1000), (64, 64), (64, 777)])
-def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, T):
+@pytest.mark.parametrize("D,e,T,with_res", [(32, 4, 64, False), (32, 4, 1000, False), (64, 4, 64, False),
+                                             (64, 4, 777, False), (128, 4, 200, False), (256, 2, 401, False),
+                                             (256, 2, 130, True)])
+def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, e, T, with_res):
     """hv_mhc_fused (one launch, on-chip intermediates) vs the six-launch chain, both bf16."""
     from hv_amd import ManifoldHyperConnection
     from hv_amd import manifold as MF
-    m = ManifoldHyperConnection(D, expansion_rate=4, use_mixed_precision=True)
+    from hv_amd.runtime import RunCtx, use_ctx
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
     W.load_formula_weights(m, "wc")
     m = m.to(gpu_device).eval()
-    x = torch.randn(T, D, generator=torch.Generator().manual_seed(T)).to(gpu_device)
-    MF.USE_FUSED = True
-    y1 = m(x).float().cpu().numpy()
-    MF.USE_FUSED = False
-    try:
-        y0 = m(x).float().cpu().numpy()
-    finally:
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
+    res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
+    from hv_amd import _lib
+    _lib.lib().hv_mhc_fused_enable_wide(1)
+    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
         MF.USE_FUSED = True
+        y1 = m.forward_tokens(x, residual=res).float().cpu().numpy()
+        MF.USE_FUSED = False
+        try:
+            y0 = m.forward_tokens(x, residual=res).float().cpu().numpy()
+        finally:
+            MF.USE_FUSED = True
+            _lib.lib().hv_mhc_fused_enable_wide(0)
     assert rel_l2(y1, y0) < 1e-2
     assert np.abs(y1 - y0).max() < 0.1
 
@@ -148,6 +157,43 @@ def test_model_bf16_agreement(gpu_device, tag, tiny, fam, S, B, sub):
         if sure.any():
             agree.append((ci[sure] == g[f"cls{s}_f64"][sure]).mean())
     assert agree and min(agree) > 0.9, agree
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_capture_replays_the_eager_forward(gpu_device, precision):
+    """The hipGraph-captured step (Sinkhorn + prep + token path) equals the eager forward."""
+    m = _build("tiny", "wc", precision, gpu_device)
+    x = cases.model_input(2, 224).to(gpu_device)
+    with torch.no_grad():
+        ref = m(x)
+        runner = m.capture(x)
+        out = runner(x)
+        for s in range(3):
+            assert torch.equal(out["predictions"][f"scale_{s}"], ref["predictions"][f"scale_{s}"])
+        assert torch.equal(out["final_features"], ref["final_features"])
+        x2 = x.flip(-1).contiguous()
+        out2 = runner(x2)["predictions"]["scale_0"].clone()
+        assert torch.equal(out2, m(x2)["predictions"]["scale_0"])
+
+
+def test_inference_engine_api(gpu_device):
+    """InferenceEngine (reference src/inference/engine.py) over the HIP model: infer on a uint8
+    BGR frame, the graph-replay streaming path, infer_batch splitting, stats."""
+    import numpy as np
+    from inference.engine import InferenceConfig, InferenceEngine
+    m = _build("tiny", "wc", "fp32", gpu_device)
+    cfg = InferenceConfig(device=str(gpu_device), use_half_precision=False, warmup_iterations=1,
+                          input_height=128, input_width=128, use_graphs=True)
+    eng = InferenceEngine(cfg, m)
+    frame = np.random.default_rng(0).integers(0, 255, (96, 160, 3), dtype=np.uint8)
+    r = eng.infer(frame)
+    assert r["batch_size"] == 1 and r["outputs"]["predictions"]["scale_0"].shape[0] == 1
+    m.freeze(False)
+    direct = m(eng._to_tensor(frame)[None], task="detection")["predictions"]["scale_0"]
+    assert torch.allclose(r["outputs"]["predictions"]["scale_0"], direct, atol=1e-5)
+    rs = eng.infer_batch([frame, frame[:, ::-1]])
+    assert len(rs) == 2 and rs[1]["outputs"]["predictions"]["scale_0"].shape[0] == 1
+    assert eng.get_performance_stats()["total_inferences"] == 1
 
 
 def test_model_deterministic_and_frozen_cache(gpu_device):
