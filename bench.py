@@ -67,7 +67,8 @@ class GemmTimer:
             out = g0(a, b, **kw)
             e.record()
             k = b.shape[1]
-            self.recs.append((s, e, 2.0 * a.shape[0] * b.shape[0] * k))
+            m, n = a.shape[0], b.shape[0]
+            self.recs.append((s, e, 2.0 * m * n * k, a.element_size() * (m * k + n * k + m * n)))
             return out
 
         def conv2d(x, w, k, stride, pad, **kw):
@@ -76,7 +77,8 @@ class GemmTimer:
             out = c0(x, w, k, stride, pad, **kw)
             e.record()
             m = out.shape[0] * out.shape[1] * out.shape[2]
-            self.recs.append((s, e, 2.0 * m * w.shape[0] * w.shape[1]))
+            self.recs.append((s, e, 2.0 * m * w.shape[0] * w.shape[1],
+                              x.element_size() * (x.numel() + w.numel() + m * w.shape[0])))
             return out
 
         ops.gemm, ops.conv2d = gemm, conv2d
@@ -88,10 +90,11 @@ class GemmTimer:
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e, _ in self.recs)
-        fl = sum(f for _, _, f in self.recs)
+        ms = sum(r[0].elapsed_time(r[1]) for r in self.recs)
+        fl = sum(r[2] for r in self.recs)
+        by = sum(r[3] for r in self.recs)
         n = len(self.recs)
-        return n, ms / n, fl / n, fl / (ms * 1e-3) / 1e12
+        return n, ms / n, fl / n, fl / (ms * 1e-3) / 1e12, by / n
 
 
 def cpu_baseline(model_cpu_sd, size, threads):
@@ -163,7 +166,12 @@ def main():
     # dominant-kernel roofline: the MFMA GEMM family, timed with HIP events in one more step
     with torch.no_grad(), GemmTimer(ops) as gt:
         model(x)
-    n_l, avg_ms, avg_flop, gemm_tflops = gt.summary()
+    n_l, avg_ms, avg_flop, gemm_tflops, avg_bytes = gt.summary()
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if a.size == 640 and a.batch == 16 and a.precision == "bf16" and os.path.exists(tf):
+        with open(tf) as f:
+            traffic = json.load(f).get("gemm", {}).get("bytes_per_launch")
 
     lat = None
     if rank == 0 and not a.no_latency:
@@ -207,7 +215,11 @@ def main():
                        "per_gpu_batch": a.batch, "seq_len": None, "parallelism": f"replicas{world}"},
             "roofline": {"bound": "mfma", "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit-GEMM conv)",
                          "achieved": round(gemm_tflops, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(gemm_tflops / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                         "frac": round(gemm_tflops / BF16_PEAK_TFLOPS, 4),
+                         "traffic": round(traffic) if traffic else None,
+                         "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload "
+                                           "(FETCH x2 gfx950 correction), profiles/r01/pmc_traffic.json",
+                         "algorithmic_bytes_per_launch": round(avg_bytes),
                          "launches_per_step": n_l, "avg_launch_ms": round(avg_ms, 4),
                          "avg_flop_per_launch": avg_flop},
             "model_tflops_reference_graph": round(GFLOP_PER_IMG_640 * value / 1e3, 2) if a.size == 640 else None,
