@@ -77,4 +77,12 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 #define HV_CHECK_LAUNCH() \
   do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
+// Instantiate KERNEL_CALL with T = storage type of dtype code dt (returns HV_EINVAL otherwise).
+#define HV_DISPATCH(dt, KERNEL_CALL)                                     \
+  do {                                                                   \
+    if ((dt) == HV_BF16) { using T = unsigned short; KERNEL_CALL; }      \
+    else if ((dt) == HV_F32) { using T = float; KERNEL_CALL; }           \
+    else return HV_EINVAL;                                               \
+  } while (0)
+
 static inline unsigned hv_cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

@@ -7,13 +7,6 @@ namespace {
 
 using bf = unsigned short;
 
-#define HV_DISPATCH(dt, KERNEL_CALL)                 \
-  do {                                               \
-    if ((dt) == HV_BF16) { using T = bf; KERNEL_CALL; } \
-    else if ((dt) == HV_F32) { using T = float; KERNEL_CALL; } \
-    else return HV_EINVAL;                           \
-  } while (0)
-
 // ---------------------------------------------------------------- row statistics / norms
 // One wave per row; two-pass mean / variance from the row held in L1.
 template <typename T>
@@ -209,20 +202,36 @@ constexpr int CM_CHUNK = 1024;
 template <typename T>
 __global__ void __launch_bounds__(256) k_chan_partial(const T* __restrict__ x, int hw, int c,
                                                       int nchunk, float* part) {
-  __shared__ float red[4][64];
-  const int cg = blockIdx.x, chunk = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ch = cg * 64 + lane;
-  float s = 0.f;
-  if (ch < c) {
+  // Each thread streams 16-byte row vectors (VEC channels) down a column of rows; a block
+  // covers RPI = 256 / (c / VEC) rows per step, so every wave load is fully coalesced.
+  // Requires c % VEC == 0 and c / VEC <= 256 (checked by the launcher).
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float red[256 * VEC];
+  const int chunk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int cv = c / VEC, rpi = 256 / cv;
+  const int g = t % cv, r = t / cv;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  if (r < rpi) {
     const int p0 = chunk * CM_CHUNK, p1 = min(hw, p0 + CM_CHUNK);
-    const T* base = x + (long)b * hw * c + ch;
-    for (int p = p0 + wv; p < p1; p += 4) s += Elem<T>::load(base, (long)p * c);
+    const T* base = x + (long)b * hw * c + g * VEC;
+    for (int p = p0 + r; p < p1; p += rpi) {
+      const uint4 v = *reinterpret_cast<const uint4*>(base + (long)p * c);
+      const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += Elem<T>::load(e, j);
+    }
   }
-  red[wv][lane] = s;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[t * VEC + j] = acc[j];
   __syncthreads();
-  if (wv == 0 && ch < c)
-    part[((long)b * nchunk + chunk) * c + ch] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  // red[(r*cv + g)*VEC + j] holds channel g*VEC+j of row-slot r; sum the rpi slots in order
+  for (int ch = t; ch < c; ch += 256) {
+    float s = 0.f;
+    for (int q = 0; q < rpi; ++q) s += red[q * c + ch];
+    part[((long)b * nchunk + chunk) * c + ch] = s;
+  }
 }
 
 __global__ void k_chan_final(const float* part, int n, int nchunk, int c, float inv, float* out) {
@@ -543,9 +552,11 @@ extern "C" size_t hv_channel_mean_work_floats(int n, int hw, int c) {
 extern "C" int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out,
                                float* work, hv_stream_t stream) {
   if (n <= 0 || hw <= 0 || c <= 0 || !work) return HV_EINVAL;
+  const int vec = dtype == HV_BF16 ? 8 : 4;
+  if (c % vec || c / vec > 256 || ((uintptr_t)x & 15)) return HV_EINVAL;
   const int nchunk = (hw + CM_CHUNK - 1) / CM_CHUNK;
   hipStream_t s = (hipStream_t)stream;
-  HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(hv_cdiv(c, 64), nchunk, n), 256, 0, s>>>(
+  HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(nchunk, n), 256, 0, s>>>(
                           (const T*)x, hw, c, nchunk, work)));
   k_chan_final<<<hv_cdiv((long)n * c, 256), 256, 0, s>>>(work, n, nchunk, c, 1.0f / hw, out);
   HV_CHECK_LAUNCH();

@@ -214,7 +214,10 @@ extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count
 }
 
 extern "C" int hv_abi_version(void) { return 1; }
-extern "C" void hv_struct_sizes(int* out2) {
-  out2[0] = (int)sizeof(hv_sinkhorn_entry);
-  out2[1] = (int)sizeof(hv_gemm_desc);
+extern "C" void hv_struct_sizes(int* out5) {
+  out5[0] = (int)sizeof(hv_sinkhorn_entry);
+  out5[1] = (int)sizeof(hv_gemm_desc);
+  out5[2] = (int)sizeof(hv_mhc_fused_args);
+  out5[3] = (int)sizeof(hv_mhc_prep_entry);
+  out5[4] = (int)sizeof(hv_wprep_entry);
 }

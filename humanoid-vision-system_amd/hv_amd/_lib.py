@@ -53,7 +53,25 @@ class MhcFusedArgs(C.Structure):
                 ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp)]
 
 
+class MhcPrepEntry(C.Structure):
+    _fields_ = [("h_pre_raw", vp), ("h_post_raw", vp), ("h_res", vp), ("gamma_pre", vp), ("beta_pre", vp),
+                ("w1", vp), ("b1", vp), ("a1", vp), ("c1", vp), ("wct", vp), ("scratch", vp),
+                ("D", i32), ("Hd", i32), ("fold", i32), ("pad_", i32), ("blk", i32 * 3), ("pad2_", i32)]
+
+
+class WprepEntry(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("gamma", vp), ("beta", vp), ("mean", vp), ("var", vp),
+                ("cbias", vp), ("scale_out", vp), ("bias_out", vp), ("n", i64),
+                ("kind", i32), ("dtype", i32), ("cin", i32), ("k", i32), ("ldk", i32), ("blk", i32),
+                ("eps", f32), ("pad_", i32)]
+
+
 _SIGS = {
+    "hv_mhc_prep_scratch_floats": ([i32, i32], C.c_size_t),
+    "hv_mhc_prep_blocks": ([i32, i32, i32, vp], None),
+    "hv_mhc_prep_group": ([vp, i32, i32, vp, vp], i32),
+    "hv_wprep_blocks": ([i32, i64, i32, i32], i32),
+    "hv_wprep_group": ([vp, i32, i32, vp], i32),
     "hv_mhc_fused_supported": ([i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
     "hv_mhc_fused_enable_wide": ([i32], None),
@@ -95,11 +113,11 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    sizes = (C.c_int * 2)()
+    sizes = (C.c_int * 5)()
     lib.hv_struct_sizes(sizes)
-    if sizes[0] != C.sizeof(SinkhornEntry) or sizes[1] != C.sizeof(GemmDesc):
-        raise RuntimeError(f"libhvs struct layout mismatch: C {list(sizes)} vs ctypes "
-                           f"{[C.sizeof(SinkhornEntry), C.sizeof(GemmDesc)]}")
+    want = [C.sizeof(s) for s in (SinkhornEntry, GemmDesc, MhcFusedArgs, MhcPrepEntry, WprepEntry)]
+    if list(sizes) != want:
+        raise RuntimeError(f"libhvs struct layout mismatch: C {list(sizes)} vs ctypes {want}")
 
 
 def lib():

@@ -364,7 +364,8 @@ class HybridVisionSystem(nn.Module):
 
     def _make_ctx(self) -> RunCtx:
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache)
+        key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":

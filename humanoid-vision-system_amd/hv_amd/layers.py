@@ -18,9 +18,11 @@ def conv_prep(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], dtype: torch.dtype,
         return ctx.plans[key]
     cout = conv.out_channels
     dev = conv.weight.device
+    if bn is not None and bn.training:
+        raise NotImplementedError("hv_amd: BatchNorm batch statistics (training mode) not implemented yet")
+    if ctx is not None and ctx.program is not None and ctx.program.dtype == dtype:
+        ctx.program.add_conv(conv, bn)            # grouped from the next forward on
     if bn is not None:
-        if bn.training:
-            raise NotImplementedError("hv_amd: BatchNorm batch statistics (training mode) not implemented yet")
         scale, bias = ops.bn_fold(cout, dev, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                   conv.bias, bn.eps)
     else:
@@ -39,6 +41,8 @@ def linear_prep(lin: nn.Linear, dtype: torch.dtype):
     if ctx is not None and key in ctx.plans:
         return ctx.plans[key]
     val = (ops.cast(ops.f32(lin.weight), dtype), ops.f32(lin.bias) if lin.bias is not None else None)
+    if ctx is not None and ctx.program is not None and ctx.program.dtype == dtype:
+        ctx.program.add_linear(lin)               # grouped from the next forward on
     if ctx is not None:
         ctx.plans[key] = val
     return val

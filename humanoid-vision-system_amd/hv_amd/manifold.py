@@ -93,8 +93,10 @@ class MhcPlan:
 
 
 def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.dtype) -> MhcPlan:
+    """Per-site coefficient prep (about ten launches per site).  The forward uses the grouped
+    prep.PrepProgram; this path is kept as its independent cross-check (tests/test_gpu_prep.py)."""
     D, Hd = m.input_dim, m.hidden_dim
-    fold = D <= FOLD_MAX_D
+    fold = D <= FOLD_MAX_D and Hd % 32 == 0
     gc, u, wct = ops.mhc_prep(m.H_pre_raw, m.H_post_raw, h_res, m.norm_pre.weight, m.norm_pre.bias,
                               gc_transposed=not fold)
     w1 = ops.f32(m.mlp[0].weight)
@@ -128,33 +130,23 @@ def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = N
     return ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x2.dtype, residual=residual)
 
 
-def sinkhorn_group_for(mods, cache: Optional[dict] = None) -> "ops.SinkhornGroup":
-    """The device table of Sinkhorn problems for these modules (reused while the parameter
-    storage and iteration counts are unchanged, so a captured graph can replay it)."""
-    key = tuple((m.H_res_raw.data_ptr(), tuple(m.H_res_raw.shape), m.sinkhorn.num_iterations) for m in mods)
-    if cache is not None and cache.get("key") == key:
-        return cache["group"]
-    raws = [m.H_res_raw.detach() for m in mods]
-    if any(r.dtype != torch.float32 or not r.is_contiguous() for r in raws):
-        raise TypeError("H_res_raw must be contiguous fp32")
-    group = ops.SinkhornGroup(raws, [m.sinkhorn.num_iterations for m in mods], raws[0].device,
-                              mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau)
-    group.run(raws)                      # uploads the table once
-    if cache is not None:
-        cache["key"], cache["group"] = key, group
-    return group
-
-
-def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None) -> None:
-    """Grouped Sinkhorn for every mHC module of a model + per-site coefficient prep."""
+def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None) -> None:
+    """Sinkhorn + coefficient prep for every mHC module in `mods` through one grouped
+    PrepProgram (reused from `cache` while `key` -- the owner's parameter/buffer storage --
+    and the precision are unchanged, so a captured graph replays the same buffers)."""
+    from .prep import PrepProgram
     mods = [m for m in mods if id(m) not in ctx.plans]
     if not mods:
         return
-    group = sinkhorn_group_for(mods, cache)
-    outs = group.run()
-    for m, h, hist in zip(mods, outs, group.hists):
-        m.sinkhorn.convergence_history.copy_(hist[: m.sinkhorn.num_iterations])
-        ctx.plans[id(m)] = build_plan(m, h[0], ctx.dtype)
+    prog = None
+    if cache is not None and cache.get("key") == (key, ctx.dtype, FOLD_MAX_D):
+        prog = cache["program"]
+    if prog is None:
+        prog = PrepProgram(mods, ctx.dtype, mods[0].H_res_raw.device, FOLD_MAX_D)
+        if cache is not None:
+            cache["key"], cache["program"] = (key, ctx.dtype, FOLD_MAX_D), prog
+    ctx.program = prog
+    prog.run(ctx)
 
 
 # ================================================================== mHC layer

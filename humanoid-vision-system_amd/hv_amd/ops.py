@@ -234,7 +234,7 @@ class SinkhornGroup:
     on every run, so the table's pointers stay valid.
     """
 
-    def __init__(self, raws, iters, device, eps: float = 1e-8, tau: float = 1.0):
+    def __init__(self, raws, iters, device, eps: float = 1e-8, tau: float = 1.0, hists=None):
         self.raws = list(raws)
         self.iters = list(iters)
         lib = L.lib()
@@ -250,7 +250,7 @@ class SinkhornGroup:
             if m > 2048:
                 raise ValueError("hv sinkhorn supports up to 2048 columns")
             out = torch.empty((b, n, m), device=device, dtype=torch.float32)
-            hist = torch.zeros(max(it, 1), device=device, dtype=torch.float32)
+            hist = hists[i] if hists is not None else torch.zeros(max(it, 1), device=device, dtype=torch.float32)
             work = torch.empty(lib.hv_sinkhorn_work_floats(b, n, m, it), device=device, dtype=torch.float32)
             self.outs.append(out)
             self.hists.append(hist)

@@ -2,8 +2,9 @@
 
 The reference recomputes every parameter-only quantity (sigmoid gates, the Sinkhorn
 projection, autocast weight copies) inside every forward.  Here the top-level module
-prepares all of them once at the start of a forward (one grouped Sinkhorn launch set for
-all 76 mHC sites, one prep per site) and the layers look them up by module.  With
+prepares all of them once at the start of a forward (prep.PrepProgram: a fixed handful of
+grouped launches for all 76 mHC sites and every Conv/Linear weight) and the layers look
+them up by module.  With
 ``freeze()`` (eval streaming) the prepared state is reused across forwards until a
 parameter's version counter changes.
 """
@@ -24,6 +25,7 @@ PRECISIONS = {"bf16": torch.bfloat16, "fp32": torch.float32}
 class RunCtx:
     dtype: torch.dtype
     plans: Dict[int, object] = field(default_factory=dict)
+    program: Optional[object] = None      # prep.PrepProgram that produced `plans` (grouped prep)
 
 
 def current() -> Optional[RunCtx]:

@@ -33,8 +33,8 @@ enum { HV_ACT_NONE = 0, HV_ACT_RELU = 1, HV_ACT_SILU = 2, HV_ACT_GELU = 3,
 enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
 
 int hv_abi_version(void);
-/* sizeof(hv_sinkhorn_entry), sizeof(hv_gemm_desc): lets bindings verify their mirrors */
-void hv_struct_sizes(int* out2);
+/* lets bindings verify their struct mirrors */
+void hv_struct_sizes(int* out5);  /* sizeof of the 5 ABI structs, in declaration order */
 
 /* ------------------------------------------------------------------------------------
  * Sinkhorn-Knopp projection, grouped.
@@ -161,6 +161,68 @@ int hv_gemv(const float* W, const float* x, const float* b, int N, int K, float*
 
 /* elementwise cast fp32 -> (fp32|bf16) */
 int hv_cast(const float* x, long n, int y_dtype, void* y, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Grouped per-forward coefficient preparation (every mHC site of a model in 3 launches).
+ * Replaces ManifoldHyperConnection.constrained_matrices (manifold_layers.py:205-221) plus
+ * the fold of H_pre into the first MLP Linear (:253-256) for all sites at once:
+ *   phase 1: column partials of g.s(H_pre_raw), b.s(H_pre_raw); row means of H_res, H_post
+ *   phase 2: Gc (fp32 scratch [D,Hd] when folding; Gc^T [Hd,D] in dtype otherwise), u, Wc^T
+ *   phase 3 (fold sites): A1^T = W1 Gc^T [2Hd, D] (MFMA, dtype) and c1 = W1 u + b1 (fp32)
+ * Unfolded sites get c1 = u.  blk[] are exclusive per-phase block prefixes filled by the
+ * host with hv_mhc_prep_blocks(); totals are the sums.
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_mhc_prep_entry {
+  const float* h_pre_raw;   /* [D, Hd] */
+  const float* h_post_raw;  /* [Hd, D] */
+  const float* h_res;       /* [D, D] Sinkhorn output */
+  const float* gamma_pre;   /* [D] */
+  const float* beta_pre;    /* [D] */
+  const float* w1;          /* [2Hd, Hd] mlp[0].weight (fold sites) */
+  const float* b1;          /* [2Hd] mlp[0].bias (fold sites) */
+  void* a1;                 /* fold: A1^T [2Hd, D]; else Gc^T [Hd, D]  (dtype) */
+  float* c1;                /* fold: [2Hd]; else u [Hd] */
+  void* wct;                /* [D, D+Hd] (dtype) */
+  float* scratch;           /* hv_mhc_prep_scratch_floats(D, Hd) */
+  int D, Hd, fold, pad_;
+  int blk[3];
+  int pad2_;
+} hv_mhc_prep_entry;
+
+size_t hv_mhc_prep_scratch_floats(int D, int Hd);
+/* blocks of each phase for one entry (out3[0..2]) */
+void hv_mhc_prep_blocks(int D, int Hd, int fold, int* out3);
+int hv_mhc_prep_group(const hv_mhc_prep_entry* dev_table, int count, int dtype,
+                      const int* totals3 /* host */, hv_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Grouped weight preparation: fp32 parameters -> GEMM operands in one launch.
+ *   kind 0 (cast):  dst[i] = src[i], i < n
+ *   kind 1 (conv):  dst[co, (kh*k+kw)*cin + ci] = w[co, ci, kh, kw], zero-padded to ldk
+ *                   columns; the per-channel scale/bias of eval BatchNorm (+ conv bias),
+ *                   computed exactly as hv_bn_fold (gamma == NULL: s = 1, bias = conv bias
+ *                   or 0), go to scale_out / bias_out (when non-NULL) for the GEMM epilogue.
+ * Replaces the per-forward weight casts of autocast and the BN folding of the reference's
+ * Conv-BN pairs (vision_backbone.py:113, feature_fusion.py:44, yolo_head.py:122).
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_wprep_entry {
+  const float* src;
+  void* dst;
+  const float* gamma;
+  const float* beta;
+  const float* mean;
+  const float* var;
+  const float* cbias;
+  float* scale_out;
+  float* bias_out;
+  long n;                   /* cast: elements; conv: cout */
+  int kind, dtype, cin, k, ldk, blk;
+  float eps;
+  int pad_;
+} hv_wprep_entry;
+
+int hv_wprep_blocks(int kind, long n, int cin, int k);
+int hv_wprep_group(const hv_wprep_entry* dev_table, int count, int total_blocks, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Pointwise / layout kernels of the CNN + FPN path (NHWC).

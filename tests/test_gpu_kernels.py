@@ -202,6 +202,10 @@ def test_norms_and_pointwise_vs_torch(gpu_device, prec):
     assert rel_err(mp, F.max_pool2d(xf.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)) < tol
     cm = ops.channel_mean(xd)
     assert rel_err(cm, xf.mean(dim=(1, 2))) < 1e-5
+    for (n, hw, c) in [(3, 2500, 32), (2, 1030, 1024), (1, 77, 2048 if dt == torch.bfloat16 else 1024), (2, 9, 40)]:
+        xc = torch.randn(n, hw, c, generator=g).to(dt)
+        got = ops.channel_mean(xc.to(gpu_device))
+        assert rel_err(got, xc.float().mean(dim=1)) < 1e-5, (n, hw, c)
     b = torch.randn(2, 6, 5, 64, generator=g).to(dt)
     up = ops.upsample_add(xd, b.to(gpu_device))
     ref = xf + F.interpolate(b.float().permute(0, 3, 1, 2), size=(12, 10), mode="nearest").permute(0, 2, 3, 1)

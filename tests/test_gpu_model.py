@@ -136,7 +136,10 @@ def _check_fp32(out, g, sub):
 def test_model_fp32_matches_reference(gpu_device, tag, tiny, fam, S, B, sub):
     g = golden(f"model_{tag}")
     m = _build("tiny" if tiny else "base", fam, "fp32", gpu_device)
-    out = m(cases.model_input(B, S).to(gpu_device), task="detection")
+    x = cases.model_input(B, S).to(gpu_device)
+    first = m(x, task="detection")["predictions"]["scale_2"].clone()   # discovers convs/linears
+    out = m(x, task="detection")                                      # fully grouped prep
+    assert torch.equal(first, out["predictions"]["scale_2"])
     _check_fp32(out, g, sub)
     assert set(out) >= {"backbone_features", "vit_features", "fused_features", "predictions", "decoded",
                         "final_features"}
@@ -146,7 +149,10 @@ def test_model_fp32_matches_reference(gpu_device, tag, tiny, fam, S, B, sub):
 def test_model_bf16_agreement(gpu_device, tag, tiny, fam, S, B, sub):
     g = golden(f"model_{tag}")
     m = _build("tiny" if tiny else "base", fam, "bf16", gpu_device)
-    out = m(cases.model_input(B, S).to(gpu_device), task="detection")
+    x = cases.model_input(B, S).to(gpu_device)
+    first = m(x, task="detection")["predictions"]["scale_2"].clone()
+    out = m(x, task="detection")
+    assert torch.equal(first, out["predictions"]["scale_2"])
     agree = []
     for s in range(3):
         step = sub if s == 0 else 1
