@@ -37,6 +37,22 @@ template <> struct Elem<unsigned short> {
 __device__ __forceinline__ float hv_gelu(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
+// GELU for bf16 outputs: x * sigmoid(x * p(x^2)) with p fitted (minimax over all x, x^2
+// clamped at 64) to |err| <= 2.6e-5 against the exact erf GELU -- far below bf16 resolution --
+// in 9 VALU instructions (2 transcendental) instead of ~15 for an erf evaluation.
+__device__ __forceinline__ float hv_gelu_fast(float x) {
+  const float x2 = fminf(x * x, 64.f);
+  const float p = fmaf(fmaf(1.0142630839702301e-3f, x2, -0.10677572552514955f), x2, -2.3011213415186913f);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two floats -> two RNE bf16 in one dword (v_cvt_pk_bf16_f32), low half = a
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
 __device__ __forceinline__ float hv_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float hv_silu(float x) { return x / (1.0f + __expf(-x)); }
 

@@ -17,6 +17,7 @@
 // 16-deep step is permuted identically for A and B, so the products are exact).
 // 256 threads = 4 waves in a 2x2 grid; block -> tile mapping is XCD-aware (bijective).
 #include "hv_common.h"
+#include "hv_gemm_epi.h"
 
 namespace {
 
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
 #pragma unroll
         for (int b = 0; b < RN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, fa[a]), __builtin_bit_cast(bf16x8, fb[b]), acc[a][b], 0, 0, 0);
+              __builtin_bit_cast(bf16x8, fb[b]), __builtin_bit_cast(bf16x8, fa[a]), acc[a][b], 0, 0, 0);
     } else {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
 #pragma unroll
           for (int b = 0; b < RN; ++b) {
             const uint32_t bv = s == 0 ? fb[b].x : s == 1 ? fb[b].y : s == 2 ? fb[b].z : fb[b].w;
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av), __uint_as_float(bv),
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(bv), __uint_as_float(av),
                                                              acc[a][b], 0, 0, 0);
           }
         }
@@ -269,31 +270,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  const int rbase = m0 + wr * (BM / 2) + (lane >> 4) * 4;
-  const int cbase = n0 + wc * (BN / 2) + (lane & 15);
-#pragma unroll
-  for (int b = 0; b < RN; ++b) {
-    const int col = cbase + b * 16;
-    if (col >= d.N) continue;
-    const float sc = d.scale ? d.scale[col] : 1.f;
-    const float bi = d.bias ? d.bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < RM; ++a) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = rbase + a * 16 + j;
-        if (row >= d.M) continue;
-        float v = acc[a][b][j] * d.alpha * sc + bi;
-        v = hv_act(v, d.act);
-        if (d.residual)
-          v += ld_any(d.residual, d.r_dtype, (long)(d.r_mod > 0 ? row % d.r_mod : row) * d.ldr + col);
-        const long o = (long)row * d.ldc + col;
-        if (d.c_dtype == HV_BF16) ((unsigned short*)d.C)[o] = f2bf(v);
-        else ((float*)d.C)[o] = v;
-      }
-    }
-  }
+  // ---- epilogue (hv_gemm_epi.h: sub-tiles accumulated transposed; LN prologue already applied)
+  gemm_epilogue<BM, BN, false>(d, acc, m0, n0);
 }
 
 template <typename T, int BM, int BN>

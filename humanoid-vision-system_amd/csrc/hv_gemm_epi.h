@@ -1,0 +1,95 @@
+// Epilogue shared by the two MFMA GEMM kernels (hv_gemm.hip, hv_gemm_glds.hip).
+//
+//   acc' = acc                                        (plain / LN-prologue kernels)
+//        = rstd[m] * (acc - mean[m] * colsum[n])      (LN_EPI: LayerNorm of A applied AFTER the
+//                                                      product -- exact because
+//                                                      ((a - mean) rstd) . b = rstd (a.b - mean sum(b)))
+//   v = act(alpha * scale[n] * acc' + bias[n])  (+ residual[m or m % r_mod, n])  -> c_dtype
+//   (GELU into a bf16 result without residual uses hv_gelu_fast, |err| <= 2.6e-5)
+//
+// Both kernels accumulate every 16x16 sub-tile TRANSPOSED (B fragment as the MFMA A operand),
+// so a lane holds 4 consecutive columns of one row: one 8-byte (bf16) or 16-byte (fp32)
+// store per sub-tile instead of four scattered 2-byte stores, and one LN row statistic.
+#pragma once
+#include "hv_common.h"
+
+template <int BM, int BN, bool LN_EPI>
+__device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4 (&acc)[BM / 32][BN / 32],
+                                              int m0, int n0) {
+  constexpr int RM = BM / 32, RN = BN / 32;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
+  const bool gelu_fast = c_bf && !d.residual;
+  const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 4 == 0 &&
+                   (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 4 == 0));
+
+  float sc[RN][4], bi[RN][4], cs[RN][4];
+#pragma unroll
+  for (int b = 0; b < RN; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * (BN / 2) + b * 16 + fg * 4 + j;
+      const bool ok = col < d.N;
+      sc[b][j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
+      bi[b][j] = (d.bias && ok) ? d.bias[col] : 0.f;
+      cs[b][j] = 0.f;
+      if constexpr (LN_EPI) cs[b][j] = ok ? d.b_colsum[col] : 0.f;
+    }
+
+#pragma unroll
+  for (int a = 0; a < RM; ++a) {
+    const int row = m0 + wr * (BM / 2) + a * 16 + fr;
+    if (row >= d.M) continue;
+    float mean = 0.f, rstd = 1.f;
+    if constexpr (LN_EPI) {
+      mean = d.a_mean[row];
+      rstd = d.a_rstd[row];
+    }
+    const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
+#pragma unroll
+    for (int b = 0; b < RN; ++b) {
+      const int col = n0 + wc * (BN / 2) + b * 16 + fg * 4;
+      if (col >= d.N) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = acc[a][b][j];
+        if constexpr (LN_EPI) x = rstd * (x - mean * cs[b][j]);
+        x = x * sc[b][j] + bi[b][j];
+        v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+      }
+      if (vec && col + 4 <= d.N) {
+        if (d.residual) {
+          if (r_bf) {
+            const uint2 r = *reinterpret_cast<const uint2*>((const unsigned short*)d.residual + rrow * d.ldr + col);
+            v[0] += __uint_as_float(r.x << 16);
+            v[1] += __uint_as_float(r.x & 0xffff0000u);
+            v[2] += __uint_as_float(r.y << 16);
+            v[3] += __uint_as_float(r.y & 0xffff0000u);
+          } else {
+            const float4 r = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col);
+            v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+          }
+        }
+        if (c_bf)
+          *reinterpret_cast<uint2*>((unsigned short*)d.C + (long)row * d.ldc + col) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        else
+          *reinterpret_cast<float4*>((float*)d.C + (long)row * d.ldc + col) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (col + j >= d.N) break;
+          float x = v[j];
+          if (d.residual)
+            x += r_bf ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
+                      : ((const float*)d.residual)[rrow * d.ldr + col + j];
+          const long o = (long)row * d.ldc + col + j;
+          if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
+          else ((float*)d.C)[o] = x;
+        }
+      }
+    }
+  }
+}

@@ -9,6 +9,7 @@
 // the MFMAs of tile t run.  Out-of-image conv taps read a zero line; rows past M are
 // clamped (computed, never stored).
 #include "hv_common.h"
+#include "hv_gemm_epi.h"
 
 __device__ __attribute__((aligned(64))) uint4 hv_glds_zero_line[4];   // read by out-of-image taps
 
@@ -142,40 +143,17 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
       for (int a = 0; a < RM; ++a)
 #pragma unroll
         for (int b = 0; b < RN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[a]),
-                                                              __builtin_bit_cast(bf16x8, fb[b]), acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[b]),
+                                                              __builtin_bit_cast(bf16x8, fa[a]), acc[a][b], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // ---- epilogue (same contract as the register-staged kernel)
-  const int rbase = m0 + wr * (BM / 2) + (lane >> 4) * 4;
-  const int cbase = n0 + wc * (BN / 2) + (lane & 15);
-#pragma unroll
-  for (int b = 0; b < RN; ++b) {
-    const int col = cbase + b * 16;
-    if (col >= d.N) continue;
-    const float sc = d.scale ? d.scale[col] : 1.f;
-    const float bi = d.bias ? d.bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < RM; ++a) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = rbase + a * 16 + j;
-        if (row >= d.M) continue;
-        float v = acc[a][b][j] * d.alpha * sc + bi;
-        v = hv_act(v, d.act);
-        if (d.residual) {
-          const long ri = (long)(d.r_mod > 0 ? row % d.r_mod : row) * d.ldr + col;
-          v += d.r_dtype == HV_BF16 ? bf2f(((const unsigned short*)d.residual)[ri]) : ((const float*)d.residual)[ri];
-        }
-        const long o = (long)row * d.ldc + col;
-        if (d.c_dtype == HV_BF16) ((unsigned short*)d.C)[o] = f2bf(v);
-        else ((float*)d.C)[o] = v;
-      }
-    }
-  }
+  // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
+  //      LN_EPI: LayerNorm after the product)
+  if (d.a_mean) gemm_epilogue<BM, BN, true>(d, acc, m0, n0);
+  else gemm_epilogue<BM, BN, false>(d, acc, m0, n0);
 }
 
 template <int BM, int BN>
@@ -191,7 +169,8 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
-  if (d.dtype != HV_BF16 || d.a_mean || d.K % 64) return HV_EUNSUPPORTED;
+  if (d.dtype != HV_BF16 || d.K % 64) return HV_EUNSUPPORTED;
+  if (d.a_mean && (!d.b_colsum || d.A2 || d.conv_k > 0)) return HV_EUNSUPPORTED;
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
   if (d.ldb % 8) return HV_EUNSUPPORTED;

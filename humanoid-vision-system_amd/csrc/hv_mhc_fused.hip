@@ -16,7 +16,9 @@
 // exactly one lane as an MFMA B fragment, so each lane loads its 16-byte fragments straight
 // from L2 into a 2-slot register ring (chunk c+1 is in flight while chunk c computes).  LDS
 // holds the x/z tile, a double-buffered h1 chunk (one barrier per chunk), h2 and a small
-// LayerNorm exchange.  GELU uses an erf with |err| <= 1.5e-7 (A&S 7.1.26), far below bf16.
+// LayerNorm exchange.  GEMM1 and GEMM2 are computed transposed (weights as the MFMA A operand)
+// so each lane ends with 4 consecutive hidden units of one token: GELU + bf16 pack + one
+// 8-byte LDS store per tile.  GELU is hv_gelu_fast (|err| <= 2.6e-5, below bf16 resolution).
 #include "hv_common.h"
 
 namespace {
@@ -61,15 +63,6 @@ __device__ __forceinline__ f32x4 mfma(uint4 a, uint4 b, f32x4 c) {
                                                  c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float gelu_fast(float x) {
-  const float u = x * 0.70710678118654752f;
-  const float a = fabsf(u);
-  const float t = 1.0f / (1.0f + 0.3275911f * a);
-  const float p = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t + 0.254829592f) * t;
-  const float e = 1.0f - p * __expf(-a * a);
-  return 0.5f * x * (1.0f + copysignf(e, u));
-}
-
 template <int D, int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
     const unsigned short* __restrict__ x, int T,
@@ -89,9 +82,9 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   const long t0 = (long)blockIdx.x * BM;
 
   // ---------------- weight-fragment ring (registers), 2 slots
-  uint4 fb1[2][C::T1W][D / 32];      // GEMM1 B fragments (rows of A1^T)
-  uint4 fb2[2][C::C2];               // GEMM2 B fragments (rows of W2)
-  float cb1[2][C::T1W];              // c1 bias per GEMM1 tile column
+  uint4 fb1[2][C::T1W][D / 32];      // GEMM1 A fragments (rows of A1^T)
+  uint4 fb2[2][C::C2];               // GEMM2 A fragments (rows of W2)
+  float4 cb1[2][C::T1W];             // c1 for the 4 hidden rows a lane holds per GEMM1 tile
   auto load_chunk = [&](int slot, int ch) {
 #pragma unroll
     for (int i = 0; i < C::T1W; ++i) {
@@ -99,7 +92,7 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
       const int n = ch * KC + ct * 16 + fr;
 #pragma unroll
       for (int ks = 0; ks < D / 32; ++ks) fb1[slot][i][ks] = gl16(a1t + (long)n * D + ks * 32 + fg * 8);
-      cb1[slot][i] = c1[n];
+      cb1[slot][i] = *reinterpret_cast<const float4*>(c1 + ch * KC + ct * 16 + fg * 4);
     }
 #pragma unroll
     for (int b = 0; b < C::C2; ++b)
@@ -158,40 +151,43 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
   for (int ch = 0; ch < C::NCH; ++ch) {
     const int slot = ch & 1;
     unsigned char* h1 = smem + C::OFF_H1 + slot * BM * C::H1S;
+    // GEMM1 transposed (h1^T = A1^T z^T): a lane ends with 4 consecutive hidden units of one
+    // token, i.e. one 8-byte row segment of h1 -> one ds_write_b64 of two packed bf16 pairs
 #pragma unroll
     for (int i = 0; i < C::T1W; ++i) {
       const int t = w * C::T1W + i, rt = t / (KC / 16), ct = t % (KC / 16);
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < D / 32; ++ks)
-        acc = mfma(lds16(smem + C::OFF_Z + (rt * 16 + fr) * C::XS + ks * 64 + fg * 16), fb1[slot][i][ks], acc);
-      const float bias = cb1[slot][i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *(unsigned short*)(h1 + (rt * 16 + fg * 4 + j) * C::H1S + (ct * 16 + fr) * 2) = f2bf(gelu_fast(acc[j] + bias));
+        acc = mfma(fb1[slot][i][ks], lds16(smem + C::OFF_Z + (rt * 16 + fr) * C::XS + ks * 64 + fg * 16), acc);
+      const float4 bias = cb1[slot][i];
+      const uint32_t lo = pack_bf16x2(hv_gelu_fast(acc[0] + bias.x), hv_gelu_fast(acc[1] + bias.y));
+      const uint32_t hi = pack_bf16x2(hv_gelu_fast(acc[2] + bias.z), hv_gelu_fast(acc[3] + bias.w));
+      *reinterpret_cast<uint2*>(h1 + (rt * 16 + fr) * C::H1S + (ct * 16 + fg * 4) * 2) = make_uint2(lo, hi);
     }
     __syncthreads();
     uint4 fa[C::R2];
 #pragma unroll
     for (int a = 0; a < C::R2; ++a) fa[a] = lds16(h1 + (a * 16 + fr) * C::H1S + fg * 16);
+    // GEMM2 transposed too (acc2[a][b] holds h2^T: 4 hidden units x 1 token per lane)
 #pragma unroll
     for (int b = 0; b < C::C2; ++b)
 #pragma unroll
-      for (int a = 0; a < C::R2; ++a) acc2[a][b] = mfma(fa[a], fb2[slot][b], acc2[a][b]);
+      for (int a = 0; a < C::R2; ++a) acc2[a][b] = mfma(fb2[slot][b], fa[a], acc2[a][b]);
     if (ch + 2 < C::NCH) load_chunk(slot, ch + 2);
   }
 
-  // ---------------- phase 2: h2 = GELU(acc2 + b2) -> LDS
+  // ---------------- phase 2: h2 = GELU(acc2 + b2) -> LDS (row-major [token][hidden])
 #pragma unroll
   for (int b = 0; b < C::C2; ++b) {
-    const int col = w * (HD / NW) + b * 16 + fr;
-    const float bias = b2[col];
+    const int col = w * (HD / NW) + b * 16 + fg * 4;
+    const float4 bias = *reinterpret_cast<const float4*>(b2 + col);
 #pragma unroll
-    for (int a = 0; a < C::R2; ++a)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *(unsigned short*)(smem + C::OFF_H2 + (a * 16 + fg * 4 + j) * C::H2S + col * 2) =
-            f2bf(gelu_fast(acc2[a][b][j] + bias));
+    for (int a = 0; a < C::R2; ++a) {
+      const uint32_t lo = pack_bf16x2(hv_gelu_fast(acc2[a][b][0] + bias.x), hv_gelu_fast(acc2[a][b][1] + bias.y));
+      const uint32_t hi = pack_bf16x2(hv_gelu_fast(acc2[a][b][2] + bias.z), hv_gelu_fast(acc2[a][b][3] + bias.w));
+      *reinterpret_cast<uint2*>(smem + C::OFF_H2 + (a * 16 + fr) * C::H2S + col * 2) = make_uint2(lo, hi);
+    }
   }
   __syncthreads();
 
@@ -219,95 +215,92 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
       const uint4 fa = ks < D / 32 ? lds16(smem + C::OFF_X + row * C::XS + ks * 64 + fg * 16)
                                    : lds16(smem + C::OFF_H2 + row * C::H2S + (ks - D / 32) * 64 + fg * 16);
 #pragma unroll
-      for (int c = 0; c < C::CT3; ++c) acc3[r][c] = mfma(fa, fw[slot][c], acc3[r][c]);
+      for (int c = 0; c < C::CT3; ++c) acc3[r][c] = mfma(fw[slot][c], fa, acc3[r][c]);   // transposed tile
     }
     if (ks + 2 < C::KS3) load_wc(slot, ks + 2);
   }
 
   // ---------------- phase 4: LN_post from the accumulators
-  // row (r, j) of this wave = 16 lanes (same fg) x CT3 tiles, x CG waves when CG > 1
+  // acc3[r][c] is a transposed tile: lane -> token (rg*RT3 + r)*16 + fr, columns
+  // (cg*CT3 + c)*16 + fg*4 .. +3.  A token's row = 4 lane groups x CT3 tiles (x CG waves).
   float* red = (float*)(smem + C::OFF_RED);
-  float mu[C::RT3][4], rs[C::RT3][4];
+  float mu[C::RT3], rs[C::RT3];
 #pragma unroll
-  for (int r = 0; r < C::RT3; ++r)
+  for (int r = 0; r < C::RT3; ++r) {
+    float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int c = 0; c < C::CT3; ++c) s += acc3[r][c][j];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-      mu[r][j] = s;
-    }
+    for (int c = 0; c < C::CT3; ++c) sum += (acc3[r][c][0] + acc3[r][c][1]) + (acc3[r][c][2] + acc3[r][c][3]);
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    mu[r] = sum;
+  }
   if constexpr (C::CG > 1) {
 #pragma unroll
     for (int r = 0; r < C::RT3; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (fr == 0) red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + cg] = mu[r][j];
+      if (fg == 0) red[((rg * C::RT3 + r) * 16 + fr) * C::CG + cg] = mu[r];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < C::RT3; ++r)
+    for (int r = 0; r < C::RT3; ++r) {
+      float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int g = 0; g < C::CG; ++g) s += red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + g];
-        mu[r][j] = s;
-      }
+      for (int g = 0; g < C::CG; ++g) sum += red[((rg * C::RT3 + r) * 16 + fr) * C::CG + g];
+      mu[r] = sum;
+    }
     __syncthreads();
   }
 #pragma unroll
-  for (int r = 0; r < C::RT3; ++r)
+  for (int r = 0; r < C::RT3; ++r) {
+    mu[r] *= 1.0f / D;
+    float q = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      mu[r][j] *= 1.0f / D;
-      float q = 0.f;
+    for (int c = 0; c < C::CT3; ++c)
 #pragma unroll
-      for (int c = 0; c < C::CT3; ++c) { const float dd = acc3[r][c][j] - mu[r][j]; q += dd * dd; }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
-      rs[r][j] = q;
-    }
+      for (int j = 0; j < 4; ++j) { const float dd = acc3[r][c][j] - mu[r]; q += dd * dd; }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    rs[r] = q;
+  }
   if constexpr (C::CG > 1) {
 #pragma unroll
     for (int r = 0; r < C::RT3; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (fr == 0) red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + cg] = rs[r][j];
+      if (fg == 0) red[((rg * C::RT3 + r) * 16 + fr) * C::CG + cg] = rs[r];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < C::RT3; ++r)
+    for (int r = 0; r < C::RT3; ++r) {
+      float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int g = 0; g < C::CG; ++g) s += red[((rg * C::RT3 + r) * 16 + fg * 4 + j) * C::CG + g];
-        rs[r][j] = s;
-      }
+      for (int g = 0; g < C::CG; ++g) sum += red[((rg * C::RT3 + r) * 16 + fr) * C::CG + g];
+      rs[r] = sum;
+    }
   }
-  float gp[C::CT3], bp[C::CT3];
+  float4 gp[C::CT3], bp[C::CT3];
 #pragma unroll
   for (int c = 0; c < C::CT3; ++c) {
-    gp[c] = g_post[(cg * C::CT3 + c) * 16 + fr];
-    bp[c] = b_post[(cg * C::CT3 + c) * 16 + fr];
+    gp[c] = *reinterpret_cast<const float4*>(g_post + (cg * C::CT3 + c) * 16 + fg * 4);
+    bp[c] = *reinterpret_cast<const float4*>(b_post + (cg * C::CT3 + c) * 16 + fg * 4);
   }
 #pragma unroll
-  for (int r = 0; r < C::RT3; ++r)
+  for (int r = 0; r < C::RT3; ++r) {
+    const float inv = rsqrtf(rs[r] * (1.0f / D) + 1e-5f);
+    const long row = t0 + (rg * C::RT3 + r) * 16 + fr;
+    if (row >= T) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float inv = rsqrtf(rs[r][j] * (1.0f / D) + 1e-5f);
-      const long row = t0 + (rg * C::RT3 + r) * 16 + fg * 4 + j;
-      if (row < T) {
-#pragma unroll
-        for (int c = 0; c < C::CT3; ++c) {
-          const int col = (cg * C::CT3 + c) * 16 + fr;
-          float v = (acc3[r][c][j] - mu[r][j]) * inv * gp[c] + bp[c];
-          if (res) v += bf2f(res[row * D + col]);
-          out[row * D + col] = f2bf(v);
-        }
+    for (int c = 0; c < C::CT3; ++c) {
+      const int col = (cg * C::CT3 + c) * 16 + fg * 4;
+      float v0 = (acc3[r][c][0] - mu[r]) * inv * gp[c].x + bp[c].x;
+      float v1 = (acc3[r][c][1] - mu[r]) * inv * gp[c].y + bp[c].y;
+      float v2 = (acc3[r][c][2] - mu[r]) * inv * gp[c].z + bp[c].z;
+      float v3 = (acc3[r][c][3] - mu[r]) * inv * gp[c].w + bp[c].w;
+      if (res) {
+        const uint2 q = *reinterpret_cast<const uint2*>(res + row * D + col);
+        v0 += __uint_as_float(q.x << 16);
+        v1 += __uint_as_float(q.x & 0xffff0000u);
+        v2 += __uint_as_float(q.y << 16);
+        v3 += __uint_as_float(q.y & 0xffff0000u);
       }
+      *reinterpret_cast<uint2*>(out + row * D + col) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
     }
+  }
 }
 
 template <int D, int HD, int NW>

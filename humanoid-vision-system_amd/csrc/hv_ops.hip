@@ -400,6 +400,83 @@ __global__ void __launch_bounds__(128) k_attention(const T* q, const T* k, const
   }
 }
 
+// ---- bf16 MFMA attention, head dim 32 (manifold_layers.py:404-427 core).
+// One wave = 16 queries, no LDS, no barriers.  Every product is computed transposed so a lane
+// owns one query:  S^T = K Q^T (lane: 4+4 keys of query fr), online softmax in the log2
+// domain with max/sum across the 4 lane groups (xor 16/32), then O^T += V^T P^T where the
+// 32-key contraction uses the permuted key order {4g..4g+3, 16+4g..16+4g+3} on BOTH
+// operands (P straight from the S^T registers; V^T rows from the pre-transposed vt).
+__global__ void k_vt_pad(const unsigned short* __restrict__ v, int L, int Lp, int heads,
+                         unsigned short* __restrict__ vt) {
+  // vt[b][h][d][key] = v[b][key][h*32 + d], zero for L <= key < Lp
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int bh = blockIdx.y, b = bh / heads, h = bh % heads;
+  if (i >= 32L * Lp) return;
+  const int d = i / Lp, key = i % Lp;
+  vt[(long)bh * 32 * Lp + i] = key < L ? v[((long)b * L + key) * heads * 32 + h * 32 + d] : (unsigned short)0;
+}
+
+__global__ void __launch_bounds__(256) k_attention_mfma(const unsigned short* __restrict__ q,
+                                                        const unsigned short* __restrict__ k,
+                                                        const unsigned short* __restrict__ vt,
+                                                        unsigned short* __restrict__ out, int L, int Lp,
+                                                        int heads, float sl2) {
+  const int b = blockIdx.z, h = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int D = heads * 32;
+  const int q0 = blockIdx.x * 64 + w * 16;
+  if (q0 >= L) return;
+  const unsigned short* qb = q + (long)b * L * D + h * 32;
+  const unsigned short* kb = k + (long)b * L * D + h * 32;
+  const unsigned short* vb = vt + ((long)b * heads + h) * 32 * Lp;
+  const uint4 qf = *reinterpret_cast<const uint4*>(qb + (long)min(q0 + fr, L - 1) * D + fg * 8);
+  f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < L; k0 += 32) {
+    const uint4 kf0 = *reinterpret_cast<const uint4*>(kb + (long)min(k0 + fr, L - 1) * D + fg * 8);
+    const uint4 kf1 = *reinterpret_cast<const uint4*>(kb + (long)min(k0 + 16 + fr, L - 1) * D + fg * 8);
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf0), __builtin_bit_cast(bf16x8, qf), z, 0, 0, 0);
+    const f32x4 s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf1), __builtin_bit_cast(bf16x8, qf), z, 0, 0, 0);
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t[j] = (k0 + fg * 4 + j < L) ? s0[j] * sl2 : -INFINITY;
+      t[4 + j] = (k0 + 16 + fg * 4 + j < L) ? s1[j] * sl2 : -INFINITY;
+    }
+    float mx = fmaxf(fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])), fmaxf(fmaxf(t[4], t[5]), fmaxf(t[6], t[7])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float corr = __builtin_amdgcn_exp2f(m - mn);
+    float p[8], ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { p[j] = __builtin_amdgcn_exp2f(t[j] - mn); ps += p[j]; }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * corr + ps;
+    m = mn;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o0[j] *= corr; o1[j] *= corr; }
+    const uint4 pf = make_uint4(pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3]), pack_bf16x2(p[4], p[5]),
+                                pack_bf16x2(p[6], p[7]));
+    const unsigned short* v0 = vb + (long)fr * Lp + k0 + fg * 4;
+    const unsigned short* v1 = vb + (long)(16 + fr) * Lp + k0 + fg * 4;
+    const uint2 a0 = *reinterpret_cast<const uint2*>(v0), a1 = *reinterpret_cast<const uint2*>(v0 + 16);
+    const uint2 c0 = *reinterpret_cast<const uint2*>(v1), c1 = *reinterpret_cast<const uint2*>(v1 + 16);
+    o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, make_uint4(a0.x, a0.y, a1.x, a1.y)),
+                                                 __builtin_bit_cast(bf16x8, pf), o0, 0, 0, 0);
+    o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, make_uint4(c0.x, c0.y, c1.x, c1.y)),
+                                                 __builtin_bit_cast(bf16x8, pf), o1, 0, 0, 0);
+  }
+  if (q0 + fr < L) {
+    const float inv = 1.0f / l;
+    unsigned short* ob = out + ((long)b * L + q0 + fr) * D + h * 32 + fg * 4;
+    *reinterpret_cast<uint2*>(ob) = make_uint2(pack_bf16x2(o0[0] * inv, o0[1] * inv), pack_bf16x2(o0[2] * inv, o0[3] * inv));
+    *reinterpret_cast<uint2*>(ob + 16) = make_uint2(pack_bf16x2(o1[0] * inv, o1[1] * inv), pack_bf16x2(o1[2] * inv, o1[3] * inv));
+  }
+}
+
 template <typename T>
 __global__ void k_gather_rows(const T* x, long stride_rows, int n, int c, T* y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -635,6 +712,25 @@ extern "C" int hv_attention(int dtype, const void* q, const void* k, const void*
   const dim3 g(hv_cdiv(L, 128), heads, n);
   HV_DISPATCH(dtype, (k_attention<T, 32><<<g, 128, 0, (hipStream_t)stream>>>(
                           (const T*)q, (const T*)k, (const T*)v, (T*)out, L, heads, sm_scale)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_attention_work_elems(int n, int L, int heads, int hd) {
+  return (size_t)n * heads * hd * ((L + 31) / 32 * 32);
+}
+
+extern "C" int hv_attention_mfma(const void* q, const void* k, const void* v, void* vt_work, void* out,
+                                 int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream) {
+  if (n <= 0 || L <= 0 || heads <= 0 || !vt_work) return HV_EINVAL;
+  if (hd != 32 || (((uintptr_t)q | (uintptr_t)k | (uintptr_t)vt_work | (uintptr_t)out) & 15)) return HV_EUNSUPPORTED;
+  const int Lp = (L + 31) / 32 * 32;
+  hipStream_t s = (hipStream_t)stream;
+  k_vt_pad<<<dim3(hv_cdiv(32L * Lp, 256), n * heads), 256, 0, s>>>((const unsigned short*)v, L, Lp, heads,
+                                                                   (unsigned short*)vt_work);
+  k_attention_mfma<<<dim3(hv_cdiv(L, 64), heads, n), 256, 0, s>>>(
+      (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)vt_work, (unsigned short*)out, L, Lp,
+      heads, sm_scale * 1.4426950408889634f);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -6,8 +6,9 @@
 // per mHC site and 2 per Conv-BN pair (about a thousand per forward, each a few
 // microseconds of mostly idle GPU).  Here every site of the model is one entry of a device
 // table and each phase is one launch over the concatenated block ranges of all entries:
-//   hv_mhc_prep_group: 3 launches for all 76 mHC sites (column sums / row means, centred
-//                      Gc + u + Wc^T, fold GEMM A1^T = W1 Gc^T on MFMA + c1 = W1 u + b1);
+//   hv_mhc_prep_group: 4 launches for all 76 mHC sites (column sums / row means, centred
+//                      Gc + u + Wc^T, fold GEMM A1^T = W1 Gc^T on MFMA + c1 = W1 u + b1,
+//                      row sums of the stored A1^T for the GEMM's LayerNorm epilogue);
 //   hv_wprep_group:    1 launch for every cast and every Conv(+BN) weight reorder/fold.
 // A block finds its entry by binary search over the entries' exclusive block prefixes.
 #include "hv_common.h"
@@ -20,7 +21,7 @@ constexpr int PT = 64;           // H_pre tiles: 64 (k) x 64 (i)
 
 struct PrepSizes {
   int ntk, nrb;                  // column tiles over Hd, row blocks over D
-  int colsum, rowmean, write, wct, fold, gemv;
+  int colsum, rowmean, write, wct, fold, gemv, rowsum;
 };
 
 __host__ __device__ inline PrepSizes prep_sizes(int D, int Hd, int fold) {
@@ -33,6 +34,7 @@ __host__ __device__ inline PrepSizes prep_sizes(int D, int Hd, int fold) {
   s.wct = ((D + Hd + 31) / 32) * ((D + 31) / 32);
   s.fold = fold ? (2 * Hd / 64) * ((D + 63) / 64) : 0;
   s.gemv = fold ? (2 * Hd + 15) / 16 : 0;
+  s.rowsum = ((fold ? 2 * Hd : Hd) + 3) / 4;
   return s;
 }
 
@@ -294,6 +296,24 @@ __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict
   }
 }
 
+// ------------------------------------------------------------------ phase 4
+// cs[n] = sum_k a1[n, k] over the values as stored (bf16-rounded in bf16 mode), so the
+// LN-after-GEMM epilogue rstd (x.a1 - mean cs) equals LN-before-GEMM on the same operand.
+template <typename T>
+__global__ void __launch_bounds__(256) k_pg4(const hv_mhc_prep_entry* __restrict__ tab, int count) {
+  const int ei = find_entry<hv_mhc_prep_entry, 3>(tab, count, blockIdx.x);
+  const hv_mhc_prep_entry& e = tab[ei];
+  const int rows = e.fold ? 2 * e.Hd : e.Hd, K = e.D;
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x - e.blk[3]) * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const T* p = (const T*)e.a1 + (long)r * K;
+  float acc = 0.f;
+  for (int k = lane; k < K; k += 64) acc += Elem<T>::load(p, k);
+  acc = wave_sum(acc);
+  if (lane == 0) e.cs[r] = acc;
+}
+
 // ------------------------------------------------------------------ weight prep group
 constexpr int WP_CAST_CHUNK = 4096;   // elements per block (cast)
 constexpr int WP_CONV_ROWS = 4;       // output channels per block (conv), one wave each
@@ -369,11 +389,12 @@ extern "C" size_t hv_mhc_prep_scratch_floats(int D, int Hd) {
   return (size_t)D * Hd + Hd + (D + Hd) + 2L * s.nrb * Hd;
 }
 
-extern "C" void hv_mhc_prep_blocks(int D, int Hd, int fold, int* out3) {
+extern "C" void hv_mhc_prep_blocks(int D, int Hd, int fold, int* out4) {
   const PrepSizes s = prep_sizes(D, Hd, fold);
-  out3[0] = s.colsum + s.rowmean;
-  out3[1] = s.write + s.wct;
-  out3[2] = s.fold + s.gemv;
+  out4[0] = s.colsum + s.rowmean;
+  out4[1] = s.write + s.wct;
+  out4[2] = s.fold + s.gemv;
+  out4[3] = s.rowsum;
 }
 
 extern "C" int hv_mhc_prep_group(const hv_mhc_prep_entry* tab, int count, int dtype, const int* totals,
@@ -384,6 +405,7 @@ extern "C" int hv_mhc_prep_group(const hv_mhc_prep_entry* tab, int count, int dt
   if (totals[0] > 0) k_pg1<<<totals[0], 256, 0, s>>>(tab, count);
   if (totals[1] > 0) HV_DISPATCH(dtype, (k_pg2<T><<<totals[1], 256, 0, s>>>(tab, count)));
   if (totals[2] > 0) HV_DISPATCH(dtype, (k_pg3<T><<<totals[2], 256, 0, s>>>(tab, count)));
+  if (totals[3] > 0) HV_DISPATCH(dtype, (k_pg4<T><<<totals[3], 256, 0, s>>>(tab, count)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -44,7 +44,7 @@ class GemmDesc(C.Structure):
                 ("residual", vp), ("ldr", i64), ("r_dtype", i32), ("r_mod", i32),
                 ("conv_n", i32), ("conv_h", i32), ("conv_w", i32), ("conv_c", i32),
                 ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
-                ("conv_oh", i32), ("conv_ow", i32)]
+                ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp)]
 
 
 class MhcFusedArgs(C.Structure):
@@ -55,8 +55,8 @@ class MhcFusedArgs(C.Structure):
 
 class MhcPrepEntry(C.Structure):
     _fields_ = [("h_pre_raw", vp), ("h_post_raw", vp), ("h_res", vp), ("gamma_pre", vp), ("beta_pre", vp),
-                ("w1", vp), ("b1", vp), ("a1", vp), ("c1", vp), ("wct", vp), ("scratch", vp),
-                ("D", i32), ("Hd", i32), ("fold", i32), ("pad_", i32), ("blk", i32 * 3), ("pad2_", i32)]
+                ("w1", vp), ("b1", vp), ("a1", vp), ("c1", vp), ("wct", vp), ("scratch", vp), ("cs", vp),
+                ("D", i32), ("Hd", i32), ("fold", i32), ("pad_", i32), ("blk", i32 * 4)]
 
 
 class WprepEntry(C.Structure):
@@ -101,6 +101,8 @@ _SIGS = {
     "hv_interp_linear": ([vp, i32, i32, i32, vp, vp], i32),
     "hv_vit_tokens": ([i32, vp, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "hv_attention": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
+    "hv_attention_work_elems": ([i32, i32, i32, i32], C.c_size_t),
+    "hv_attention_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
 }

@@ -90,6 +90,7 @@ class MhcPlan:
     wct: torch.Tensor
     g_post: torch.Tensor
     b_post: torch.Tensor
+    cs: Optional[torch.Tensor] = None   # row sums of b1 as stored: LayerNorm applied after GEMM1
 
 
 def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.dtype) -> MhcPlan:
@@ -121,9 +122,9 @@ def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = N
         return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post, residual)
     mean, rstd = ops.row_stats(x2, 1e-5)
     if p.fold:
-        h1 = ops.gemm(x2, p.b1, bias=p.c1, act="gelu", a_mean=mean, a_rstd=rstd)
+        h1 = ops.gemm(x2, p.b1, bias=p.c1, act="gelu", a_mean=mean, a_rstd=rstd, b_colsum=p.cs)
     else:
-        e = ops.gemm(x2, p.b1, bias=p.c1, a_mean=mean, a_rstd=rstd)
+        e = ops.gemm(x2, p.b1, bias=p.c1, a_mean=mean, a_rstd=rstd, b_colsum=p.cs)
         h1 = ops.gemm(e, p.w1, bias=p.bias1, act="gelu")
     h2 = ops.gemm(h1, p.w2, bias=p.bias2, act="gelu")
     yc = ops.gemm(x2, p.wct, a2=h2, out_dtype=torch.float32)

@@ -35,11 +35,12 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
          act: str = "none", alpha: float = 1.0, residual: Optional[Tensor] = None,
          a_mean: Optional[Tensor] = None, a_rstd: Optional[Tensor] = None,
          a2: Optional[Tensor] = None, out_dtype: Optional[torch.dtype] = None,
-         out: Optional[Tensor] = None, residual_mod: int = 0) -> Tensor:
+         out: Optional[Tensor] = None, residual_mod: int = 0, b_colsum: Optional[Tensor] = None) -> Tensor:
     """C = act((a' @ b^T) * alpha * scale + bias) + residual.
 
     a: [M, K1] (row stride may exceed K1), b: [N, K] with K = K1 (+ K2 if a2 [M, K2] given).
-    a_mean/a_rstd: per-row LayerNorm statistics applied to a while it is loaded.
+    a_mean/a_rstd: per-row LayerNorm statistics of a (applied on load, or -- given
+    b_colsum = b.sum(1) in fp32 -- after the product as rstd * (acc - mean * b_colsum)).
     """
     _cuda(a, b)
     if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
@@ -65,6 +66,7 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
     d.B, d.ldb = b.data_ptr(), b.stride(0)
     d.C, d.ldc, d.c_dtype = out.data_ptr(), out.stride(0), dtype_code(out.dtype)
     d.a_mean, d.a_rstd = ptr(a_mean), ptr(a_rstd)
+    d.b_colsum = ptr(b_colsum) if a_mean is not None else None
     d.scale, d.bias = ptr(scale), ptr(bias)
     d.act = L.ACT[act]
     d.alpha = alpha
@@ -422,6 +424,12 @@ def attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
     n, Lq, D = q.shape
     hd = D // heads
     o = torch.empty_like(q)
+    if q.dtype == torch.bfloat16 and hd == 32:
+        vt = torch.empty(L.lib().hv_attention_work_elems(n, Lq, heads, hd), device=q.device, dtype=q.dtype)
+        check(L.lib().hv_attention_mfma(_contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
+                                        _contig(v, "v").data_ptr(), vt.data_ptr(), o.data_ptr(), n, Lq, heads, hd,
+                                        hd ** -0.5, stream_ptr()), "hv_attention_mfma")
+        return o
     check(L.lib().hv_attention(dtype_code(q.dtype), _contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
                                _contig(v, "v").data_ptr(), o.data_ptr(), n, Lq, heads, hd, hd ** -0.5,
                                stream_ptr()), "hv_attention")

@@ -7,7 +7,7 @@ does all of it in a fixed, small number of launches over device tables:
 
     Sinkhorn group   2*iters+3 launches  (hv_sinkhorn_group_forward; histories written
                                           straight into each module's convergence_history)
-    mHC prep group   3 launches          (hv_mhc_prep_group: Gc/u/Wc^T + fold GEMM + c1)
+    mHC prep group   4 launches          (hv_mhc_prep_group: Gc/u/Wc^T + fold GEMM + c1 + row sums)
     weight prep      1 launch            (hv_wprep_group: casts + Conv(+BN) reorder/fold)
 
 and publishes the results into the forward's RunCtx.plans under the same keys the
@@ -67,8 +67,8 @@ class PrepProgram:
             total += (lib.hv_mhc_prep_scratch_floats(m.input_dim, m.hidden_dim) + 63) // 64 * 64
         self.scratch = torch.empty(max(total, 1), device=device, dtype=torch.float32)
         self.mout: List[Tuple] = []
-        tot = [0, 0, 0]
-        blk = (L.i32 * 3)()
+        tot = [0, 0, 0, 0]
+        blk = (L.i32 * 4)()
         self.wcasts: List[Tuple[torch.Tensor, torch.Tensor]] = []     # (src, dst) for the weight group
         for i, m in enumerate(self.mods):
             D, Hd = m.input_dim, m.hidden_dim
@@ -76,6 +76,7 @@ class PrepProgram:
             a1 = torch.empty((2 * Hd, D) if fold else (Hd, D), device=device, dtype=dtype)
             c1 = torch.empty(2 * Hd if fold else Hd, device=device, dtype=torch.float32)
             wct = torch.empty((D, D + Hd), device=device, dtype=dtype)
+            cs = torch.empty(a1.shape[0], device=device, dtype=torch.float32)
             w1 = _param(m.mlp[0].weight, "mlp[0].weight")
             w2 = _param(m.mlp[3].weight, "mlp[3].weight")
             w2c = self._cast_target(w2)
@@ -90,13 +91,14 @@ class PrepProgram:
             e.b1 = _param(m.mlp[0].bias, "mlp[0].bias").data_ptr()
             e.a1, e.c1, e.wct = a1.data_ptr(), c1.data_ptr(), wct.data_ptr()
             e.scratch = self.scratch.data_ptr() + 4 * offs[i]
+            e.cs = cs.data_ptr()
             e.D, e.Hd, e.fold = D, Hd, int(fold)
             lib.hv_mhc_prep_blocks(D, Hd, int(fold), blk)
-            for p in range(3):
+            for p in range(4):
                 e.blk[p] = tot[p]
                 tot[p] += blk[p]
-            self.mout.append((fold, a1, c1, wct, w1c, w2c))
-        self.mtotals = (L.i32 * 3)(*tot)
+            self.mout.append((fold, a1, c1, wct, w1c, w2c, cs))
+        self.mtotals = (L.i32 * 4)(*tot)
         self.mtable = _upload(self.mentries, device)
         # ---- weight prep (casts of the mHC MLP weights + registered convs / linears)
         self.convs: Dict[int, Tuple] = {}
@@ -198,11 +200,11 @@ class PrepProgram:
         if self.wtable is not None:
             check(lib.hv_wprep_group(self.wtable.data_ptr(), len(self.wentries), self.wtotal, stream_ptr()),
                   "hv_wprep_group")
-        for m, (fold, a1, c1, wct, w1c, w2c) in zip(self.mods, self.mout):
+        for m, (fold, a1, c1, wct, w1c, w2c, cs) in zip(self.mods, self.mout):
             ctx.plans[id(m)] = MhcPlan(
                 D=m.input_dim, Hd=m.hidden_dim, fold=fold, dtype=self.dtype, b1=a1, c1=c1,
                 w1=w1c, bias1=None if fold else m.mlp[0].bias.detach(), w2=w2c, bias2=m.mlp[3].bias.detach(),
-                wct=wct, g_post=m.norm_post.weight.detach(), b_post=m.norm_post.bias.detach())
+                wct=wct, g_post=m.norm_post.weight.detach(), b_post=m.norm_post.bias.detach(), cs=cs)
         for conv, bn, w, scale, bias_out, val in self.convs.values():
             ctx.plans[("conv", id(conv))] = val
         for lin, val in self.linears.values():

@@ -90,6 +90,9 @@ typedef struct hv_gemm_desc {
   /* implicit-GEMM convolution: A is an NHWC image [conv_n, conv_h, conv_w, conv_c];
      K = conv_k*conv_k*conv_c ordered (kh, kw, c); M = conv_n*conv_oh*conv_ow */
   int conv_n, conv_h, conv_w, conv_c, conv_k, conv_stride, conv_pad, conv_oh, conv_ow;
+  /* with a_mean/a_rstd: b_colsum[n] = sum_k B[n,k] lets the LDS-DMA kernel apply the
+     LayerNorm after the product, rstd (acc - mean colsum) (exact); NULL: LN on load */
+  const float* b_colsum;
 } hv_gemm_desc;
 
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
@@ -169,6 +172,7 @@ int hv_cast(const float* x, long n, int y_dtype, void* y, hv_stream_t stream);
  *   phase 1: column partials of g.s(H_pre_raw), b.s(H_pre_raw); row means of H_res, H_post
  *   phase 2: Gc (fp32 scratch [D,Hd] when folding; Gc^T [Hd,D] in dtype otherwise), u, Wc^T
  *   phase 3 (fold sites): A1^T = W1 Gc^T [2Hd, D] (MFMA, dtype) and c1 = W1 u + b1 (fp32)
+ *   phase 4: cs = row sums of a1 as stored (hv_gemm_desc.b_colsum of the first GEMM)
  * Unfolded sites get c1 = u.  blk[] are exclusive per-phase block prefixes filled by the
  * host with hv_mhc_prep_blocks(); totals are the sums.
  * ------------------------------------------------------------------------------------ */
@@ -184,16 +188,16 @@ typedef struct hv_mhc_prep_entry {
   float* c1;                /* fold: [2Hd]; else u [Hd] */
   void* wct;                /* [D, D+Hd] (dtype) */
   float* scratch;           /* hv_mhc_prep_scratch_floats(D, Hd) */
+  float* cs;                /* [rows of a1] fp32 row sums of a1 as stored (LN-after-GEMM) */
   int D, Hd, fold, pad_;
-  int blk[3];
-  int pad2_;
+  int blk[4];
 } hv_mhc_prep_entry;
 
 size_t hv_mhc_prep_scratch_floats(int D, int Hd);
-/* blocks of each phase for one entry (out3[0..2]) */
-void hv_mhc_prep_blocks(int D, int Hd, int fold, int* out3);
+/* blocks of each phase for one entry (out4[0..3]) */
+void hv_mhc_prep_blocks(int D, int Hd, int fold, int* out4);
 int hv_mhc_prep_group(const hv_mhc_prep_entry* dev_table, int count, int dtype,
-                      const int* totals3 /* host */, hv_stream_t stream);
+                      const int* totals4 /* host */, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Grouped weight preparation: fp32 parameters -> GEMM operands in one launch.
@@ -264,6 +268,12 @@ int hv_vit_tokens(int dtype, const void* x, const float* cls, const float* pos, 
 /* out = softmax(q k^T * sm_scale) v per (batch, head); q/k/v/out token-major [n, L, heads*hd] */
 int hv_attention(int dtype, const void* q, const void* k, const void* v, void* out,
                  int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream);
+/* bf16 MFMA attention for hd == 32 (flash-style online softmax, P rounded to bf16 as the
+   MFMA operand).  vt_work: hv_attention_work_elems() bf16 elements (V transposed per head,
+   keys zero-padded to a multiple of 32). */
+size_t hv_attention_work_elems(int n, int L, int heads, int hd);
+int hv_attention_mfma(const void* q, const void* k, const void* v, void* vt_work, void* out,
+                      int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream);
 /* y[b, c] = x[b, 0, c]  (strided row gather) */
 int hv_gather_rows(int dtype, const void* x, long stride_rows, int n, int c, void* y,
                    hv_stream_t stream);

@@ -120,6 +120,25 @@ def test_gemm_ln_prologue_and_concat(gpu_device, prec):
     assert rel_err(out2, torch.cat([x, h], 1).float() @ bc.float().T) < TOL[prec]
 
 
+@pytest.mark.parametrize("T,D,N", [(200, 64, 96), (1000, 256, 1024), (77, 128, 40)])
+def test_gemm_ln_epilogue_equals_prologue(gpu_device, T, D, N):
+    """LDS-DMA kernel with the LayerNorm applied after the product, rstd (x.b - mean colsum(b)),
+    against the LN-on-load register-staged path and a torch reference (bf16 operands)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(T + D)
+    x = (torch.randn(T, D, generator=g) * 2 + 3).to(torch.bfloat16).to(gpu_device)   # large mean
+    b = (torch.randn(N, D, generator=g) / 8).to(torch.bfloat16).to(gpu_device)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    mean, rstd = ops.row_stats(x, 1e-5)
+    cs = b.float().sum(1).contiguous()
+    epi = ops.gemm(x, b, bias=bias, act="gelu", a_mean=mean, a_rstd=rstd, b_colsum=cs, out_dtype=torch.float32)
+    pro = ops.gemm(x, b, bias=bias, act="gelu", a_mean=mean, a_rstd=rstd, out_dtype=torch.float32)
+    z = F.layer_norm(x.float().cpu(), (D,), eps=1e-5)
+    ref = F.gelu(z @ b.float().cpu().T + bias.cpu())
+    assert rel_err(epi, ref) < 1e-4            # exact operand: better than the bf16-rounded z of `pro`
+    assert rel_err(pro, ref) < TOL["bf16"]
+
+
 def test_gemm_residual_mod(gpu_device):
     ops = _ops()
     a = torch.randn(6 * 10, 32)
@@ -230,7 +249,7 @@ def test_norms_and_pointwise_vs_torch(gpu_device, prec):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("L", [1, 50, 257, 401])
+@pytest.mark.parametrize("L", [1, 33, 50, 257, 401, 1025])
 def test_attention_vs_torch(gpu_device, prec, L):
     ops = _ops()
     dt = DT[prec]
