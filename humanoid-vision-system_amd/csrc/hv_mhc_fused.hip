@@ -1,70 +1,70 @@
 // Fused mHC token chain (gfx950, bf16 MFMA), replacing the six launches of the unfused path
-// (row stats, 3 GEMMs, LayerNorm) for every site with D <= 256 and hidden width <= 512:
+// (row stats, 3 GEMMs, LayerNorm) for the mHC sites with D <= 128:
 //
 //   z   = (x - mean) * rstd                    (LN_pre core; gamma/beta folded into A1/c1)
-//   h1  = GELU(z A1 + c1)          [BM x 2HD]  produced KC columns at a time, never stored
-//   h2  = GELU(h1 W2^T + b2)       [BM x HD]   accumulated in registers over the 2HD chunks
-//   y   = [x | h2] Wc              [BM x D]    Wc = centred [H_res ; H_post]
+//   h1  = GELU(z A1 + c1)          [T x 2HD]   produced KC = 32 columns at a time
+//   h2  = GELU(h1 W2^T + b2)       [T x HD]    accumulated in registers over the 2HD chunks
+//   y   = [x | h2] Wc              [T x D]     Wc = centred [H_res ; H_post]
 //   out = LN_post(y) * g2 + b2' (+ residual)   computed from the GEMM3 accumulators
 //
 // Reference: ManifoldHyperConnection.forward (manifold_layers.py:223-280); the algebra
-// (fold + centring) is documented in hv_amd/manifold.py and DESIGN.md.  Per token tile only x
-// (D*2 bytes/token) is read and out written: the [T, 2HD] and [T, HD] intermediates of the
-// unfused chain never reach HBM.
+// (fold + centring) is in hv_amd/manifold.py and DESIGN.md.  Only x is read and out written:
+// the [T, 2HD] and [T, HD] intermediates never leave the registers.
 //
-// Weights are not staged through LDS: every weight element a workgroup needs is consumed by
-// exactly one lane as an MFMA B fragment, so each lane loads its 16-byte fragments straight
-// from L2 into a 2-slot register ring (chunk c+1 is in flight while chunk c computes).  LDS
-// holds the x/z tile, a double-buffered h1 chunk (one barrier per chunk), h2 and a small
-// LayerNorm exchange.  GEMM1 and GEMM2 are computed transposed (weights as the MFMA A operand)
-// so each lane ends with 4 consecutive hidden units of one token: GELU + bf16 pack + one
-// 8-byte LDS store per tile.  GELU is hv_gelu_fast (|err| <= 2.6e-5, below bf16 resolution).
+// Layout of the work: every wave owns TPW = 16*TB tokens end to end.  All three products are
+// computed TRANSPOSED (weights as the MFMA A operand, activations as B), so a lane always
+// holds 4 consecutive hidden units of ONE token; two such 16-wide tiles are exactly the B
+// fragment of the next product when its 32-deep contraction runs in the permuted order
+// {4g..4g+3, 16+4g..16+4g+3} (lane group g) -- which the weight (A) fragment then also uses.
+// So h1 -> GEMM2 and h2 -> GEMM3 go register to register, no LDS, no cross-wave exchange.
+// The weights are the only shared data: per 32-wide chunk of 2HD, the A1^T rows and the W2
+// columns of that chunk are DMA'd (global_load_lds, 16 B/lane, XOR-swizzled rows) into a
+// double-buffered LDS stage shared by the 8 waves -- one barrier per chunk -- and Wc^T is
+// streamed the same way for GEMM3.  GELU is hv_gelu_fast (|err| <= 2.6e-5, below bf16).
 #include "hv_common.h"
 
 namespace {
-
-template <int D, int HD, int NW>
-struct Cfg {
-  static constexpr int NT = 64 * NW;
-  static constexpr int BM = 4096 * NW / HD;       // acc2: BM x HD/NW per wave = 16 tiles (64 regs)
-  static constexpr int KC = 32;                   // 2HD chunk per step (one MFMA k-step)
-  static constexpr int NCH = 2 * HD / KC;
-  static constexpr int NV = (D + 63) / 64;        // row values per lane in row-wise passes
-  static constexpr int XS = D * 2 + 16;           // x / z row stride (bytes), == 16 mod 64
-  static constexpr int H1S = KC * 2 + 16;
-  static constexpr int H2S = HD * 2 + 16;
-  // GEMM1: (BM/16) x (KC/16) tiles over NW waves
-  static constexpr int T1W = (BM / 16) * (KC / 16) / NW;
-  // GEMM2: wave owns HD/NW columns x all BM rows
-  static constexpr int R2 = BM / 16, C2 = HD / NW / 16;
-  // GEMM3: (BM/16) row tiles x (D/16) col tiles; CG column groups per row tile
-  static constexpr int CG = NW > BM / 16 ? NW / (BM / 16) : 1;
-  static constexpr int RT3 = (BM / 16) * CG / NW;
-  static constexpr int CT3 = (D / 16) / CG;
-  static constexpr int KS3 = (D + HD) / 32;
-  // LDS carve
-  static constexpr int OFF_X = 0;
-  static constexpr int OFF_Z = BM * XS;
-  static constexpr int OFF_H1 = 2 * BM * XS;      // 2 buffers
-  static constexpr int OFF_H2 = OFF_H1 + 2 * BM * H1S;
-  static constexpr int OFF_RED = OFF_H2 + BM * H2S;   // [BM][CG] floats
-  static constexpr int LDS = OFF_RED + BM * CG * 4;
-  static_assert(R2 * C2 == 16, "acc2 tiling");
-  static_assert(T1W >= 1 && (BM / 16) * (KC / 16) % NW == 0, "gemm1 tiling");
-  static_assert(RT3 >= 1 && CT3 >= 1 && (D / 16) % CG == 0, "gemm3 tiling");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
-__device__ __forceinline__ uint4 lds16(const unsigned char* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ uint4 gl16(const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); }
 
 __device__ __forceinline__ f32x4 mfma(uint4 a, uint4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
                                                  c, 0, 0, 0);
 }
 
-template <int D, int HD, int NW>
-__global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
+__device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+#else
+  (void)src; (void)lds_wave_base;
+#endif
+}
+
+template <int D, int HD, int TB_>
+struct Cfg {
+  static constexpr int NW = 8, NT = 512;
+  static constexpr int TB = TB_;                   // 16-token blocks per wave (acc2: HT*TB tiles)
+  static constexpr int TPW = 16 * TB, BM = NW * TPW;
+  static constexpr int KC = 32, NCH = 2 * HD / KC;
+  static constexpr int HT = HD / 16, DT = D / 16, KS1 = D / 32;
+  static constexpr int CPA = D / 8;                // 16-B chunks per A1^T row (2D bytes)
+  static constexpr int A1B = KC * D * 2;           // bytes of one A1^T chunk  [KC rows x D]
+  static constexpr int W2B = HD * 64;              // bytes of one W2 chunk    [HD rows x 32 k]
+  static constexpr int STAGE = A1B + W2B;
+  static constexpr int WCB = D * 64;               // bytes of one Wc^T k-chunk [D rows x 32 k]
+  static constexpr int KS3 = (D + HD) / 32;
+  static constexpr int LDS = 2 * (STAGE > WCB ? STAGE : WCB);
+  static_assert(HD % 32 == 0 && D % 32 == 0 && TB >= 1, "shape");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// 64-byte rows (W2 / Wc^T chunks): 16-B chunk c of row r lives at c ^ ((r >> 2) & 3), which
+// makes the permuted 8-byte fragment reads (ds_read_b64, 32-lane groups) conflict-free.
+__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
+// A1^T rows (2D bytes, CPA chunks): chunk c of row r at c ^ (r & (CPA - 1)).
+template <int CPA>
+__device__ __forceinline__ int swzA(int r, int c) { return c ^ (r & (CPA - 1)); }
+
+template <int D, int HD, int TB_, int MINB>
+__global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
     const unsigned short* __restrict__ x, int T,
     const unsigned short* __restrict__ a1t,   // [2HD, D]
     const float* __restrict__ c1,             // [2HD]
@@ -74,239 +74,238 @@ __global__ void __launch_bounds__(64 * NW) mhc_fused_kernel(
     const float* __restrict__ g_post, const float* __restrict__ b_post,
     const unsigned short* __restrict__ res,   // optional [T, D], added after LN_post
     unsigned short* __restrict__ out) {
-  using C = Cfg<D, HD, NW>;
-  constexpr int BM = C::BM, KC = C::KC;
+  using C = Cfg<D, HD, TB_>;
+  constexpr int TB = C::TB, KC = C::KC;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const long t0 = (long)blockIdx.x * BM;
+  const long tw = (long)blockIdx.x * C::BM + w * C::TPW;     // first token of this wave
 
-  // ---------------- weight-fragment ring (registers), 2 slots
-  uint4 fb1[2][C::T1W][D / 32];      // GEMM1 A fragments (rows of A1^T)
-  uint4 fb2[2][C::C2];               // GEMM2 A fragments (rows of W2)
-  float4 cb1[2][C::T1W];             // c1 for the 4 hidden rows a lane holds per GEMM1 tile
-  auto load_chunk = [&](int slot, int ch) {
+  // ---- weight chunk DMA: A1^T rows [ch*KC, +KC) and W2 columns [ch*KC, +KC) -> stage st
+  auto issue_chunk = [&](int ch, int st) {
+    unsigned char* sa = smem + st * C::STAGE;
+    unsigned char* sw = sa + C::A1B;
 #pragma unroll
-    for (int i = 0; i < C::T1W; ++i) {
-      const int t = w * C::T1W + i, ct = t % (KC / 16);
-      const int n = ch * KC + ct * 16 + fr;
-#pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks) fb1[slot][i][ks] = gl16(a1t + (long)n * D + ks * 32 + fg * 8);
-      cb1[slot][i] = *reinterpret_cast<const float4*>(c1 + ch * KC + ct * 16 + fg * 4);
+    for (int p0 = 0; p0 < KC * C::CPA; p0 += 512) {
+      const int p = p0 + tid;
+      if (p0 + (tid & ~63) < KC * C::CPA) {                   // wave-uniform
+        const int r = p / C::CPA, pc = p % C::CPA;
+        dma16(a1t + (long)(ch * KC + r) * D + swzA<C::CPA>(r, pc) * 8, sa + (p - lane) * 16);
+      }
     }
 #pragma unroll
-    for (int b = 0; b < C::C2; ++b)
-      fb2[slot][b] = gl16(w2 + (long)(w * (HD / NW) + b * 16 + fr) * (2 * HD) + ch * KC + fg * 8);
+    for (int p0 = 0; p0 < HD * 4; p0 += 512) {
+      const int p = p0 + tid;
+      if (p0 + (tid & ~63) < HD * 4) {
+        const int r = p >> 2, pc = p & 3;
+        dma16(w2 + (long)r * (2 * HD) + ch * KC + swz64(r, pc) * 8, sw + (p - lane) * 16);
+      }
+    }
   };
-  load_chunk(0, 0);
-  load_chunk(1, 1);
-
-  // ---------------- phase 0: x tile -> LDS; LN_pre -> z (bf16)
-  {
-    constexpr int CH = D / 8;
-    for (int c = tid; c < BM * CH; c += C::NT) {
-      const int r = c / CH, k = c % CH;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (t0 + r < T) v = gl16(x + (t0 + r) * D + k * 8);
-      *reinterpret_cast<uint4*>(smem + C::OFF_X + r * C::XS + k * 16) = v;
+  auto issue_wc = [&](int ks, int st) {
+    unsigned char* sb = smem + st * C::WCB;
+#pragma unroll
+    for (int p0 = 0; p0 < D * 4; p0 += 512) {
+      const int p = p0 + tid;
+      if (p0 + (tid & ~63) < D * 4) {
+        const int r = p >> 2, pc = p & 3;
+        dma16(wct + (long)r * (D + HD) + ks * 32 + swz64(r, pc) * 8, sb + (p - lane) * 16);
+      }
     }
-  }
-  __syncthreads();
-  for (int r = w; r < BM; r += NW) {
-    const unsigned short* xr = (const unsigned short*)(smem + C::OFF_X + r * C::XS);
-    float v[C::NV];
+  };
+
+  issue_chunk(0, 0);
+
+  // ---- x fragments (B operand, standard k order) and LN_pre -> z fragments
+  // (x is re-read from L2 for GEMM3 rather than held across the chunk loop)
+  uint4 zf[TB][C::KS1];
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb) {
+    const long tok = min(tw + tb * 16 + fr, (long)T - 1);
+    uint4 xf[C::KS1];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < C::NV; ++i) {
-      const int j = lane + 64 * i;
-      v[i] = j < D ? bf2f(xr[j]) : 0.f;
-      s += v[i];
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      xf[ks] = *reinterpret_cast<const uint4*>(x + tok * D + ks * 32 + fg * 8);
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __uint_as_float(wv[e] << 16) + __uint_as_float(wv[e] & 0xffff0000u);
     }
-    const float mu = wave_sum(s) / D;
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < C::NV; ++i) {
-      const int j = lane + 64 * i;
-      v[i] = j < D ? v[i] - mu : 0.f;
-      q += v[i] * v[i];
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(wv[e] << 16) - mu, b = __uint_as_float(wv[e] & 0xffff0000u) - mu;
+        q += a * a + b * b;
+      }
     }
-    const float rs = rsqrtf(wave_sum(q) / D + 1e-5f);
-    unsigned short* zr = (unsigned short*)(smem + C::OFF_Z + r * C::XS);
-#pragma unroll
-    for (int i = 0; i < C::NV; ++i) {
-      const int j = lane + 64 * i;
-      if (j < D) zr[j] = f2bf(v[i] * rs);
-    }
-  }
-  __syncthreads();
-
-  // ---------------- phase 1: 2HD chunks
-  f32x4 acc2[C::R2][C::C2];
-#pragma unroll
-  for (int a = 0; a < C::R2; ++a)
-#pragma unroll
-    for (int b = 0; b < C::C2; ++b) acc2[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int ch = 0; ch < C::NCH; ++ch) {
-    const int slot = ch & 1;
-    unsigned char* h1 = smem + C::OFF_H1 + slot * BM * C::H1S;
-    // GEMM1 transposed (h1^T = A1^T z^T): a lane ends with 4 consecutive hidden units of one
-    // token, i.e. one 8-byte row segment of h1 -> one ds_write_b64 of two packed bf16 pairs
-#pragma unroll
-    for (int i = 0; i < C::T1W; ++i) {
-      const int t = w * C::T1W + i, rt = t / (KC / 16), ct = t % (KC / 16);
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < D / 32; ++ks)
-        acc = mfma(fb1[slot][i][ks], lds16(smem + C::OFF_Z + (rt * 16 + fr) * C::XS + ks * 64 + fg * 16), acc);
-      const float4 bias = cb1[slot][i];
-      const uint32_t lo = pack_bf16x2(hv_gelu_fast(acc[0] + bias.x), hv_gelu_fast(acc[1] + bias.y));
-      const uint32_t hi = pack_bf16x2(hv_gelu_fast(acc[2] + bias.z), hv_gelu_fast(acc[3] + bias.w));
-      *reinterpret_cast<uint2*>(h1 + (rt * 16 + fr) * C::H1S + (ct * 16 + fg * 4) * 2) = make_uint2(lo, hi);
-    }
-    __syncthreads();
-    uint4 fa[C::R2];
-#pragma unroll
-    for (int a = 0; a < C::R2; ++a) fa[a] = lds16(h1 + (a * 16 + fr) * C::H1S + fg * 16);
-    // GEMM2 transposed too (acc2[a][b] holds h2^T: 4 hidden units x 1 token per lane)
-#pragma unroll
-    for (int b = 0; b < C::C2; ++b)
-#pragma unroll
-      for (int a = 0; a < C::R2; ++a) acc2[a][b] = mfma(fb2[slot][b], fa[a], acc2[a][b]);
-    if (ch + 2 < C::NCH) load_chunk(slot, ch + 2);
-  }
-
-  // ---------------- phase 2: h2 = GELU(acc2 + b2) -> LDS (row-major [token][hidden])
-#pragma unroll
-  for (int b = 0; b < C::C2; ++b) {
-    const int col = w * (HD / NW) + b * 16 + fg * 4;
-    const float4 bias = *reinterpret_cast<const float4*>(b2 + col);
-#pragma unroll
-    for (int a = 0; a < C::R2; ++a) {
-      const uint32_t lo = pack_bf16x2(hv_gelu_fast(acc2[a][b][0] + bias.x), hv_gelu_fast(acc2[a][b][1] + bias.y));
-      const uint32_t hi = pack_bf16x2(hv_gelu_fast(acc2[a][b][2] + bias.z), hv_gelu_fast(acc2[a][b][3] + bias.w));
-      *reinterpret_cast<uint2*>(smem + C::OFF_H2 + (a * 16 + fr) * C::H2S + col * 2) = make_uint2(lo, hi);
-    }
-  }
-  __syncthreads();
-
-  // ---------------- phase 3: y = [x | h2] Wc ; wave = (row-tile group, column group)
-  const int rg = w / C::CG, cg = w % C::CG;
-  f32x4 acc3[C::RT3][C::CT3];
-#pragma unroll
-  for (int r = 0; r < C::RT3; ++r)
-#pragma unroll
-    for (int c = 0; c < C::CT3; ++c) acc3[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 fw[2][C::CT3];
-  auto load_wc = [&](int slot, int ks) {
-#pragma unroll
-    for (int c = 0; c < C::CT3; ++c)
-      fw[slot][c] = gl16(wct + (long)((cg * C::CT3 + c) * 16 + fr) * (D + HD) + ks * 32 + fg * 8);
-  };
-  load_wc(0, 0);
-  load_wc(1, 1);
-#pragma unroll
-  for (int ks = 0; ks < C::KS3; ++ks) {
-    const int slot = ks & 1;
-#pragma unroll
-    for (int r = 0; r < C::RT3; ++r) {
-      const int row = (rg * C::RT3 + r) * 16 + fr;
-      const uint4 fa = ks < D / 32 ? lds16(smem + C::OFF_X + row * C::XS + ks * 64 + fg * 16)
-                                   : lds16(smem + C::OFF_H2 + row * C::H2S + (ks - D / 32) * 64 + fg * 16);
-#pragma unroll
-      for (int c = 0; c < C::CT3; ++c) acc3[r][c] = mfma(fw[slot][c], fa, acc3[r][c]);   // transposed tile
-    }
-    if (ks + 2 < C::KS3) load_wc(slot, ks + 2);
-  }
-
-  // ---------------- phase 4: LN_post from the accumulators
-  // acc3[r][c] is a transposed tile: lane -> token (rg*RT3 + r)*16 + fr, columns
-  // (cg*CT3 + c)*16 + fg*4 .. +3.  A token's row = 4 lane groups x CT3 tiles (x CG waves).
-  float* red = (float*)(smem + C::OFF_RED);
-  float mu[C::RT3], rs[C::RT3];
-#pragma unroll
-  for (int r = 0; r < C::RT3; ++r) {
-    float sum = 0.f;
-#pragma unroll
-    for (int c = 0; c < C::CT3; ++c) sum += (acc3[r][c][0] + acc3[r][c][1]) + (acc3[r][c][2] + acc3[r][c][3]);
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    mu[r] = sum;
-  }
-  if constexpr (C::CG > 1) {
-#pragma unroll
-    for (int r = 0; r < C::RT3; ++r)
-      if (fg == 0) red[((rg * C::RT3 + r) * 16 + fr) * C::CG + cg] = mu[r];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < C::RT3; ++r) {
-      float sum = 0.f;
-#pragma unroll
-      for (int g = 0; g < C::CG; ++g) sum += red[((rg * C::RT3 + r) * 16 + fr) * C::CG + g];
-      mu[r] = sum;
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < C::RT3; ++r) {
-    mu[r] *= 1.0f / D;
-    float q = 0.f;
-#pragma unroll
-    for (int c = 0; c < C::CT3; ++c)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { const float dd = acc3[r][c][j] - mu[r]; q += dd * dd; }
     q += __shfl_xor(q, 16, 64);
     q += __shfl_xor(q, 32, 64);
-    rs[r] = q;
-  }
-  if constexpr (C::CG > 1) {
+    const float rs = rsqrtf(q * (1.0f / D) + 1e-5f);
 #pragma unroll
-    for (int r = 0; r < C::RT3; ++r)
-      if (fg == 0) red[((rg * C::RT3 + r) * 16 + fr) * C::CG + cg] = rs[r];
-    __syncthreads();
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+      uint32_t zv[4];
 #pragma unroll
-    for (int r = 0; r < C::RT3; ++r) {
-      float sum = 0.f;
-#pragma unroll
-      for (int g = 0; g < C::CG; ++g) sum += red[((rg * C::RT3 + r) * 16 + fr) * C::CG + g];
-      rs[r] = sum;
+      for (int e = 0; e < 4; ++e)
+        zv[e] = pack_bf16x2((__uint_as_float(wv[e] << 16) - mu) * rs, (__uint_as_float(wv[e] & 0xffff0000u) - mu) * rs);
+      zf[tb][ks] = make_uint4(zv[0], zv[1], zv[2], zv[3]);
     }
   }
-  float4 gp[C::CT3], bp[C::CT3];
+
+  // ---- GEMM1 + GEMM2 over the 2HD chunks
+  f32x4 acc2[C::HT][TB];
 #pragma unroll
-  for (int c = 0; c < C::CT3; ++c) {
-    gp[c] = *reinterpret_cast<const float4*>(g_post + (cg * C::CT3 + c) * 16 + fg * 4);
-    bp[c] = *reinterpret_cast<const float4*>(b_post + (cg * C::CT3 + c) * 16 + fg * 4);
-  }
+  for (int h = 0; h < C::HT; ++h)
 #pragma unroll
-  for (int r = 0; r < C::RT3; ++r) {
-    const float inv = rsqrtf(rs[r] * (1.0f / D) + 1e-5f);
-    const long row = t0 + (rg * C::RT3 + r) * 16 + fr;
-    if (row >= T) continue;
+    for (int tb = 0; tb < TB; ++tb) acc2[h][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    const int st = ch & 1;
+    const float4 cb0 = *reinterpret_cast<const float4*>(c1 + ch * KC + fg * 4);
+    const float4 cb1 = *reinterpret_cast<const float4*>(c1 + ch * KC + 16 + fg * 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                   // chunk ch landed; stage st^1 is free
+    if (ch + 1 < C::NCH) issue_chunk(ch + 1, st ^ 1);
+    const unsigned char* sa = smem + st * C::STAGE;
+    const unsigned char* sw = sa + C::A1B;
+
+    // GEMM1 (transposed): h1^T[hidden ct*16 + 4g + j][token] ; A = A1^T rows from LDS
+    uint4 hb[TB];
+    {
+      f32x4 g1[2][TB];
 #pragma unroll
-    for (int c = 0; c < C::CT3; ++c) {
-      const int col = (cg * C::CT3 + c) * 16 + fg * 4;
-      float v0 = (acc3[r][c][0] - mu[r]) * inv * gp[c].x + bp[c].x;
-      float v1 = (acc3[r][c][1] - mu[r]) * inv * gp[c].y + bp[c].y;
-      float v2 = (acc3[r][c][2] - mu[r]) * inv * gp[c].z + bp[c].z;
-      float v3 = (acc3[r][c][3] - mu[r]) * inv * gp[c].w + bp[c].w;
-      if (res) {
-        const uint2 q = *reinterpret_cast<const uint2*>(res + row * D + col);
-        v0 += __uint_as_float(q.x << 16);
-        v1 += __uint_as_float(q.x & 0xffff0000u);
-        v2 += __uint_as_float(q.y << 16);
-        v3 += __uint_as_float(q.y & 0xffff0000u);
+      for (int ct = 0; ct < 2; ++ct) {
+        const int r = ct * 16 + fr;
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) g1[ct][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < C::KS1; ++ks) {
+          const uint4 af = *reinterpret_cast<const uint4*>(sa + r * (2 * D) + swzA<C::CPA>(r, ks * 4 + fg) * 16);
+#pragma unroll
+          for (int tb = 0; tb < TB; ++tb) g1[ct][tb] = mfma(af, zf[tb][ks], g1[ct][tb]);
+        }
       }
-      *reinterpret_cast<uint2*>(out + row * D + col) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb)
+        hb[tb] = make_uint4(pack_bf16x2(hv_gelu_fast(g1[0][tb][0] + cb0.x), hv_gelu_fast(g1[0][tb][1] + cb0.y)),
+                            pack_bf16x2(hv_gelu_fast(g1[0][tb][2] + cb0.z), hv_gelu_fast(g1[0][tb][3] + cb0.w)),
+                            pack_bf16x2(hv_gelu_fast(g1[1][tb][0] + cb1.x), hv_gelu_fast(g1[1][tb][1] + cb1.y)),
+                            pack_bf16x2(hv_gelu_fast(g1[1][tb][2] + cb1.z), hv_gelu_fast(g1[1][tb][3] + cb1.w)));
+    }
+    // GEMM2 (transposed): acc2[ht] += W2[ht*16 + fr][perm k] . h1^T ; permuted k order
+#pragma unroll
+    for (int h = 0; h < C::HT; ++h) {
+      const int r = h * 16 + fr;
+      const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+      const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) acc2[h][tb] = mfma(af, hb[tb], acc2[h][tb]);
+      if ((h & 7) == 7) __builtin_amdgcn_sched_barrier(0);   // bound the fragments in flight
+    }
+  }
+
+  // ---- GEMM3 (transposed): y^T[d][token] = Wc^T[d][k] . [x | h2]^T, Wc^T streamed via LDS
+  f32x4 acc3[C::DT][TB];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();                                     // every wave is done with the chunk stages
+  issue_wc(0, 0);
+#pragma unroll
+  for (int ks = 0; ks < C::KS3; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ks + 1 < C::KS3) issue_wc(ks + 1, (ks + 1) & 1);
+    const unsigned char* sb = smem + (ks & 1) * C::WCB;
+    uint4 xg[TB], h2f[TB];
+    if (ks < C::KS1) {
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb)
+        xg[tb] = *reinterpret_cast<const uint4*>(x + min(tw + tb * 16 + fr, (long)T - 1) * D + ks * 32 + fg * 8);
+    } else {
+      // h2 = GELU(acc2 + b2) for hidden [32s, 32s+32): two transposed tiles -> one B fragment
+      // in the permuted k order, built just before use (acc2 tiles die here)
+      const int s2 = ks - C::KS1;
+      const float4 ba = *reinterpret_cast<const float4*>(b2 + s2 * 32 + fg * 4);
+      const float4 bb = *reinterpret_cast<const float4*>(b2 + s2 * 32 + 16 + fg * 4);
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) {
+        const f32x4 p = acc2[ks >= C::KS1 ? 2 * s2 : 0][tb], q = acc2[ks >= C::KS1 ? 2 * s2 + 1 : 0][tb];
+        h2f[tb] = make_uint4(pack_bf16x2(hv_gelu_fast(p[0] + ba.x), hv_gelu_fast(p[1] + ba.y)),
+                             pack_bf16x2(hv_gelu_fast(p[2] + ba.z), hv_gelu_fast(p[3] + ba.w)),
+                             pack_bf16x2(hv_gelu_fast(q[0] + bb.x), hv_gelu_fast(q[1] + bb.y)),
+                             pack_bf16x2(hv_gelu_fast(q[2] + bb.z), hv_gelu_fast(q[3] + bb.w)));
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int r = dt * 16 + fr;
+      if (ks < C::KS1) {                               // x part: standard k order
+        const uint4 af = *reinterpret_cast<const uint4*>(sb + r * 64 + swz64(r, fg) * 16);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, xg[tb], acc3[dt][tb]);
+      } else {                                         // h2 part: permuted k order
+        const uint2 lo = *reinterpret_cast<const uint2*>(sb + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(sb + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, h2f[tb], acc3[dt][tb]);
+      }
+    }
+  }
+
+  // ---- LN_post per token (lane: token tb*16 + fr, columns dt*16 + 4g + j) + residual
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb) {
+    float s = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) s += (acc3[dt][tb][0] + acc3[dt][tb][1]) + (acc3[dt][tb][2] + acc3[dt][tb][3]);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float dd = acc3[dt][tb][j] - mu; q += dd * dd; }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float inv = rsqrtf(q * (1.0f / D) + 1e-5f);
+    const long tok = tw + tb * 16 + fr;
+    if (tok >= T) continue;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int col = dt * 16 + fg * 4;
+      const float4 gp = *reinterpret_cast<const float4*>(g_post + col);
+      const float4 bp = *reinterpret_cast<const float4*>(b_post + col);
+      float v0 = (acc3[dt][tb][0] - mu) * inv * gp.x + bp.x;
+      float v1 = (acc3[dt][tb][1] - mu) * inv * gp.y + bp.y;
+      float v2 = (acc3[dt][tb][2] - mu) * inv * gp.z + bp.z;
+      float v3 = (acc3[dt][tb][3] - mu) * inv * gp.w + bp.w;
+      if (res) {
+        const uint2 r2 = *reinterpret_cast<const uint2*>(res + tok * D + col);
+        v0 += __uint_as_float(r2.x << 16);
+        v1 += __uint_as_float(r2.x & 0xffff0000u);
+        v2 += __uint_as_float(r2.y << 16);
+        v3 += __uint_as_float(r2.y & 0xffff0000u);
+      }
+      *reinterpret_cast<uint2*>(out + tok * D + col) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
     }
   }
 }
 
-template <int D, int HD, int NW>
+template <int D, int HD, int TB, int MINB>
 int launch(const hv_mhc_fused_args* a, hipStream_t s) {
-  using C = Cfg<D, HD, NW>;
-  auto k = mhc_fused_kernel<D, HD, NW>;
+  using C = Cfg<D, HD, TB>;
+  auto k = mhc_fused_kernel<D, HD, TB, MINB>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -321,24 +320,36 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
 }
 
 int g_fused_wide = 0;
+int g_variant = 0;
 
 }  // namespace
 
 extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype) {
   if (dtype != HV_BF16) return 0;
-  // (256, 512) is instantiated but not dispatched by default: at D = 256 the per-tile weight
-  // re-stream (1.9 MB per 64 tokens) makes it slower than the unfused GEMM chain.
   return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
          (D == 256 && Hd == 512 && g_fused_wide);
 }
 extern "C" void hv_mhc_fused_enable_wide(int on) { g_fused_wide = on; }
+// tuning knob (tools/mhc_variants.py): 0 = default tokens-per-wave for D, 1 = half of it
+extern "C" void hv_mhc_fused_set_variant(int v) { g_variant = v; }
 
 extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   if (!a || a->T <= 0) return HV_EINVAL;
   if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype)) return HV_EUNSUPPORTED;
+  const uintptr_t al = (uintptr_t)a->x | (uintptr_t)a->a1t | (uintptr_t)a->w2 | (uintptr_t)a->wct |
+                       (uintptr_t)a->out | (uintptr_t)a->c1 | (uintptr_t)a->b2 | (uintptr_t)a->g_post |
+                       (uintptr_t)a->b_post | (uintptr_t)a->residual;
+  if (al & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  if (a->D == 32) return launch<32, 128, 4>(a, s);
-  if (a->D == 64) return launch<64, 256, 8>(a, s);
-  if (a->D == 128) return launch<128, 512, 8>(a, s);
-  return launch<256, 512, 8>(a, s);
+  // measured (tools/mhc_variants.py): more tokens per wave wins while acc2 fits in registers
+  if (a->D == 32) {
+    if (g_variant == 1) return launch<32, 128, 2, 1>(a, s);
+    return launch<32, 128, 4, 1>(a, s);
+  }
+  if (a->D == 64) {
+    if (g_variant == 1) return launch<64, 256, 1, 1>(a, s);
+    return launch<64, 256, 2, 1>(a, s);
+  }
+  if (a->D == 128) return launch<128, 512, 1, 1>(a, s);
+  return launch<256, 512, 1, 1>(a, s);
 }
