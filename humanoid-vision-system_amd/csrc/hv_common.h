@@ -67,6 +67,33 @@ __device__ __forceinline__ float hv_act(float v, int act) {
   }
 }
 
+// Derivative of hv_act at the pre-activation z (training backward).
+__device__ __forceinline__ float hv_act_grad(float z, int act) {
+  switch (act) {
+    case HV_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case HV_ACT_SILU: { const float s = hv_sigmoid(z); return s * (1.f + z * (1.f - s)); }
+    case HV_ACT_GELU:
+      return 0.5f * (1.0f + erff(z * 0.70710678118654752f)) + z * 0.3989422804014327f * __expf(-0.5f * z * z);
+    case HV_ACT_LEAKY: return z > 0.f ? 1.f : 0.1f;
+    case HV_ACT_SIGMOID: { const float s = hv_sigmoid(z); return s * (1.f - s); }
+    default: return 1.f;
+  }
+}
+
+// Dropout keep mask shared by every training kernel: element idx of a tensor dropped with
+// probability p under `seed` (counter-based, so the backward regenerates it instead of storing).
+__device__ __forceinline__ uint32_t hv_hash32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float hv_drop_scale(uint32_t seed, unsigned long long idx, float p) {
+  if (p <= 0.f) return 1.f;
+  uint32_t h = hv_hash32((uint32_t)idx * 0x9E3779B1u + seed);
+  h = hv_hash32(h ^ ((uint32_t)(idx >> 32) * 0x85EBCA77u) ^ (seed * 0x27d4eb2fu));
+  const float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.0f / (1.0f - p) : 0.f;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

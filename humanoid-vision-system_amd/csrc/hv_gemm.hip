@@ -27,7 +27,7 @@ template <typename T> struct Tr;
 template <> struct Tr<float> { static constexpr int EPC = 4; };           // elems per 16 B chunk
 template <> struct Tr<unsigned short> { static constexpr int EPC = 8; };
 
-enum { AM_DENSE = 0, AM_LN = 1, AM_CONV = 2, AM_CONV_SCALAR = 3 };
+enum { AM_DENSE = 0, AM_LN = 1, AM_CONV = 2, AM_CONV_SCALAR = 3, AM_CONVT = 4 };
 
 __device__ __forceinline__ float ldT(const float* p, long i) { return p[i]; }
 __device__ __forceinline__ float ldT(const unsigned short* p, long i) { return bf2f(p[i]); }
@@ -84,7 +84,7 @@ struct RowCtx {        // per-thread context of one A row it stages
   float mean, rstd;    // LN prologue
 };
 
-template <typename T, int BM, int BN, int AMODE>
+template <typename T, int BM, int BN, int AMODE, bool TRAIN>
 __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
   constexpr int EPC = Tr<T>::EPC;
   constexpr int KSTEP = 4 * EPC;          // elements per 64-byte k-step
@@ -121,12 +121,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
     rc[i].valid = row < d.M;
     rc[i].mean = 0.f; rc[i].rstd = 1.f;
     const int rr = rc[i].valid ? row : 0;
-    if constexpr (AMODE == AM_CONV || AMODE == AM_CONV_SCALAR) {
+    if constexpr (AMODE == AM_CONV || AMODE == AM_CONV_SCALAR || AMODE == AM_CONVT) {
       const int hw = d.conv_oh * d.conv_ow;
       const int b = rr / hw, p = rr % hw;
       const int oh = p / d.conv_ow, ow = p % d.conv_ow;
-      rc[i].ih0 = oh * d.conv_stride - d.conv_pad;
-      rc[i].iw0 = ow * d.conv_stride - d.conv_pad;
+      if constexpr (AMODE == AM_CONVT) {         // row = forward input pixel (ih, iw)
+        rc[i].ih0 = oh + d.conv_pad;
+        rc[i].iw0 = ow + d.conv_pad;
+      } else {
+        rc[i].ih0 = oh * d.conv_stride - d.conv_pad;
+        rc[i].iw0 = ow * d.conv_stride - d.conv_pad;
+      }
       rc[i].base = (const T*)d.A + (long)b * d.conv_h * d.conv_w * d.conv_c;
     } else {
       rc[i].ih0 = rc[i].iw0 = 0;
@@ -176,6 +181,16 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
         return make_uint4(0, 0, 0, 0);
       return *reinterpret_cast<const uint4*>((const T*)r.base +
                                             ((long)ih * d.conv_w + iw) * d.conv_c + ci);
+    } else if constexpr (AMODE == AM_CONVT) {
+      // transposed conv (dgrad): tap (kh, kw) of input pixel reads output pixel (th/s, tw/s)
+      if (k >= d.K) return make_uint4(0, 0, 0, 0);
+      const int tap = k / d.conv_c, ci = k - tap * d.conv_c;
+      const int kh = tap / d.conv_k, kw = tap - kh * d.conv_k;
+      const int th = r.ih0 - kh, tw = r.iw0 - kw;
+      if (th < 0 || tw < 0 || th % d.conv_stride || tw % d.conv_stride) return make_uint4(0, 0, 0, 0);
+      const int oh = th / d.conv_stride, ow = tw / d.conv_stride;
+      if (oh >= d.conv_h || ow >= d.conv_w) return make_uint4(0, 0, 0, 0);
+      return *reinterpret_cast<const uint4*>((const T*)r.base + ((long)oh * d.conv_w + ow) * d.conv_c + ci);
     } else {
       float f[EPC];
 #pragma unroll
@@ -271,25 +286,38 @@ __global__ void __launch_bounds__(256) gemm_kernel(const hv_gemm_desc d) {
   }
 
   // ---- epilogue (hv_gemm_epi.h: sub-tiles accumulated transposed; LN prologue already applied)
-  gemm_epilogue<BM, BN, false>(d, acc, m0, n0);
+  gemm_epilogue<BM, BN, false, TRAIN>(d, acc, m0, n0);
+}
+
+template <typename T, int BM, int BN, bool TRAIN>
+int launch_mode_t(const hv_gemm_desc& d, hipStream_t s) {
+  const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
+  constexpr int EPC = Tr<T>::EPC;
+  if (d.conv_k > 0 && d.conv_transposed) {
+    gemm_kernel<T, BM, BN, AM_CONVT, TRAIN><<<grid, 256, 0, s>>>(d);
+  } else if (d.conv_k > 0) {
+    if (d.conv_c % EPC == 0)
+      gemm_kernel<T, BM, BN, AM_CONV, TRAIN><<<grid, 256, 0, s>>>(d);
+    else
+      gemm_kernel<T, BM, BN, AM_CONV_SCALAR, TRAIN><<<grid, 256, 0, s>>>(d);
+  } else if (d.a_mean) {
+    gemm_kernel<T, BM, BN, AM_LN, TRAIN><<<grid, 256, 0, s>>>(d);
+  } else {
+    gemm_kernel<T, BM, BN, AM_DENSE, TRAIN><<<grid, 256, 0, s>>>(d);
+  }
+  HV_CHECK_LAUNCH();
+  return HV_OK;
 }
 
 template <typename T, int BM, int BN>
 int launch_mode(const hv_gemm_desc& d, hipStream_t s) {
-  const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
-  constexpr int EPC = Tr<T>::EPC;
-  if (d.conv_k > 0) {
-    if (d.conv_c % EPC == 0)
-      gemm_kernel<T, BM, BN, AM_CONV><<<grid, 256, 0, s>>>(d);
-    else
-      gemm_kernel<T, BM, BN, AM_CONV_SCALAR><<<grid, 256, 0, s>>>(d);
-  } else if (d.a_mean) {
-    gemm_kernel<T, BM, BN, AM_LN><<<grid, 256, 0, s>>>(d);
+  // training epilogues are separate instantiations: the inference kernels keep their registers
+  if constexpr (BM * BN > 128 * 64) {
+    if (d.epi_mode) return HV_EUNSUPPORTED;     // never selected (launch_typed picks 64x128)
+    return launch_mode_t<T, BM, BN, false>(d, s);
   } else {
-    gemm_kernel<T, BM, BN, AM_DENSE><<<grid, 256, 0, s>>>(d);
+    return d.epi_mode ? launch_mode_t<T, BM, BN, true>(d, s) : launch_mode_t<T, BM, BN, false>(d, s);
   }
-  HV_CHECK_LAUNCH();
-  return HV_OK;
 }
 
 template <typename T>
@@ -298,7 +326,7 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
   const long tiles128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   if (d.N <= 64) return launch_mode<T, 128, 64>(d, s);
   if (tiles128 < 512 && d.M > 64) return launch_mode<T, 64, 128>(d, s);
-  if (d.M <= 64) return launch_mode<T, 64, 128>(d, s);
+  if (d.M <= 64 || d.epi_mode) return launch_mode<T, 64, 128>(d, s);
   return launch_mode<T, 128, 128>(d, s);
 }
 
@@ -320,6 +348,7 @@ extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
     if (d.K != d.conv_k * d.conv_k * d.conv_c || d.M != d.conv_n * d.conv_oh * d.conv_ow)
       return HV_EINVAL;
     if (d.a_mean || d.A2) return HV_EUNSUPPORTED;
+    if (d.conv_transposed && (d.conv_c % epc || d.conv_stride < 1)) return HV_EUNSUPPORTED;
   } else {
     if (d.lda % epc) return HV_EUNSUPPORTED;
     if (d.A2 && (d.k1 % (4 * epc) || d.lda2 % epc)) return HV_EUNSUPPORTED;

@@ -13,7 +13,33 @@
 #pragma once
 #include "hv_common.h"
 
-template <int BM, int BN, bool LN_EPI>
+// Training epilogue modes (hv_gemm_desc.epi_mode 1/2, see hv_kernels.h).
+__device__ __forceinline__ void epi_train(const hv_gemm_desc& d, const f32x4& acc, float (&v)[4], int row, int col,
+                                       const float (&sc)[4], const float (&bi)[4], const float (&cs)[4],
+                                       float mean, float rstd, bool ln_epi) {
+  const bool aux_bf = d.aux_dtype == HV_BF16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (col + j >= d.N) { v[j] = 0.f; continue; }
+    const unsigned long long idx = (unsigned long long)row * d.N + col + j;
+    const long ai = (long)row * d.ld_aux + col + j;
+    float x = acc[j];
+    if (d.epi_mode == 1) {
+      if (ln_epi) x = rstd * (x - mean * cs[j]);
+      x = x * sc[j] + bi[j];
+      if (aux_bf) ((unsigned short*)d.aux)[ai] = f2bf(x);
+      else ((float*)d.aux)[ai] = x;
+      // the activation sees the value the backward will see (rounded when stored in bf16)
+      const float z = aux_bf ? bf2f(f2bf(x)) : x;
+      v[j] = hv_act(z, d.act) * hv_drop_scale(d.drop_seed, idx, d.drop_p);
+    } else {
+      const float z = aux_bf ? bf2f(((const unsigned short*)d.aux)[ai]) : ((const float*)d.aux)[ai];
+      v[j] = x * d.alpha * hv_drop_scale(d.drop_seed, idx, d.drop_p) * hv_act_grad(z, d.act);
+    }
+  }
+}
+
+template <int BM, int BN, bool LN_EPI, bool TRAIN = false>
 __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4 (&acc)[BM / 32][BN / 32],
                                               int m0, int n0) {
   constexpr int RM = BM / 32, RN = BN / 32;
@@ -52,12 +78,16 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
       const int col = n0 + wc * (BN / 2) + b * 16 + fg * 4;
       if (col >= d.N) continue;
       float v[4];
+      if constexpr (!TRAIN) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float x = acc[a][b][j];
-        if constexpr (LN_EPI) x = rstd * (x - mean * cs[b][j]);
-        x = x * sc[b][j] + bi[b][j];
-        v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+        for (int j = 0; j < 4; ++j) {
+          float x = acc[a][b][j];
+          if constexpr (LN_EPI) x = rstd * (x - mean * cs[b][j]);
+          x = x * sc[b][j] + bi[b][j];
+          v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+        }
+      } else {
+        epi_train(d, acc[a][b], v, row, col, sc[b], bi[b], cs[b], mean, rstd, LN_EPI);
       }
       if (vec && col + 4 <= d.N) {
         if (d.residual) {

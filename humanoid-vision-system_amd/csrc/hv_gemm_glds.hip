@@ -26,7 +26,7 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base)
 #endif
 }
 
-template <int BM, int BN, bool CONV>
+template <int BM, int BN, bool CONV, bool TRAIN>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
   constexpr int AI = BM / 32;               // A wave-instructions (8 rows each) per wave
@@ -152,15 +152,24 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 
   // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
   //      LN_EPI: LayerNorm after the product)
-  if (d.a_mean) gemm_epilogue<BM, BN, true>(d, acc, m0, n0);
-  else gemm_epilogue<BM, BN, false>(d, acc, m0, n0);
+  if (d.a_mean) gemm_epilogue<BM, BN, true, TRAIN>(d, acc, m0, n0);
+  else gemm_epilogue<BM, BN, false, TRAIN>(d, acc, m0, n0);
 }
 
 template <int BM, int BN>
 int launch(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
-  if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true><<<grid, 256, 0, s>>>(d);
-  else gemm_glds_kernel<BM, BN, false><<<grid, 256, 0, s>>>(d);
+  if (d.epi_mode) {
+    if constexpr (BM * BN > 128 * 64) {
+      return HV_EUNSUPPORTED;                   // never selected: the training epilogue uses 64x128
+    } else {
+      if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(d);
+      else gemm_glds_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(d);
+    }
+  } else {
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>(d);
+  }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -169,13 +178,13 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
-  if (d.dtype != HV_BF16 || d.K % 64) return HV_EUNSUPPORTED;
+  if (d.dtype != HV_BF16 || d.K % 64 || d.conv_transposed) return HV_EUNSUPPORTED;
   if (d.a_mean && (!d.b_colsum || d.A2 || d.conv_k > 0)) return HV_EUNSUPPORTED;
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
   if (d.ldb % 8) return HV_EUNSUPPORTED;
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   if (d.N <= 64) return launch<128, 64>(d, s);
-  if (d.M <= 64 || t128 < 256) return launch<64, 128>(d, s);
+  if (d.M <= 64 || t128 < 256 || d.epi_mode) return launch<64, 128>(d, s);   // 128x128 + training epilogue spills
   return launch<128, 128>(d, s);
 }

@@ -213,6 +213,228 @@ extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count
   return HV_OK;
 }
 
+
+// ============================================================================ backward
+// Reverse-mode through every step (autograd of manifold_layers.py:56-73), G = dL/dM kept
+// dense in `draw`.  With M after the column step of iteration t = diag(a_t+1) K diag(b_t+1)
+// and 1/(c_t + eps) = b_t+1 / b_t, 1/(r_t + eps) = a_t+1 / a_t (forward identities):
+//   column step:  s_j = b_t+1,j sum_i G_ij a_t+1,i K_ij ;  G_ij <- (G_ij - s_j) b_t+1,j / b_t,j
+//   row step:     s_i = a_t+1,i sum_j G_ij K_ij b_t,j   ;  G_ij <- (G_ij - s_i) a_t+1,i / a_t,i
+//   softmax:      draw_ij = K_ij (G_ij - sum_j' G_ij' K_ij' / m) / tau
+// One fused row pass per iteration (column-step update, row step, next column partials) +
+// one column reduce, like the forward.
+namespace {
+
+struct BWork {
+  float* K;      // [batch*n, m]
+  float* part;   // [batch, nrb, m]
+  float* s;      // [batch*m]
+};
+__device__ __forceinline__ BWork bcarve(const hv_sinkhorn_bwd_entry& e) {
+  BWork w;
+  const long bn = (long)e.fwd.batch * e.fwd.n, bm = (long)e.fwd.batch * e.fwd.m;
+  const long nrb = (e.fwd.n + RB - 1) / RB;
+  w.K = e.bwork;
+  w.part = w.K + bn * e.fwd.m;
+  w.s = w.part + (long)e.fwd.batch * nrb * e.fwd.m;
+  (void)bm;
+  return w;
+}
+
+template <int FIELD>
+__device__ __forceinline__ int find_bentry(const hv_sinkhorn_bwd_entry* t, int count, int idx) {
+  int lo = 0, hi = count - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    int s = FIELD == 0 ? t[mid].fwd.row_start : (FIELD == 1 ? t[mid].fwd.row_block_start : t[mid].fwd.col_start);
+    if (s <= idx) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// K = softmax(raw/tau)*m into bwork; G = dout into draw.
+__global__ void __launch_bounds__(256) skb_init(const hv_sinkhorn_bwd_entry* __restrict__ tab, int count,
+                                                int total_rows) {
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= total_rows) return;
+  const hv_sinkhorn_bwd_entry e = tab[find_bentry<0>(tab, count, g)];
+  const int row = g - e.fwd.row_start, m = e.fwd.m;
+  const float* src = e.fwd.raw + (long)row * m;
+  const BWork w = bcarve(e);
+  float* K = w.K + (long)row * m;
+  const float inv_tau = 1.0f / e.fwd.tau;
+  float mx = -INFINITY;
+  for (int j = lane; j < m; j += 64) mx = fmaxf(mx, src[j] * inv_tau);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int j = lane; j < m; j += 64) s += __expf(src[j] * inv_tau - mx);
+  s = wave_sum(s);
+  const float k = (float)m / s;
+  for (int j = lane; j < m; j += 64) {
+    K[j] = __expf(src[j] * inv_tau - mx) * k;
+    e.draw[(long)row * m + j] = e.dout[(long)row * m + j];
+  }
+}
+
+// column partials of G (.) a_{t+1} (.) K for the column step of iteration t = iters-1
+__global__ void __launch_bounds__(256) skb_colpart0(const hv_sinkhorn_bwd_entry* __restrict__ tab, int count) {
+  const hv_sinkhorn_bwd_entry e = tab[find_bentry<1>(tab, count, blockIdx.x)];
+  if (e.fwd.iters <= 0) return;
+  const int n = e.fwd.n, m = e.fwd.m, t = e.fwd.iters - 1;
+  const int nrb = (n + RB - 1) / RB;
+  const int lb = blockIdx.x - e.fwd.row_block_start;
+  const int bidx = lb / nrb, rb = lb % nrb;
+  const Work fw = carve(e.fwd);
+  const BWork w = bcarve(e);
+  const float* a1 = fw.a + (long)(t + 1) * e.fwd.batch * n + (long)bidx * n;
+  float* part = w.part + ((long)bidx * nrb + rb) * m;
+  for (int j = threadIdx.x; j < m; j += 256) {
+    float acc = 0.f;
+    for (int r = 0; r < RB; ++r) {
+      const int i = rb * RB + r;
+      if (i >= n) break;
+      const long o = ((long)bidx * n + i) * m + j;
+      acc += e.draw[o] * a1[i] * w.K[o];
+    }
+    part[j] = acc;
+  }
+}
+
+// s_j = b_{t+1,j} * sum over row blocks
+__global__ void __launch_bounds__(256) skb_cols(const hv_sinkhorn_bwd_entry* __restrict__ tab, int count,
+                                                int total_cols, int t) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= total_cols) return;
+  const hv_sinkhorn_bwd_entry e = tab[find_bentry<2>(tab, count, g)];
+  if (t >= e.fwd.iters) return;
+  const Work fw = carve(e.fwd);
+  const BWork w = bcarve(e);
+  const int c = g - e.fwd.col_start;
+  const int bidx = c / e.fwd.m, j = c % e.fwd.m;
+  const int nrb = (e.fwd.n + RB - 1) / RB;
+  const float* part = w.part + (long)bidx * nrb * e.fwd.m + j;
+  float s = 0.f;
+  for (int r = 0; r < nrb; ++r) s += part[(long)r * e.fwd.m];
+  const long bm = (long)e.fwd.batch * e.fwd.m;
+  w.s[c] = fw.b[(long)(t + 1) * bm + c] * s;
+}
+
+// fused: column-step update (iteration t), row step (iteration t), next column partials (t-1)
+__global__ void __launch_bounds__(256) skb_rows(const hv_sinkhorn_bwd_entry* __restrict__ tab, int count, int t) {
+  __shared__ float bt_s[64 * MAXQ];
+  __shared__ float cf_s[64 * MAXQ];
+  __shared__ float sj_s[64 * MAXQ];
+  __shared__ float colpart[4][64 * MAXQ];
+  const hv_sinkhorn_bwd_entry e = tab[find_bentry<1>(tab, count, blockIdx.x)];
+  if (t >= e.fwd.iters) return;
+  const int n = e.fwd.n, m = e.fwd.m;
+  const int nrb = (n + RB - 1) / RB;
+  const int lb = blockIdx.x - e.fwd.row_block_start;
+  const int bidx = lb / nrb, rb = lb % nrb;
+  const Work fw = carve(e.fwd);
+  const BWork w = bcarve(e);
+  const long bn = (long)e.fwd.batch * n, bm = (long)e.fwd.batch * m;
+  const float* bt = fw.b + (long)t * bm + (long)bidx * m;
+  const float* bt1 = fw.b + (long)(t + 1) * bm + (long)bidx * m;
+  const float* at = fw.a + (long)t * bn + (long)bidx * n;
+  const float* at1 = fw.a + (long)(t + 1) * bn + (long)bidx * n;
+  const float* sj = w.s + (long)bidx * m;
+  for (int j = threadIdx.x; j < m; j += 256) {
+    bt_s[j] = bt[j];
+    cf_s[j] = bt1[j] / bt[j];
+    sj_s[j] = sj[j];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nq = (m + 63) >> 6;
+  float acc[MAXQ];
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q) acc[q] = 0.f;
+  for (int rr = 0; rr < RB / 4; ++rr) {
+    const int i = rb * RB + wv * (RB / 4) + rr;
+    if (i >= n) break;
+    const long ro = ((long)bidx * n + i) * m;
+    float gq[MAXQ], kq[MAXQ];
+    float dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int j = lane + 64 * q;
+      gq[q] = 0.f; kq[q] = 0.f;
+      if (q < nq && j < m) {
+        kq[q] = w.K[ro + j];
+        gq[q] = (e.draw[ro + j] - sj_s[j]) * cf_s[j];          // column-step backward
+        dot += gq[q] * kq[q] * bt_s[j];
+      }
+    }
+    dot = wave_sum(dot);
+    const float a1 = at1[i];
+    const float si = a1 * dot;
+    const float rf = a1 / at[i];
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int j = lane + 64 * q;
+      if (q < nq && j < m) {
+        const float gn = (gq[q] - si) * rf;                  // row-step backward
+        e.draw[ro + j] = gn;
+        acc[q] += gn * at[i] * kq[q];                        // partial for column step t-1
+      }
+    }
+  }
+  if (t == 0) return;
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q)
+    if (q < nq) colpart[wv][lane + 64 * q] = acc[q];
+  __syncthreads();
+  float* part = w.part + ((long)bidx * nrb + rb) * m;
+  for (int j = threadIdx.x; j < m; j += 256)
+    part[j] = (colpart[0][j] + colpart[1][j]) + (colpart[2][j] + colpart[3][j]);
+}
+
+// softmax backward: draw = K (G - rowdot(G, K)/m) / tau
+__global__ void __launch_bounds__(256) skb_final(const hv_sinkhorn_bwd_entry* __restrict__ tab, int count,
+                                                 int total_rows) {
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= total_rows) return;
+  const hv_sinkhorn_bwd_entry e = tab[find_bentry<0>(tab, count, g)];
+  const int row = g - e.fwd.row_start, m = e.fwd.m;
+  const BWork w = bcarve(e);
+  const float* K = w.K + (long)row * m;
+  float* G = e.draw + (long)row * m;
+  float d = 0.f;
+  for (int j = lane; j < m; j += 64) d += G[j] * K[j];
+  d = wave_sum(d) / (float)m;
+  const float it = 1.0f / e.fwd.tau;
+  for (int j = lane; j < m; j += 64) G[j] = K[j] * (G[j] - d) * it;
+}
+
+}  // namespace
+
+extern "C" size_t hv_sinkhorn_bwd_work_floats(int batch, int n, int m) {
+  const size_t nrb = (size_t)(n + RB - 1) / RB;
+  return (size_t)batch * n * m + (size_t)batch * nrb * m + (size_t)batch * m;
+}
+
+extern "C" int hv_sinkhorn_group_backward(const hv_sinkhorn_bwd_entry* tab, int count, int total_rows,
+                                          int total_row_blocks, int total_cols, int max_iters, hv_stream_t stream) {
+  if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  skb_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
+  if (max_iters > 0) skb_colpart0<<<total_row_blocks, 256, 0, s>>>(tab, count);
+  HV_CHECK_LAUNCH();
+  // entries with fewer iterations join the reverse sweep when t < their iters; their first
+  // column partials come from skb_colpart0, later ones from the fused row pass
+  for (int t = max_iters - 1; t >= 0; --t) {
+    skb_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, t);
+    skb_rows<<<total_row_blocks, 256, 0, s>>>(tab, count, t);
+  }
+  HV_CHECK_LAUNCH();
+  skb_final<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
 extern "C" int hv_abi_version(void) { return 1; }
 extern "C" void hv_struct_sizes(int* out5) {
   out5[0] = (int)sizeof(hv_sinkhorn_entry);

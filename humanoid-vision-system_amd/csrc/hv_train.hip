@@ -1,0 +1,955 @@
+// Training-step kernels for gfx950: BatchNorm batch statistics and its
+// backward, row-norm (LayerNorm / RMSNorm) training forward + backward with fused dropout,
+// activation backward, column reductions for bias gradients, weight-operand layouts for the
+// dgrad GEMMs, squeeze-excite / pooling / upsample / token-assembly backward, the fused
+// YOLOLoss forward+backward, and grad-norm clipping + AdamW over a parameter table.
+//
+// All reductions are two-pass with a fixed order (bitwise reproducible run to run).
+#include "hv_common.h"
+
+namespace {
+
+template <typename T> __device__ __forceinline__ float ld(const T* p, long i);
+template <> __device__ __forceinline__ float ld<float>(const float* p, long i) { return p[i]; }
+template <> __device__ __forceinline__ float ld<unsigned short>(const unsigned short* p, long i) { return bf2f(p[i]); }
+template <typename T> __device__ __forceinline__ void st(T* p, long i, float v);
+template <> __device__ __forceinline__ void st<float>(float* p, long i, float v) { p[i] = v; }
+template <> __device__ __forceinline__ void st<unsigned short>(unsigned short* p, long i, float v) { p[i] = f2bf(v); }
+
+__device__ __forceinline__ float ld_dt(const void* p, int dt, long i) {
+  return dt == HV_BF16 ? bf2f(((const unsigned short*)p)[i]) : ((const float*)p)[i];
+}
+__device__ __forceinline__ void st_dt(void* p, int dt, long i, float v) {
+  if (dt == HV_BF16) ((unsigned short*)p)[i] = f2bf(v);
+  else ((float*)p)[i] = v;
+}
+
+// ------------------------------------------------------------------ weight layouts
+__global__ void k_dgrad_wprep(const float* __restrict__ w, int cout, int cin, int k, int flip, int dt, void* y) {
+  const long total = (long)cout * cin * k * k;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    // i over y [ci][kh][kw][co]
+    const int co = (int)(i % cout);
+    long r = i / cout;
+    const int kw = (int)(r % k); r /= k;
+    const int kh = (int)(r % k);
+    const int ci = (int)(r / k);
+    const int sh = flip ? k - 1 - kh : kh, sw = flip ? k - 1 - kw : kw;
+    st_dt(y, dt, i, w[(((long)co * cin + ci) * k + sh) * k + sw]);
+  }
+}
+
+__global__ void k_transpose_cast(const float* __restrict__ x, int rows, int cols, int dt, void* y) {
+  __shared__ float tile[32][33];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 8 rows per pass
+  for (int r = ty; r < 32; r += 8) {
+    const int row = by + r, col = bx + tx;
+    tile[r][tx] = (row < rows && col < cols) ? x[(long)row * cols + col] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int orow = bx + r, ocol = by + tx;                 // y[cols][rows]
+    if (orow < cols && ocol < rows) st_dt(y, dt, (long)orow * rows + ocol, tile[tx][r]);
+  }
+}
+
+__global__ void k_conv_grad_reorder(const float* __restrict__ g, int cout, int cin, int k, float* y) {
+  const long total = (long)cout * cin * k * k;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    // i over y [co][ci][kh][kw]
+    const int kw = (int)(i % k);
+    long r = i / k;
+    const int kh = (int)(r % k); r /= k;
+    const int ci = (int)(r % cin);
+    const int co = (int)(r / cin);
+    y[i] = g[(long)co * k * k * cin + (kh * k + kw) * cin + ci];
+  }
+}
+
+// ------------------------------------------------------------------ column reductions
+// chunking of `rows` for two-pass column reductions (shared by colsum / BN / chan_dot)
+__host__ __device__ inline int red_chunks(long rows) {
+  long c = (rows + 63) / 64;
+  return (int)(c > 1024 ? 1024 : (c < 1 ? 1 : c));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_colsum_part(const T* __restrict__ x, long ldx, long rows, int cols,
+                                                     int nchunk, float* part) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int ch = blockIdx.y;
+  if (col >= cols) return;
+  const long per = (rows + nchunk - 1) / nchunk;
+  const long r0 = ch * per, r1 = min(rows, r0 + per);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += ld<T>(x, r * ldx + col);
+  part[(long)ch * cols + col] = s;
+}
+
+__global__ void k_colsum_final(const float* part, int nchunk, int cols, float* out, int accumulate) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += part[(long)c * cols + col];
+  out[col] = accumulate ? out[col] + s : s;
+}
+
+// ------------------------------------------------------------------ BatchNorm (train)
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_part(const T* __restrict__ x, long rows, int c, int nchunk,
+                                                 float* part) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int ch = blockIdx.y;
+  if (col >= c) return;
+  const long per = (rows + nchunk - 1) / nchunk;
+  const long r0 = ch * per, r1 = min(rows, r0 + per);
+  float s = 0.f, ss = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    const float v = ld<T>(x, r * c + col);
+    s += v;
+    ss += v * v;
+  }
+  part[((long)ch * 2) * c + col] = s;
+  part[((long)ch * 2 + 1) * c + col] = ss;
+}
+
+__global__ void k_bn_final(const float* part, int nchunk, int c, long rows, float eps, float momentum,
+                           float* mean, float* rstd, float* rmean, float* rvar) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= c) return;
+  double s = 0.0, ss = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += part[((long)k * 2) * c + col];
+    ss += part[((long)k * 2 + 1) * c + col];
+  }
+  const double m = s / (double)rows;
+  double var = ss / (double)rows - m * m;
+  var = var < 0.0 ? 0.0 : var;
+  mean[col] = (float)m;
+  rstd[col] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) rmean[col] = (1.f - momentum) * rmean[col] + momentum * (float)m;
+  if (rvar) {
+    const double unb = rows > 1 ? var * (double)rows / (double)(rows - 1) : var;
+    rvar[col] = (1.f - momentum) * rvar[col] + momentum * (float)unb;
+  }
+}
+
+template <typename T>
+__global__ void k_bn_apply(const T* __restrict__ x, long total, int c, const float* mean, const float* rstd,
+                           const float* g, const float* b, int act, T* y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    const float z = (ld<T>(x, i) - mean[col]) * rstd[col] * (g ? g[col] : 1.f) + (b ? b[col] : 0.f);
+    st<T>(y, i, hv_act(z, act));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_bwd_part(const T* __restrict__ x, const T* __restrict__ dy, long rows,
+                                                     int c, const float* mean, const float* rstd, const float* g,
+                                                     const float* b, int act, int nchunk, float* part) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int ch = blockIdx.y;
+  if (col >= c) return;
+  const long per = (rows + nchunk - 1) / nchunk;
+  const long r0 = ch * per, r1 = min(rows, r0 + per);
+  const float mu = mean[col], rs = rstd[col], gg = g ? g[col] : 1.f, bb = b ? b[col] : 0.f;
+  float sg = 0.f, sgx = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    const float xh = (ld<T>(x, r * c + col) - mu) * rs;
+    const float gr = ld<T>(dy, r * c + col) * hv_act_grad(xh * gg + bb, act);
+    sg += gr;
+    sgx += gr * xh;
+  }
+  part[((long)ch * 2) * c + col] = sg;
+  part[((long)ch * 2 + 1) * c + col] = sgx;
+}
+
+__global__ void k_bn_bwd_final(const float* part, int nchunk, int c, float* dgamma, float* dbeta, float* sums) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= c) return;
+  float sg = 0.f, sgx = 0.f;
+  for (int k = 0; k < nchunk; ++k) {
+    sg += part[((long)k * 2) * c + col];
+    sgx += part[((long)k * 2 + 1) * c + col];
+  }
+  if (dgamma) dgamma[col] = sgx;
+  if (dbeta) dbeta[col] = sg;
+  sums[col] = sg;
+  sums[c + col] = sgx;
+}
+
+template <typename T>
+__global__ void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy, long rows, int c,
+                               const float* mean, const float* rstd, const float* g, const float* b, int act,
+                               const float* sums, T* dx) {
+  const long total = rows * c;
+  const float inv = 1.0f / (float)rows;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    const float rs = rstd[col], gg = g ? g[col] : 1.f, bb = b ? b[col] : 0.f;
+    const float xh = (ld<T>(x, i) - mean[col]) * rs;
+    const float gr = ld<T>(dy, i) * hv_act_grad(xh * gg + bb, act);
+    st<T>(dx, i, gg * rs * (gr - sums[col] * inv - xh * sums[c + col] * inv));
+  }
+}
+
+// ------------------------------------------------------------------ row norms (train)
+constexpr int RQ = 32;     // up to 2048 columns per row held per lane
+
+// mode 0 LayerNorm, 1 RMSNorm; one wave per row
+template <typename TX, typename TY>
+__global__ void __launch_bounds__(256) k_rownorm_train(int mode, const TX* __restrict__ x, int rows, int cols,
+                                                       float eps, const float* g, const float* b, float p,
+                                                       uint32_t seed, TY* y, const TY* res, float* mean,
+                                                       float* rstd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const TX* xr = x + (long)row * cols;
+  float s = 0.f;
+  if (mode == 0) {
+    for (int j = lane; j < cols; j += 64) s += ld<TX>(xr, j);
+    s = wave_sum(s);
+  }
+  const float mu = mode == 0 ? s / cols : 0.f;
+  float v = 0.f;
+  for (int j = lane; j < cols; j += 64) {
+    const float d = ld<TX>(xr, j) - mu;
+    v += d * d;
+  }
+  v = wave_sum(v);
+  const float rs = 1.0f / sqrtf(v / cols + eps);
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    rstd[row] = rs;
+  }
+  for (int j = lane; j < cols; j += 64) {
+    const long o = (long)row * cols + j;
+    float val = (ld<TX>(xr, j) - mu) * rs * (g ? g[j] : 1.f) + (b ? b[j] : 0.f);
+    val *= hv_drop_scale(seed, (unsigned long long)o, p);
+    if (res) val += ld<TY>(res, o);
+    st<TY>(y, o, val);
+  }
+}
+
+// backward: one wave per row; per-wave column partials of g*xhat and g (for dgamma/dbeta)
+template <typename TX, typename TD, typename TO>
+__global__ void __launch_bounds__(256) k_rownorm_bwd(int mode, const TX* __restrict__ x, const TD* __restrict__ dy,
+                                                     int rows, int cols, int rows_per_wave, const float* mean,
+                                                     const float* rstd, const float* g, float p, uint32_t seed,
+                                                     TO* dx, const TO* dx_add, float* wpart) {
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nq = (cols + 63) >> 6;
+  float agx[RQ], ag[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) { agx[q] = 0.f; ag[q] = 0.f; }
+  const int r0 = wave * rows_per_wave, r1 = min(rows, r0 + rows_per_wave);
+  for (int row = r0; row < r1; ++row) {
+    const long base = (long)row * cols;
+    const float mu = mode == 0 ? mean[row] : 0.f, rs = rstd[row];
+    float xh[RQ], gg[RQ];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int j = lane + 64 * q;
+      xh[q] = 0.f; gg[q] = 0.f;
+      if (q < nq && j < cols) {
+        xh[q] = (ld<TX>(x, base + j) - mu) * rs;
+        const float gr = ld<TD>(dy, base + j) * hv_drop_scale(seed, (unsigned long long)(base + j), p);
+        agx[q] += gr * xh[q];
+        ag[q] += gr;
+        gg[q] = gr * (g ? g[j] : 1.f);
+        s1 += gg[q];
+        s2 += gg[q] * xh[q];
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int j = lane + 64 * q;
+      if (q < nq && j < cols) {
+        float d = mode == 0 ? rs * (gg[q] - s1 - xh[q] * s2) : rs * (gg[q] - xh[q] * s2);
+        if (dx_add) d += ld<TO>(dx_add, base + j);
+        st<TO>(dx, base + j, d);
+      }
+    }
+  }
+  if (wpart) {
+    float* o = wpart + (long)wave * 2 * cols;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int j = lane + 64 * q;
+      if (q < nq && j < cols) { o[j] = agx[q]; o[cols + j] = ag[q]; }
+    }
+  }
+}
+
+__global__ void k_rownorm_param_final(const float* wpart, int nwaves, int cols, float* dgamma, float* dbeta) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  float a = 0.f, b = 0.f;
+  for (int w = 0; w < nwaves; ++w) {
+    a += wpart[(long)w * 2 * cols + col];
+    b += wpart[(long)w * 2 * cols + cols + col];
+  }
+  if (dgamma) dgamma[col] = a;
+  if (dbeta) dbeta[col] = b;
+}
+
+// ------------------------------------------------------------------ elementwise
+template <typename T>
+__global__ void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ pre, long n, int act, float p,
+                          uint32_t seed, T* dpre) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    st<T>(dpre, i, ld<T>(dy, i) * hv_drop_scale(seed, (unsigned long long)i, p) * hv_act_grad(ld<T>(pre, i), act));
+}
+
+template <typename T>
+__global__ void k_dropout(const T* __restrict__ x, long n, float p, uint32_t seed, T* y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    st<T>(y, i, ld<T>(x, i) * hv_drop_scale(seed, (unsigned long long)i, p));
+}
+
+// ------------------------------------------------------------------ SE / pooling / upsample
+template <typename T>
+__global__ void __launch_bounds__(256) k_chan_dot_part(const T* __restrict__ a, const T* __restrict__ b, int hw,
+                                                       int c, int nchunk, float* part) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  const int img = blockIdx.z, ch = blockIdx.y;
+  if (col >= c) return;
+  const long per = (hw + nchunk - 1) / nchunk;
+  const long r0 = ch * per, r1 = min((long)hw, r0 + per);
+  const long base = (long)img * hw * c;
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    const long i = base + r * c + col;
+    s += b ? ld<T>(a, i) * ld<T>(b, i) : ld<T>(a, i);
+  }
+  part[((long)img * nchunk + ch) * c + col] = s;
+}
+
+__global__ void k_chan_dot_final(const float* part, int n, int nchunk, int c, float* out) {
+  const int col = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
+  if (col >= c) return;
+  float s = 0.f;
+  for (int k = 0; k < nchunk; ++k) s += part[((long)img * nchunk + k) * c + col];
+  out[(long)img * c + col] = s;
+}
+
+// per image: recompute the SE MLP and backpropagate dgate -> dpooled; keep ds / act / dh for
+// the parameter reductions.  work per image: [c ds][cr act][cr dh]
+__global__ void __launch_bounds__(256) k_se_bwd_img(const float* pooled, const float* dgate, int c, int cr,
+                                                    const float* w1, const float* b1, const float* w2,
+                                                    const float* b2, float* dpooled, float* work) {
+  extern __shared__ float sm[];
+  float* h = sm;            // [cr]
+  float* ds = sm + cr;      // [c]
+  const int img = blockIdx.x;
+  const float* p = pooled + (long)img * c;
+  float* wk = work + (long)img * (c + 2 * cr);
+  for (int r = threadIdx.x; r < cr; r += blockDim.x) {
+    float s = b1[r];
+    for (int k = 0; k < c; ++k) s += w1[(long)r * c + k] * p[k];
+    h[r] = s;
+    wk[c + r] = hv_silu(s);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < c; j += blockDim.x) {
+    float s = b2[j];
+    for (int r = 0; r < cr; ++r) s += w2[(long)j * cr + r] * hv_silu(h[r]);
+    const float gt = hv_sigmoid(s);
+    const float d = dgate[(long)img * c + j] * gt * (1.f - gt);
+    ds[j] = d;
+    wk[j] = d;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < cr; r += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < c; ++j) s += w2[(long)j * cr + r] * ds[j];
+    const float dh = s * hv_act_grad(h[r], HV_ACT_SILU);
+    wk[c + cr + r] = dh;
+    h[r] = dh;      // reuse: dh
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < c; k += blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < cr; ++r) s += w1[(long)r * c + k] * h[r];
+    dpooled[(long)img * c + k] = s;
+  }
+}
+
+// parameter gradients of the SE MLP, summed over images in order
+__global__ void k_se_bwd_params(const float* pooled, const float* work, int n, int c, int cr, float* dw1,
+                                float* db1, float* dw2, float* db2) {
+  const long total = 2L * c * cr + c + cr;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    if (i < (long)c * cr) {                 // dw2[j][r] = sum ds[j] act[r]
+      const int j = (int)(i / cr), r = (int)(i % cr);
+      for (int b = 0; b < n; ++b) s += work[(long)b * (c + 2 * cr) + j] * work[(long)b * (c + 2 * cr) + c + r];
+      dw2[i] = s;
+    } else if (i < 2L * c * cr) {           // dw1[r][k] = sum dh[r] pooled[k]
+      const long t = i - (long)c * cr;
+      const int r = (int)(t / c), k = (int)(t % c);
+      for (int b = 0; b < n; ++b) s += work[(long)b * (c + 2 * cr) + c + cr + r] * pooled[(long)b * c + k];
+      dw1[t] = s;
+    } else if (i < 2L * c * cr + c) {
+      const int j = (int)(i - 2L * c * cr);
+      for (int b = 0; b < n; ++b) s += work[(long)b * (c + 2 * cr) + j];
+      db2[j] = s;
+    } else {
+      const int r = (int)(i - 2L * c * cr - c);
+      for (int b = 0; b < n; ++b) s += work[(long)b * (c + 2 * cr) + c + cr + r];
+      db1[r] = s;
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_se_bwd_apply(const T* __restrict__ dout, const float* gate, const float* dpooled, int hw, int c,
+                               long total, float inv_hw, T* dy) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    const long img = i / ((long)hw * c);
+    st<T>(dy, i, ld<T>(dout, i) * gate[img * c + col] + dpooled[img * c + col] * inv_hw);
+  }
+}
+
+template <typename T>
+__global__ void k_maxpool_bwd(const T* __restrict__ x, const T* __restrict__ dy, int n, int h, int w, int c, T* dx) {
+  const int oh = h / 2, ow = w / 2;
+  const long total = (long)n * oh * ow * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    long r = i / c;
+    const int ox = (int)(r % ow); r /= ow;
+    const int oy = (int)(r % oh);
+    const int b = (int)(r / oh);
+    long idx[4];
+    int best = 0;
+    float bv = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int yy = 2 * oy + (t >> 1), xx = 2 * ox + (t & 1);
+      idx[t] = (((long)b * h + yy) * w + xx) * c + col;
+      const float v = ld<T>(x, idx[t]);
+      if (t == 0 || v > bv) { bv = v; best = t; }
+    }
+    const float g = ld<T>(dy, i);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) st<T>(dx, idx[t], t == best ? g : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void k_upsample_bwd(const T* __restrict__ dy, int n, int h, int w, int c, int hb, int wb, T* db) {
+  const int fy = h / hb, fx = w / wb;
+  const long total = (long)n * hb * wb * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    long r = i / c;
+    const int bx = (int)(r % wb); r /= wb;
+    const int by = (int)(r % hb);
+    const int b = (int)(r / hb);
+    float s = 0.f;
+    for (int yy = 0; yy < fy; ++yy)
+      for (int xx = 0; xx < fx; ++xx) s += ld<T>(dy, (((long)b * h + by * fy + yy) * w + bx * fx + xx) * c + col);
+    st<T>(db, i, s);
+  }
+}
+
+template <typename T>
+__global__ void k_vit_assemble(const T* x, const float* cls, const float* pos, int n, int t, int d, T* z) {
+  const long total = (long)n * (t + 1) * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % d);
+    const long r = i / d;
+    const int tok = (int)(r % (t + 1));
+    const long b = r / (t + 1);
+    const float v = tok == 0 ? cls[col] : ld<T>(x, (b * t + tok - 1) * d + col);
+    st<T>(z, i, v + pos[(long)tok * d + col]);
+  }
+}
+
+template <typename T>
+__global__ void k_vit_assemble_bwd(const T* dz, int n, int t, int d, T* dx, float* dcls, float* dpos) {
+  const long total = (long)(t + 1) * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % d);
+    const int tok = (int)(i / d);
+    float s = 0.f;
+    for (int b = 0; b < n; ++b) {
+      const float g = ld<T>(dz, ((long)b * (t + 1) + tok) * d + col);
+      s += g;
+      if (tok > 0) st<T>(dx, ((long)b * t + tok - 1) * d + col, g);
+    }
+    dpos[i] = s;
+    if (tok == 0) dcls[col] = s;
+  }
+}
+
+template <typename T>
+__global__ void k_scatter_rows(const T* dy, long stride, int n, int c, T* dx) {
+  const long total = (long)n * stride * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % c);
+    const long r = i / c;
+    const long b = r / stride;
+    st<T>(dx, i, (r % stride) == 0 ? ld<T>(dy, b * c + col) : 0.f);
+  }
+}
+
+// ------------------------------------------------------------------ YOLO loss
+__global__ void __launch_bounds__(1024) k_yolo_count(const float* targets, long cells, int P, float* nobj) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  for (long i = threadIdx.x; i < cells; i += blockDim.x) s += targets[i * P + 4] > 0.5f ? 1.f : 0.f;
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) nobj[0] = s;
+}
+
+__device__ __forceinline__ float bce_logits(float x, float t) {
+  return fmaxf(x, 0.f) - x * t + log1pf(__expf(-fabsf(x)));
+}
+
+// one thread per (image, anchor, y, x) cell; block partials of the 4 raw sums
+template <typename T, typename TD>
+__global__ void __launch_bounds__(256) k_yolo_loss(const T* __restrict__ lg, const float* __restrict__ tg, int n,
+                                                   int h, int w, int A, int P, float lc, float lo, float ln,
+                                                   float lcl, const float* nobj, TD* dlg, float* part) {
+  __shared__ float scratch[16];
+  const long cells = (long)n * A * h * w;
+  const long cell = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const float N = nobj[0];
+  const float inv = N > 0.f ? 1.0f / N : 0.f;
+  float s_coord = 0.f, s_obj = 0.f, s_noobj = 0.f, s_cls = 0.f;
+  if (cell < cells) {
+    long r = cell;
+    const int x = (int)(r % w); r /= w;
+    const int y = (int)(r % h); r /= h;
+    const int a = (int)(r % A);
+    const int b = (int)(r / A);
+    const long lbase = (((long)b * h + y) * w + x) * (long)(A * P) + (long)a * P;   // NHWC logits
+    const float* t = tg + cell * P;                                               // [n, A, h, w, P]
+    const float t4 = t[4];
+    const bool obj = t4 > 0.5f, noobj = t4 < 0.5f;
+    for (int k = 0; k < P; ++k) {
+      const float p = ld<T>(lg, lbase + k);
+      float gr = 0.f;
+      if (k < 4) {
+        if (obj) {
+          const float d = p - t[k];
+          s_coord += d * d;
+          gr = lc * inv * 2.f * d;
+        }
+      } else if (k == 4) {
+        if (obj) { s_obj += bce_logits(p, t4); gr = lo * inv * (hv_sigmoid(p) - t4); }
+        else if (noobj) { s_noobj += bce_logits(p, t4); gr = ln * inv * (hv_sigmoid(p) - t4); }
+      } else if (obj) {
+        s_cls += bce_logits(p, t[k]);
+        gr = lcl * inv * (hv_sigmoid(p) - t[k]);
+      }
+      st<TD>(dlg, lbase + k, N > 0.f ? gr : 0.f);
+    }
+  }
+  s_coord = block_sum(s_coord, scratch);
+  s_obj = block_sum(s_obj, scratch);
+  s_noobj = block_sum(s_noobj, scratch);
+  s_cls = block_sum(s_cls, scratch);
+  if (threadIdx.x == 0) {
+    float* o = part + (long)blockIdx.x * 4;
+    o[0] = s_coord; o[1] = s_obj; o[2] = s_noobj; o[3] = s_cls;
+  }
+}
+
+__global__ void k_yolo_final(const float* part, int nblk, const float* nobj, float lc, float lo, float ln, float lcl,
+                             float* sums) {
+  if (threadIdx.x >= 4) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * 4 + threadIdx.x];
+  const float N = nobj[0];
+  sums[threadIdx.x] = N > 0.f ? s : 0.f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sums[4] = N > 0.f ? (lc * sums[0] + lo * sums[1] + ln * sums[2] + lcl * sums[3]) / N : 0.f;
+    sums[5] = N;
+  }
+}
+
+// ------------------------------------------------------------------ clipping + AdamW
+constexpr int PB_ELEMS = 2048;     // parameter elements per block
+
+__device__ __forceinline__ int find_param(const hv_param_entry* t, int count, int blk) {
+  int lo = 0, hi = count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t[mid].blk <= blk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) k_grad_sq(const hv_param_entry* tab, int count, float* part) {
+  __shared__ float scratch[16];
+  const int ei = find_param(tab, count, blockIdx.x);
+  const hv_param_entry e = tab[ei];
+  const long b0 = (long)(blockIdx.x - e.blk) * PB_ELEMS;
+  float s = 0.f;
+  if (e.grad) {
+    for (long i = b0 + threadIdx.x; i < min(e.n, b0 + PB_ELEMS); i += 256) {
+      const float g = e.grad[i];
+      s += g * g;
+    }
+  }
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) k_grad_norm_final(const hv_param_entry* tab, int count, int nblk,
+                                                         const float* part, int groups, float m0, float m1, float m2,
+                                                         float m3, float* norms, float* coefs) {
+  __shared__ float scratch[16];
+  const float mx[4] = {m0, m1, m2, m3};
+  for (int g = 0; g < groups; ++g) {
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += 256) {
+      const int ei = find_param(tab, count, b);
+      if (tab[ei].group == g) s += part[b];
+    }
+    const float tot = block_sum((float)s, scratch);
+    if (threadIdx.x == 0) {
+      const float nrm = sqrtf(tot);
+      norms[g] = nrm;
+      const float c = mx[g] / (nrm + 1e-6f);
+      coefs[g] = c < 1.f ? c : 1.f;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_adamw(const hv_param_entry* tab, int count, const float* coefs, float lr,
+                                               float b1, float b2, float eps, float wd, float bc1, float bc2s) {
+  const int ei = find_param(tab, count, blockIdx.x);
+  const hv_param_entry e = tab[ei];
+  if (!e.grad) return;
+  const long b0 = (long)(blockIdx.x - e.blk) * PB_ELEMS;
+  const float cf = coefs ? coefs[e.group] : 1.f;
+  const float step = lr / bc1;
+  for (long i = b0 + threadIdx.x; i < min(e.n, b0 + PB_ELEMS); i += 256) {
+    const float g = e.grad[i] * cf;
+    const float m = b1 * e.exp_avg[i] + (1.f - b1) * g;
+    const float v = b2 * e.exp_avg_sq[i] + (1.f - b2) * g * g;
+    e.exp_avg[i] = m;
+    e.exp_avg_sq[i] = v;
+    const float denom = sqrtf(v) / bc2s + eps;
+    float p = e.param[i] * (1.f - lr * wd);
+    e.param[i] = p - step * m / denom;
+  }
+}
+
+inline unsigned grid_for(long n) {
+  long b = (n + 255) / 256;
+  return (unsigned)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" int hv_dgrad_weight_prep(const float* w, int cout, int cin, int k, int flip, int y_dtype, void* y,
+                                    hv_stream_t stream) {
+  if (!w || !y || cout <= 0 || cin <= 0 || k <= 0) return HV_EINVAL;
+  k_dgrad_wprep<<<grid_for((long)cout * cin * k * k), 256, 0, (hipStream_t)stream>>>(w, cout, cin, k, flip, y_dtype, y);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_transpose_cast(const float* x, int rows, int cols, int y_dtype, void* y, hv_stream_t stream) {
+  if (!x || !y || rows <= 0 || cols <= 0) return HV_EINVAL;
+  dim3 grid(hv_cdiv(cols, 32), hv_cdiv(rows, 32));
+  k_transpose_cast<<<grid, 256, 0, (hipStream_t)stream>>>(x, rows, cols, y_dtype, y);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, float* y, hv_stream_t stream) {
+  if (!g || !y) return HV_EINVAL;
+  k_conv_grad_reorder<<<grid_for((long)cout * cin * k * k), 256, 0, (hipStream_t)stream>>>(g, cout, cin, k, y);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_colsum_work_floats(int rows, int cols) { return (size_t)red_chunks(rows) * cols; }
+
+extern "C" int hv_colsum(int dtype, const void* x, long ldx, int rows, int cols, float* out, int accumulate,
+                         float* work, hv_stream_t stream) {
+  if (!x || !out || !work || rows <= 0 || cols <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = red_chunks(rows);
+  dim3 grid(hv_cdiv(cols, 256), nch);
+  HV_DISPATCH(dtype, (k_colsum_part<T><<<grid, 256, 0, s>>>((const T*)x, ldx, rows, cols, nch, work)));
+  k_colsum_final<<<hv_cdiv(cols, 256), 256, 0, s>>>(work, nch, cols, out, accumulate);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_bn_work_floats(int rows, int c) { return (size_t)red_chunks(rows) * 2 * c + 2 * (size_t)c; }
+
+extern "C" int hv_bn_stats(int dtype, const void* x, int rows, int c, float eps, float momentum, float* mean,
+                           float* rstd, float* running_mean, float* running_var, float* work, hv_stream_t stream) {
+  if (!x || !mean || !rstd || !work || rows <= 0 || c <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = red_chunks(rows);
+  dim3 grid(hv_cdiv(c, 256), nch);
+  HV_DISPATCH(dtype, (k_bn_part<T><<<grid, 256, 0, s>>>((const T*)x, rows, c, nch, work)));
+  k_bn_final<<<hv_cdiv(c, 256), 256, 0, s>>>(work, nch, c, rows, eps, momentum, mean, rstd, running_mean, running_var);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_bn_apply(int dtype, const void* x, int rows, int c, const float* mean, const float* rstd,
+                           const float* gamma, const float* beta, int act, void* y, hv_stream_t stream) {
+  if (!x || !y || !mean || !rstd) return HV_EINVAL;
+  const long total = (long)rows * c;
+  HV_DISPATCH(dtype, (k_bn_apply<T><<<grid_for(total), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)x, total, c, mean, rstd, gamma, beta, act, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_bn_backward(int dtype, const void* x, const void* dy, int rows, int c, const float* mean,
+                              const float* rstd, const float* gamma, const float* beta, int act, void* dx,
+                              float* dgamma, float* dbeta, float* work, hv_stream_t stream) {
+  if (!x || !dy || !dx || !work || rows <= 0 || c <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = red_chunks(rows);
+  float* sums = work + (size_t)nch * 2 * c;
+  dim3 grid(hv_cdiv(c, 256), nch);
+  HV_DISPATCH(dtype, (k_bn_bwd_part<T><<<grid, 256, 0, s>>>((const T*)x, (const T*)dy, rows, c, mean, rstd, gamma,
+                                                            beta, act, nch, work)));
+  k_bn_bwd_final<<<hv_cdiv(c, 256), 256, 0, s>>>(work, nch, c, dgamma, dbeta, sums);
+  const long total = (long)rows * c;
+  HV_DISPATCH(dtype, (k_bn_bwd_apply<T><<<grid_for(total), 256, 0, s>>>((const T*)x, (const T*)dy, rows, c, mean,
+                                                                        rstd, gamma, beta, act, sums, (T*)dx)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, int cols, float eps,
+                                const float* gamma, const float* beta, float drop_p, unsigned int seed, int y_dtype,
+                                void* y, const void* residual, float* mean, float* rstd, hv_stream_t stream) {
+  if (!x || !y || !rstd || rows <= 0 || cols <= 0 || cols > 64 * RQ || (mode == 0 && !mean)) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = hv_cdiv(rows, 4);
+#define RN_LAUNCH(TX, TY) k_rownorm_train<TX, TY><<<grid, 256, 0, s>>>(mode, (const TX*)x, rows, cols, eps, gamma, \
+      beta, drop_p, seed, (TY*)y, (const TY*)residual, mean, rstd)
+  if (x_dtype == HV_F32 && y_dtype == HV_F32) RN_LAUNCH(float, float);
+  else if (x_dtype == HV_F32 && y_dtype == HV_BF16) RN_LAUNCH(float, unsigned short);
+  else if (x_dtype == HV_BF16 && y_dtype == HV_BF16) RN_LAUNCH(unsigned short, unsigned short);
+  else if (x_dtype == HV_BF16 && y_dtype == HV_F32) RN_LAUNCH(unsigned short, float);
+  else return HV_EINVAL;
+#undef RN_LAUNCH
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+static void rownorm_split(int rows, int* rows_per_wave, int* nwaves) {
+  int rpw = (rows + 4095) / 4096;           // <= 4096 waves
+  if (rpw < 1) rpw = 1;
+  *rows_per_wave = rpw;
+  *nwaves = (rows + rpw - 1) / rpw;
+}
+
+extern "C" size_t hv_rownorm_work_floats(int rows, int cols) {
+  int rpw, nw;
+  rownorm_split(rows, &rpw, &nw);
+  return (size_t)((nw + 3) / 4 * 4) * 2 * cols;
+}
+
+extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, const void* dy, int rows,
+                                   int cols, const float* mean, const float* rstd, const float* gamma, float drop_p,
+                                   unsigned int seed, int dx_dtype, void* dx, const void* dx_add, float* dgamma,
+                                   float* dbeta, float* work, hv_stream_t stream) {
+  if (!x || !dy || !dx || !rstd || rows <= 0 || cols <= 0 || cols > 64 * RQ || (mode == 0 && !mean))
+    return HV_EINVAL;
+  const bool params = dgamma || dbeta;
+  if (params && !work) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int rpw, nw;
+  rownorm_split(rows, &rpw, &nw);
+  const unsigned grid = hv_cdiv(nw, 4);
+  float* wp = params ? work : nullptr;
+  // (x, dy, dx) dtype combinations used by the mHC / transformer paths
+#define RB_LAUNCH(TX, TD, TO) k_rownorm_bwd<TX, TD, TO><<<grid, 256, 0, s>>>(mode, (const TX*)x, (const TD*)dy, rows, \
+      cols, rpw, mean, rstd, gamma, drop_p, seed, (TO*)dx, (const TO*)dx_add, wp)
+  const int key = x_dtype * 4 + dy_dtype * 2 + dx_dtype;
+  switch (key) {
+    case 0: RB_LAUNCH(float, float, float); break;
+    case 1: RB_LAUNCH(float, float, unsigned short); break;
+    case 2: RB_LAUNCH(float, unsigned short, float); break;
+    case 3: RB_LAUNCH(float, unsigned short, unsigned short); break;
+    case 4: RB_LAUNCH(unsigned short, float, float); break;
+    case 5: RB_LAUNCH(unsigned short, float, unsigned short); break;
+    case 6: RB_LAUNCH(unsigned short, unsigned short, float); break;
+    case 7: RB_LAUNCH(unsigned short, unsigned short, unsigned short); break;
+    default: return HV_EINVAL;
+  }
+#undef RB_LAUNCH
+  HV_CHECK_LAUNCH();
+  if (params) {
+    // waves of the last block past nw wrote nothing: only the first nw slots are summed
+    k_rownorm_param_final<<<hv_cdiv(cols, 256), 256, 0, s>>>(work, nw, cols, dgamma, dbeta);
+    HV_CHECK_LAUNCH();
+  }
+  return HV_OK;
+}
+
+extern "C" int hv_act_backward(int dtype, const void* dy, const void* pre, long n, int act, float drop_p,
+                               unsigned int seed, void* dpre, hv_stream_t stream) {
+  if (!dy || !pre || !dpre || n <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_act_bwd<T><<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const T*)dy, (const T*)pre, n, act,
+                                                                                 drop_p, seed, (T*)dpre)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed, void* y,
+                          hv_stream_t stream) {
+  if (!x || !y || n <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_dropout<T><<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const T*)x, n, drop_p, seed, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_chan_dot_work_floats(int n, int hw, int c) { return (size_t)n * red_chunks(hw) * c; }
+
+extern "C" int hv_chan_dot(int dtype, const void* a, const void* b, int n, int hw, int c, float* out, float* work,
+                           hv_stream_t stream) {
+  if (!a || !out || !work || n <= 0 || hw <= 0 || c <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = red_chunks(hw);
+  dim3 grid(hv_cdiv(c, 256), nch, n);
+  HV_DISPATCH(dtype, (k_chan_dot_part<T><<<grid, 256, 0, s>>>((const T*)a, (const T*)b, hw, c, nch, work)));
+  k_chan_dot_final<<<dim3(hv_cdiv(c, 256), n), 256, 0, s>>>(work, n, nch, c, out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_se_mlp_backward(const float* pooled, const float* dgate, int n, int c, int cr, const float* w1,
+                                  const float* b1, const float* w2, const float* b2, float* dpooled, float* dw1,
+                                  float* db1, float* dw2, float* db2, float* work, hv_stream_t stream) {
+  if (!pooled || !dgate || !dpooled || !work || n <= 0 || c <= 0 || cr <= 0) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  k_se_bwd_img<<<n, 256, (size_t)(cr + c) * sizeof(float), s>>>(pooled, dgate, c, cr, w1, b1, w2, b2, dpooled, work);
+  k_se_bwd_params<<<grid_for(2L * c * cr + c + cr), 256, 0, s>>>(pooled, work, n, c, cr, dw1, db1, dw2, db2);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_se_backward_apply(int dtype, const void* dout, const float* gate, const float* dpooled, int n,
+                                    int hw, int c, void* dy, hv_stream_t stream) {
+  if (!dout || !gate || !dpooled || !dy) return HV_EINVAL;
+  const long total = (long)n * hw * c;
+  HV_DISPATCH(dtype, (k_se_bwd_apply<T><<<grid_for(total), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)dout, gate, dpooled, hw, c, total, 1.0f / hw, (T*)dy)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_maxpool2x2_backward(int dtype, const void* x, const void* dy, int n, int h, int w, int c, void* dx,
+                                      hv_stream_t stream) {
+  if (!x || !dy || !dx || (h & 1) || (w & 1)) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_maxpool_bwd<T><<<grid_for((long)n * (h / 2) * (w / 2) * c), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)x, (const T*)dy, n, h, w, c, (T*)dx)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_upsample_backward(int dtype, const void* dy, int n, int h, int w, int c, int hb, int wb, void* db,
+                                    hv_stream_t stream) {
+  if (!dy || !db || hb <= 0 || wb <= 0 || h % hb || w % wb) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_upsample_bwd<T><<<grid_for((long)n * hb * wb * c), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)dy, n, h, w, c, hb, wb, (T*)db)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_vit_assemble(int dtype, const void* x, const float* cls, const float* pos, int n, int tokens, int d,
+                               void* z, hv_stream_t stream) {
+  if (!x || !cls || !pos || !z) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_vit_assemble<T><<<grid_for((long)n * (tokens + 1) * d), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)x, cls, pos, n, tokens, d, (T*)z)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_vit_assemble_backward(int dtype, const void* dz, int n, int tokens, int d, void* dx, float* dcls,
+                                        float* dpos, hv_stream_t stream) {
+  if (!dz || !dx || !dcls || !dpos) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_vit_assemble_bwd<T><<<grid_for((long)(tokens + 1) * d), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)dz, n, tokens, d, (T*)dx, dcls, dpos)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_scatter_rows(int dtype, const void* dy, long stride_rows, int n, int c, void* dx,
+                               hv_stream_t stream) {
+  if (!dy || !dx || stride_rows <= 0) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_scatter_rows<T><<<grid_for((long)n * stride_rows * c), 256, 0, (hipStream_t)stream>>>(
+                         (const T*)dy, stride_rows, n, c, (T*)dx)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_yolo_loss_work_floats(int n, int h, int w, int A) {
+  return 8 + (size_t)hv_cdiv((long)n * A * h * w, 256) * 4;
+}
+
+extern "C" int hv_yolo_loss(int dtype, const void* logits, const float* targets, int n, int h, int w, int A, int P,
+                            float l_coord, float l_obj, float l_noobj, float l_cls, float* sums, int d_dtype,
+                            void* dlogits, float* work, hv_stream_t stream) {
+  if (!logits || !targets || !sums || !dlogits || !work || P < 6) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const long cells = (long)n * A * h * w;
+  float* nobj = work;
+  float* part = work + 8;
+  const unsigned nblk = hv_cdiv(cells, 256);
+  k_yolo_count<<<1, 1024, 0, s>>>(targets, cells, P, nobj);
+#define YL_LAUNCH(T, TD) k_yolo_loss<T, TD><<<nblk, 256, 0, s>>>((const T*)logits, targets, n, h, w, A, P, l_coord, \
+      l_obj, l_noobj, l_cls, nobj, (TD*)dlogits, part)
+  if (dtype == HV_F32 && d_dtype == HV_F32) YL_LAUNCH(float, float);
+  else if (dtype == HV_BF16 && d_dtype == HV_BF16) YL_LAUNCH(unsigned short, unsigned short);
+  else if (dtype == HV_BF16 && d_dtype == HV_F32) YL_LAUNCH(unsigned short, float);
+  else if (dtype == HV_F32 && d_dtype == HV_BF16) YL_LAUNCH(float, unsigned short);
+  else return HV_EINVAL;
+#undef YL_LAUNCH
+  k_yolo_final<<<1, 64, 0, s>>>(part, nblk, nobj, l_coord, l_obj, l_noobj, l_cls, sums);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_param_blocks(long n) { return (int)((n + PB_ELEMS - 1) / PB_ELEMS); }
+
+extern "C" int hv_grad_norms(const hv_param_entry* tab, int count, int total_blocks, int groups,
+                             const float* max_norm, float* norms, float* coefs, float* work, hv_stream_t stream) {
+  if (!tab || count <= 0 || total_blocks <= 0 || groups < 1 || groups > 4 || !max_norm || !norms || !coefs || !work)
+    return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  k_grad_sq<<<total_blocks, 256, 0, s>>>(tab, count, work);
+  float m[4] = {1.f, 1.f, 1.f, 1.f};
+  for (int g = 0; g < groups; ++g) m[g] = max_norm[g];
+  k_grad_norm_final<<<1, 256, 0, s>>>(tab, count, total_blocks, work, groups, m[0], m[1], m[2], m[3], norms, coefs);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_adamw(const hv_param_entry* tab, int count, int total_blocks, const float* coefs, float lr,
+                        float beta1, float beta2, float eps, float weight_decay, int step, hv_stream_t stream) {
+  if (!tab || count <= 0 || total_blocks <= 0 || step < 1) return HV_EINVAL;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, lr, beta1, beta2, eps, weight_decay, bc1,
+                                                         bc2s);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}

@@ -44,7 +44,27 @@ class GemmDesc(C.Structure):
                 ("residual", vp), ("ldr", i64), ("r_dtype", i32), ("r_mod", i32),
                 ("conv_n", i32), ("conv_h", i32), ("conv_w", i32), ("conv_c", i32),
                 ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
-                ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp)]
+                ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp),
+                ("aux", vp), ("ld_aux", i64), ("aux_dtype", i32), ("epi_mode", i32),
+                ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("pad1_", i32)]
+
+
+class WgradDesc(C.Structure):
+    _fields_ = [("dtype", i32), ("P", i32), ("N1", i32), ("N2", i32),
+                ("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("C", vp), ("ldc", i64),
+                ("accumulate", i32), ("pad_", i32), ("work", vp),
+                ("conv_n", i32), ("conv_h", i32), ("conv_w", i32), ("conv_c", i32),
+                ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
+                ("conv_oh", i32), ("conv_ow", i32), ("pad2_", i32)]
+
+
+class SinkhornBwdEntry(C.Structure):
+    _fields_ = [("fwd", SinkhornEntry), ("dout", vp), ("draw", vp), ("bwork", vp)]
+
+
+class ParamEntry(C.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp),
+                ("n", i64), ("group", i32), ("blk", i32)]
 
 
 class MhcFusedArgs(C.Structure):
@@ -105,6 +125,43 @@ _SIGS = {
     "hv_attention_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    # ---- training step
+    "hv_wgrad_work_floats": ([i32, i32, i32, i32], C.c_size_t),
+    "hv_wgrad": ([vp, vp], i32),
+    "hv_dgrad_weight_prep": ([vp, i32, i32, i32, i32, i32, vp, vp], i32),
+    "hv_transpose_cast": ([vp, i32, i32, i32, vp, vp], i32),
+    "hv_conv_grad_reorder": ([vp, i32, i32, i32, vp, vp], i32),
+    "hv_colsum_work_floats": ([i32, i32], C.c_size_t),
+    "hv_colsum": ([i32, vp, i64, i32, i32, vp, i32, vp, vp], i32),
+    "hv_bn_work_floats": ([i32, i32], C.c_size_t),
+    "hv_bn_stats": ([i32, vp, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp], i32),
+    "hv_bn_apply": ([i32, vp, i32, i32, vp, vp, vp, vp, i32, vp, vp], i32),
+    "hv_bn_backward": ([i32, vp, vp, i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp], i32),
+    "hv_rownorm_train": ([i32, i32, vp, i32, i32, f32, vp, vp, f32, C.c_uint, i32, vp, vp, vp, vp, vp], i32),
+    "hv_rownorm_work_floats": ([i32, i32], C.c_size_t),
+    "hv_rownorm_backward": ([i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, f32, C.c_uint, i32, vp, vp, vp, vp,
+                             vp, vp], i32),
+    "hv_act_backward": ([i32, vp, vp, i64, i32, f32, C.c_uint, vp, vp], i32),
+    "hv_dropout": ([i32, vp, i64, f32, C.c_uint, vp, vp], i32),
+    "hv_sinkhorn_bwd_work_floats": ([i32, i32, i32], C.c_size_t),
+    "hv_sinkhorn_group_backward": ([vp, i32, i32, i32, i32, i32, vp], i32),
+    "hv_chan_dot_work_floats": ([i32, i32, i32], C.c_size_t),
+    "hv_chan_dot": ([i32, vp, vp, i32, i32, i32, vp, vp, vp], i32),
+    "hv_se_mlp_backward": ([vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "hv_se_backward_apply": ([i32, vp, vp, vp, i32, i32, i32, vp, vp], i32),
+    "hv_maxpool2x2_backward": ([i32, vp, vp, i32, i32, i32, i32, vp, vp], i32),
+    "hv_upsample_backward": ([i32, vp, i32, i32, i32, i32, i32, i32, vp, vp], i32),
+    "hv_vit_assemble": ([i32, vp, vp, vp, i32, i32, i32, vp, vp], i32),
+    "hv_vit_assemble_backward": ([i32, vp, i32, i32, i32, vp, vp, vp, vp], i32),
+    "hv_scatter_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
+    "hv_attention_train": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp], i32),
+    "hv_attention_backward": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp,
+                               vp, vp], i32),
+    "hv_yolo_loss_work_floats": ([i32, i32, i32, i32], C.c_size_t),
+    "hv_yolo_loss": ([i32, vp, vp, i32, i32, i32, i32, i32, f32, f32, f32, f32, vp, i32, vp, vp, vp], i32),
+    "hv_param_blocks": ([i64], i32),
+    "hv_grad_norms": ([vp, i32, i32, i32, vp, vp, vp, vp, vp], i32),
+    "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp], i32),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -386,7 +386,9 @@ class HybridVisionSystem(nn.Module):
                 compute_loss: bool = False) -> Dict[str, Any]:
         require_cuda(x, "HybridVisionSystem")
         if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("hv_amd: the training step (SURVEY §8a row T) is not on the HIP path yet")
+            # training step: BN batch statistics, dropout, autograd over HIP kernels
+            from .train_model import system_forward
+            return system_forward(self, x, targets, task, compute_loss)
         ctx = self._ctx()
         with torch.no_grad(), use_ctx(ctx):
             xin = to_nhwc(x, ctx.dtype)

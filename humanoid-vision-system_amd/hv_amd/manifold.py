@@ -39,12 +39,17 @@ class SinkhornKnoppProjection(nn.Module):
 
     def forward(self, matrix: torch.Tensor, return_history: bool = False):
         require_cuda(matrix, "SinkhornKnoppProjection")
-        if matrix.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("hv_amd: Sinkhorn backward is not implemented yet (inference path)")
         g = ops.SinkhornGroup([matrix.detach().float().contiguous()], [self.num_iterations],
                               matrix.device, self.epsilon, self.tau)
-        out = g.run()[0]
-        out = out.squeeze(0) if matrix.dim() == 2 else out
+        if matrix.requires_grad and torch.is_grad_enabled():
+            # autograd through every iteration (grouped reverse sweep, hv_sinkhorn_group_backward)
+            from .train_fn import SinkhornGroupFn
+            if matrix.dtype != torch.float32 or not matrix.is_contiguous():
+                raise TypeError("SinkhornKnoppProjection: differentiable input must be contiguous fp32")
+            (out,) = SinkhornGroupFn.apply(g, matrix)
+        else:
+            out = g.run()[0]
+            out = out.squeeze(0) if matrix.dim() == 2 else out
         self.convergence_history.copy_(g.hists[0][: self.num_iterations])
         if not return_history:
             return out
@@ -213,7 +218,9 @@ class ManifoldHyperConnection(nn.Module):
     def forward_tokens(self, x2: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x2: [T, D] token-major in the compute dtype."""
         if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("hv_amd: mHC training backward is not implemented yet")
+            from . import train_fn as TF
+            y = TF.mhc(self, x2, self.sinkhorn(self.H_res_raw))
+            return y if residual is None else TF.AddFn.apply(y, residual, 1.0)
         return mhc_apply(x2, self.plan(), residual)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

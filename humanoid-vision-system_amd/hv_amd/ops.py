@@ -286,6 +286,32 @@ class SinkhornGroup:
         return self.outs
 
 
+    def backward(self, douts):
+        """Grouped reverse sweep (hv_sinkhorn_group_backward): dL/draw for dL/dM = douts
+        (None entries count as zero).  Must follow run() with the same raws."""
+        lib = L.lib()
+        n_e = len(self.entries)
+        bent = (L.SinkhornBwdEntry * n_e)()
+        draws, keep = [], []
+        for i, (e, raw) in enumerate(zip(self.entries, self.raws)):
+            b, n, m = e.batch, e.n, e.m
+            d = douts[i]
+            d = torch.zeros((b, n, m), device=self.device, dtype=torch.float32) if d is None \
+                else d.detach().float().contiguous()
+            dr = torch.empty((b, n, m), device=self.device, dtype=torch.float32)
+            bw = torch.empty(lib.hv_sinkhorn_bwd_work_floats(b, n, m), device=self.device, dtype=torch.float32)
+            be = bent[i]
+            be.fwd = e
+            be.dout, be.draw, be.bwork = d.data_ptr(), dr.data_ptr(), bw.data_ptr()
+            keep += [d, bw]
+            draws.append(dr.view(raw.shape))
+        table = torch.frombuffer(bytearray(bytes(bent)), dtype=torch.uint8).to(self.device)
+        rs, rbs, cs = self.totals
+        check(lib.hv_sinkhorn_group_backward(table.data_ptr(), n_e, rs, rbs, cs, max(self.iters), stream_ptr()),
+              "hv_sinkhorn_group_backward")
+        return draws
+
+
 def sinkhorn(raw: Tensor, iters: int, eps: float = 1e-8, tau: float = 1.0):
     """One Sinkhorn-Knopp projection ([n, m] or [b, n, m]); returns (M, history)."""
     _cuda(raw)

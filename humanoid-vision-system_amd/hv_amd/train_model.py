@@ -1,0 +1,333 @@
+"""HybridVisionSystem forward in training mode, built from the autograd
+Functions of train_fn.py.  It walks the same modules (and parameters) as the inference path,
+in the reference's order (hybrid_vision.py:222-367), with BatchNorm batch statistics,
+dropout and every backward on hand-written HIP kernels.
+
+Layout: NHWC / token-major activations in the compute dtype (bf16 or fp32), fp32 parameters
+and gradients.  All 76 Sinkhorn projections run as ONE grouped autograd node
+(SinkhornGroupFn) whose backward is one grouped reverse sweep.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from . import ops_train as OT
+from . import train_fn as TF
+from .layers import to_nchw_view, to_nhwc
+from .runtime import PRECISIONS
+
+
+def _hres_table(model) -> Dict[int, torch.Tensor]:
+    mods = model._mhc_modules
+    raws = [m.H_res_raw for m in mods]
+    group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
+                              raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
+                              hists=[m.sinkhorn.convergence_history for m in mods])
+    outs = TF.SinkhornGroupFn.apply(group, *raws)
+    return {id(m): h for m, h in zip(mods, outs)}
+
+
+def _tok(m, x: torch.Tensor, H) -> torch.Tensor:
+    n, h, w, c = x.shape
+    return TF.mhc(m, x.reshape(-1, c), H[id(m)]).view(n, h, w, c)
+
+
+def _dropout2d(x: torch.Tensor, p: float) -> torch.Tensor:
+    """nn.Dropout2d on NHWC: one keep/scale per (image, channel)."""
+    if p <= 0:
+        return x
+    n, c = x.shape[0], x.shape[-1]
+    mask = OT.dropout(torch.ones((n, c), device=x.device, dtype=torch.float32), p, TF.next_seed())
+    return _ChannelScaleFn.apply(x, mask)
+
+
+class _ChannelScaleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask):
+        ctx.save_for_backward(mask)
+        return ops.scale_residual(x.contiguous(), mask, None)
+
+    @staticmethod
+    def backward(ctx, g):
+        (mask,) = ctx.saved_tensors
+        return ops.scale_residual(g.contiguous(), mask, None), None
+
+
+# ------------------------------------------------------------------------- backbone
+def conv_mhc_layer(l, x, H, extra_residual=None):
+    """ConvMHCLayer.forward (vision_backbone.py:99-134) in training mode."""
+    y = TF.conv(x, l.conv, l.bn, l.act_name)
+    if l.mhc is not None:
+        y = _tok(l.mhc, y, H)
+        if l.channel_attention is not None:
+            ca = l.channel_attention
+            y = TF.SEGateFn.apply(y, x if l.use_residual else None, ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
+            if extra_residual is not None:
+                y = TF.AddFn.apply(y, extra_residual, 1.0)
+            return y
+    if l.use_residual:
+        y = TF.AddFn.apply(y, x, 1.0)
+    if extra_residual is not None:
+        y = TF.AddFn.apply(y, extra_residual, 1.0)
+    return y
+
+
+def residual_layer(r, x, H):
+    y = x
+    for b in r.blocks:
+        y = conv_mhc_layer(b, y, H)
+    if isinstance(r.projection, nn.Identity):
+        return TF.AddFn.apply(y, x, 1.0)
+    return conv_mhc_layer(r.projection, y, H, extra_residual=x)
+
+
+def backbone(bb, x, H):
+    """HybridVisionBackbone.forward (vision_backbone.py:329-397)."""
+    from .backbone import ConvMHCLayer
+    for lyr in list(bb.stem)[:3]:
+        x = conv_mhc_layer(lyr, x, H)
+    x = TF.MaxPoolFn.apply(x)
+    raw = {"stem": x}
+    for i, st in enumerate(bb.stages):
+        for lyr in st:
+            x = conv_mhc_layer(lyr, x, H) if isinstance(lyr, ConvMHCLayer) else residual_layer(lyr, x, H)
+        raw[f"stage_{i + 1}"] = x
+    p = bb.dropout.p if isinstance(bb.dropout, nn.Dropout2d) else 0.0
+
+    def enh(mod, f):
+        return f if isinstance(mod, nn.Identity) else _tok(mod, f, H)
+
+    return {"scale_small": _dropout2d(enh(bb.enhance_small, raw["stage_2"]), p),
+            "scale_medium": _dropout2d(enh(bb.enhance_medium, raw["stage_3"]), p),
+            "scale_large": _dropout2d(enh(bb.enhance_large, raw["stage_4"]), p),
+            "raw_features": raw}
+
+
+# ------------------------------------------------------------------------- transformer
+def _positions(pe: torch.Tensor, tokens: int) -> torch.Tensor:
+    """[1, L+1, D] table -> [tokens+1, D] (shim S3: linear interpolation of the patch slots)."""
+    t = pe[0]
+    if t.shape[0] == tokens + 1:
+        return t
+    body = F.interpolate(t[1:].t().unsqueeze(0), size=(tokens,), mode="linear").squeeze(0).t()
+    return torch.cat([t[:1], body], dim=0)
+
+
+def attention(a, x, n, H):
+    """MultiHeadManifoldAttention.forward (manifold_layers.py:386-434) on x [n*L, D]."""
+    L = x.shape[0] // n
+    q = TF.mhc(a.q_proj, x, H[id(a.q_proj)]).view(n, L, -1)
+    k = TF.mhc(a.k_proj, x, H[id(a.k_proj)]).view(n, L, -1)
+    v = TF.mhc(a.v_proj, x, H[id(a.v_proj)]).view(n, L, -1)
+    p = a.dropout.p
+    o = TF.AttentionFn.apply(q, k, v, a.num_heads, p, TF.next_seed() if p > 0 else 0)
+    return TF.mhc(a.out_proj, o.reshape(n * L, -1), H[id(a.out_proj)])
+
+
+def encoder_block(blk, x, n, H):
+    """TransformerEncoderBlock.forward (vit_encoder_decoder.py:174-210)."""
+    h = TF.RMSNormFn.apply(x, blk.norm1.scale, blk.norm1.eps)
+    a = attention(blk.attention, h, n, H)
+    a = TF.mhc(blk.residual_mhc1, a, H[id(blk.residual_mhc1)])
+    p = blk.dropout.p
+    x = TF.DropAddFn.apply(x, a, p, TF.next_seed() if p > 0 else 0)
+    h = TF.RMSNormFn.apply(x, blk.norm2.scale, blk.norm2.eps)
+    h = TF.linear(h, blk.mlp[0], act="gelu", p=blk.mlp[2].p)
+    h = TF.linear(h, blk.mlp[3], act="none", p=blk.mlp[4].p)
+    h = TF.mhc(blk.residual_mhc2, h, H[id(blk.residual_mhc2)])
+    return TF.DropAddFn.apply(x, h, p, TF.next_seed() if p > 0 else 0)
+
+
+def vit_encoder(enc, x, H):
+    """VisionTransformerEncoder.forward (vit_encoder_decoder.py:277-315) -> CLS [n, D]."""
+    pe = enc.patch_embed
+    t = TF.conv(x, pe.projection)
+    n, h, w, d = t.shape
+    t = TF.mhc(pe.mhc_enhance, t.reshape(-1, d), H[id(pe.mhc_enhance)]).view(n, h * w, d)
+    pos = _positions(pe.position_embeddings, h * w)
+    z = TF.VitAssembleFn.apply(t, pe.cls_token, pos)
+    L = h * w + 1
+    t = TF.RMSNormFn.apply(z.view(n * L, d), pe.norm.scale, pe.norm.eps)
+    for blk in enc.blocks:
+        t = encoder_block(blk, t, n, H)
+    cls = TF.GatherRowsFn.apply(t, L)
+    cls = TF.RMSNormFn.apply(cls, enc.norm.scale, enc.norm.eps)
+    if isinstance(enc.head, nn.Linear):
+        cls = TF.linear(cls, enc.head)
+    return cls
+
+
+def hybrid_encoder(he, cnn, H):
+    """HybridVisionEncoder.forward (vit_encoder_decoder.py:470-520), shims S2/S3."""
+    n, h, w, c = cnn.shape
+    pe = he.pos_embed[0]
+    pos = pe if pe.shape[0] == h * w else F.interpolate(pe.t().unsqueeze(0), size=(h * w,),
+                                                        mode="linear").squeeze(0).t()
+    v = _LinearPosFn.apply(cnn.reshape(-1, c), he.cnn_to_vit.weight, he.cnn_to_vit.bias, pos, h * w)
+    v = v.view(n, h, w, -1)
+    cls = vit_encoder(he.vit_encoder, v, H)                               # [n, D]
+    e = TF.linear(cls, _Conv1x1AsLinear(he.vit_to_cnn), out_dtype=torch.float32)
+    fused = TF.AddRowvecFn.apply(cnn, e)
+    return _tok(he.fusion_mhc, fused, H)
+
+
+class _Conv1x1AsLinear:
+    """View a 1x1 Conv2d as a Linear (weight [cout, cin, 1, 1] -> [cout, cin]) for TF.linear."""
+
+    def __init__(self, conv):
+        self.weight = conv.weight.view(conv.weight.shape[0], -1)
+        self.bias = conv.bias
+
+
+class _LinearPosFn(torch.autograd.Function):
+    """1x1 conv + bias + learned positional table broadcast over images, as one GEMM epilogue
+    (vit_encoder_decoder.py:485-499): y[n*hw + p] = x W^T + b + pos[p]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, pos, hw: int):
+        dt = x.dtype
+        w = ops.cast(weight.detach().reshape(weight.shape[0], -1).float().contiguous(), dt)
+        y = ops.gemm(x, w, bias=bias.detach().float().contiguous(), residual=pos.detach().float().contiguous(),
+                     residual_mod=hw)
+        ctx.hw = hw
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        g = g.contiguous()
+        dt = x.dtype
+        w2 = weight.detach().reshape(weight.shape[0], -1)
+        dx = ops.gemm(g, OT.transpose_cast(w2, dt))
+        dw = OT.wgrad(g, x).view_as(weight)
+        db = OT.colsum(g)
+        n = g.shape[0] // ctx.hw
+        dpos = OT.colsum(g.view(n, ctx.hw * g.shape[1])).view(ctx.hw, g.shape[1])
+        return dx, dw, db, dpos, None
+
+
+# ------------------------------------------------------------------------- FPN + head
+def fpn(f, feats, H):
+    """FeaturePyramidNetwork.forward (feature_fusion.py:82-153)."""
+    def refine(i, x):
+        r = f.refinement_convs[i]
+        x = TF.conv(x, r[0], r[1], "relu")
+        x = TF.conv(x, r[3], r[4], "relu")
+        return _tok(f.mhc_fusions[i], x, H)
+
+    pl = TF.conv(feats["scale_large"], f.lateral_convs[2])
+    pm = TF.conv(feats["scale_medium"], f.lateral_convs[1])
+    ps = TF.conv(feats["scale_small"], f.lateral_convs[0])
+    rl = refine(2, pl)
+    out = {"fused_large": TF.conv(rl, f.output_convs[2])}
+    rm = refine(1, TF.UpsampleAddFn.apply(pm, rl))
+    out["fused_medium"] = TF.conv(rm, f.output_convs[1])
+    rs = refine(0, TF.UpsampleAddFn.apply(ps, rm))
+    out["fused_small"] = TF.conv(rs, f.output_convs[0])
+    return out
+
+
+def head_logits(ph, x, H):
+    """YOLOPredictionHead.forward up to the 1x1 prediction conv (yolo_head.py:170-195), NHWC."""
+    c = ph.conv_layers
+    x = TF.conv(x, c[0], c[1], "leaky")
+    x = TF.conv(x, c[3], c[4], "leaky")
+    if not isinstance(ph.mhc_enhance, nn.Identity):
+        x = _tok(ph.mhc_enhance, x, H)
+    return TF.conv(x, ph.pred_conv)
+
+
+# ------------------------------------------------------------------------- system
+def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection",
+                   compute_loss: bool = False) -> Dict[str, Any]:
+    """HybridVisionSystem.forward(x, targets, task, compute_loss) with model.training True."""
+    dt = PRECISIONS[model.hv_precision]
+    H = _hres_table(model)
+    xin = to_nhwc(x.detach(), dt)
+    bb = backbone(model.backbone, xin, H)
+    out: Dict[str, Any] = {}
+    if model.use_vit:
+        vit = hybrid_encoder(model.vit_encoder, bb["scale_large"], H)
+        bb["scale_large"] = TF.AddFn.apply(bb["scale_large"], vit, 0.5)
+        out["vit_features"] = to_nchw_view(vit)
+    fused = fpn(model.feature_fusion, bb, H)
+    head = model.detection_head
+    if task == "detection":
+        preds, decoded, logits = {}, {}, {}
+        for s, key in enumerate(("fused_small", "fused_medium", "fused_large")):
+            lg = head_logits(head.pred_heads[s], fused[key], H)
+            logits[s] = lg
+            awh = head.anchor_generator.anchors[s].reshape(head.num_anchors, 4)[:, 2:4].contiguous()
+            with torch.no_grad():
+                dec, pred = ops.yolo_decode(lg.detach(), head.num_anchors, head.num_classes, awh)
+            preds[f"scale_{s}"] = _PredViewFn.apply(lg, head.num_anchors) if lg.requires_grad else pred
+            decoded[f"scale_{s}"] = dec
+        out["predictions"] = preds
+        out["decoded"] = decoded
+        if compute_loss and targets is not None:
+            out["loss"] = yolo_loss(head.loss_fn, logits, targets, head.num_anchors)
+    out["final_features"] = final_features(model, fused, H)
+    bbv = {k: to_nchw_view(v) for k, v in bb.items() if k != "raw_features"}
+    bbv["raw_features"] = {k: to_nchw_view(v) for k, v in bb["raw_features"].items()}
+    out["backbone_features"] = bbv
+    out["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
+    return out
+
+
+class _PredViewFn(torch.autograd.Function):
+    """NHWC logits [n, h, w, A*P] -> reference predictions [n, A, h, w, P] fp32 (differentiable)."""
+
+    @staticmethod
+    def forward(ctx, lg, A: int):
+        n, h, w, ap = lg.shape
+        ctx.meta = (lg.dtype, A)
+        return lg.float().view(n, h, w, A, ap // A).permute(0, 3, 1, 2, 4).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        dt, A = ctx.meta
+        n, A_, h, w, P = g.shape
+        return g.permute(0, 2, 3, 1, 4).reshape(n, h, w, A * P).to(dt).contiguous(), None
+
+
+def yolo_loss(loss_fn, logits: Dict[int, torch.Tensor], targets, A: int) -> Dict[str, Any]:
+    """YOLOLoss.forward (yolo_head.py:374-465) on the NHWC logits of every scale; the raw
+    component sums are device tensors (no host sync), total_loss is differentiable."""
+    lam = (loss_fn.lambda_coord, loss_fn.lambda_obj, loss_fn.lambda_noobj, loss_fn.lambda_cls)
+    total = None
+    comps = torch.zeros(4, device=logits[0].device, dtype=torch.float32)
+    for s in range(loss_fn.num_scales):
+        if s not in logits:
+            continue
+        contrib, sums = TF.YoloLossFn.apply(logits[s], targets[s], A, lam)
+        comps = comps + sums[:4]
+        total = contrib if total is None else total + contrib
+    return {"coord_loss": comps[0], "obj_loss": comps[1], "noobj_loss": comps[2], "cls_loss": comps[3],
+            "total_loss": total}
+
+
+def final_features(model, fused, H):
+    """_extract_final_features (hybrid_vision.py:369-402): GAP x3 -> cat -> mHC -> MLP."""
+    pooled = [ops.channel_mean(fused[k].detach()) for k in ("fused_small", "fused_medium", "fused_large")]
+    # the reference keeps this branch in the graph; its output feeds no loss, so no
+    # gradient reaches it -- computed without autograd history
+    with torch.no_grad():
+        dt = fused["fused_small"].dtype
+        c = torch.cat(pooled, 1).to(dt).contiguous()
+        c = TF.MhcFn.apply(c, H[id(model.final_fusion)].detach(), *[t.detach() for t in (
+            model.final_fusion.H_pre_raw, model.final_fusion.H_post_raw, model.final_fusion.norm_pre.weight,
+            model.final_fusion.norm_pre.bias, model.final_fusion.mlp[0].weight, model.final_fusion.mlp[0].bias,
+            model.final_fusion.mlp[3].weight, model.final_fusion.mlp[3].bias, model.final_fusion.norm_post.weight,
+            model.final_fusion.norm_post.bias)], model.final_fusion,
+            tuple(TF.next_seed() if p > 0 else 0 for p in (model.final_fusion.mlp[2].p, model.final_fusion.mlp[5].p,
+                                                           model.final_fusion.dropout.p)))
+        h = TF.LinearFn.apply(c, model.output_projection[2].weight, model.output_projection[2].bias, "relu", 0.0, 0,
+                              None)
+        return TF.LinearFn.apply(h, model.output_projection[4].weight, model.output_projection[4].bias, "none", 0.0,
+                                 0, torch.float32)

@@ -1,0 +1,223 @@
+"""Training step driver: forward in training mode with YOLOLoss,
+backward, data-parallel gradient all-reduce over RCCL overlapped with the backward, per-group
+gradient clipping and AdamW -- the last two as HIP kernels over a device parameter table.
+
+Reference semantics followed:
+  * loss: YOLOLoss total_loss (yolo_head.py:374-465) from HybridVisionSystem.forward(...,
+    compute_loss=True) (hybrid_vision.py:222-367);
+  * clipping: mhc_trainer.py:342-383 -- torch.nn.utils.clip_grad_norm_ semantics, group
+    'mhc' (name contains 'mhc' or 'H_') at mhc_max_norm=0.5, the rest at max_grad_norm=1.0;
+  * optimizer: optimizer.py:131-191 -- AdamW (decoupled decay before the Adam update),
+    lr 1e-3, weight_decay 1e-4, betas (0.9, 0.999), eps 1e-8 (the 'manifold' branch is empty
+    because _get_param_name returns str(shape));
+  * DDP as intended by scripts/train.py: gradients averaged over ranks, rank-0 buffers (BN
+    running stats, mHC monitors) broadcast before every forward (broadcast_buffers=True),
+    per-replica BN statistics (no SyncBatchNorm).
+
+Gradients live in ONE flat fp32 buffer (each param.grad is a view), bucketed in reverse
+registration order (the order the backward produces them); a bucket's all-reduce is launched
+from the post-accumulate hook of its last parameter, so RCCL traffic over xGMI overlaps the
+rest of the backward.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from ._lib import check, stream_ptr
+
+Tensor = torch.Tensor
+
+
+def mhc_group(name: str) -> int:
+    """Clipping group of a parameter (mhc_trainer.py:356-360): 0 = mHC, 1 = other."""
+    return 0 if ("mhc" in name.lower() or "H_" in name) else 1
+
+
+class GradBuckets:
+    """Flat gradient storage + bucketed, hook-driven all-reduce (average over ranks).
+
+    Works on any device / process-group backend: the CPU `gloo` tests drive it with plain
+    torch modules, the GPU trainer with RCCL ('nccl')."""
+
+    def __init__(self, named_params: Sequence, bucket_bytes: int = 64 << 20, group=None):
+        self.params = [p for _, p in named_params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        dev = self.params[0].device
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.offsets: Dict[int, int] = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = off
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        # buckets over the reverse order (backward produces the last layers first)
+        self.buckets: List[List[Tensor]] = []
+        cur, cur_bytes = [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            cur_bytes += p.numel() * 4
+            if cur_bytes >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self._pending: List = []
+        self._ready = [0] * len(self.buckets)
+        self._hooks = []
+        if self.world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _span(self, i: int):
+        b = self.buckets[i]
+        lo = min(self.offsets[id(p)] for p in b)
+        hi = max(self.offsets[id(p)] + p.numel() for p in b)
+        return lo, hi
+
+    def _on_grad(self, p: Tensor):
+        i = self.bucket_of[id(p)]
+        self._ready[i] += 1
+        if self._ready[i] == len(self.buckets[i]):
+            lo, hi = self._span(i)
+            view = self.flat[lo:hi]
+            view.div_(self.world)
+            self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def zero(self):
+        for p in self.params:          # autograd may have replaced a view (e.g. set_to_none)
+            off = self.offsets[id(p)]
+            if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
+                p.grad = self.flat[off:off + p.numel()].view_as(p)
+        self.flat.zero_()
+        self._ready = [0] * len(self.buckets)
+        self._pending = []
+
+    def finish(self):
+        """Wait for every bucket's all-reduce; buckets whose parameters got no gradient this
+        step (unused branches) are reduced here so every rank stays in lock-step."""
+        if self.world > 1:
+            for i, b in enumerate(self.buckets):
+                if self._ready[i] != len(b):
+                    lo, hi = self._span(i)
+                    view = self.flat[lo:hi]
+                    view.div_(self.world)
+                    self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
+                    self._ready[i] = len(b)
+            for w in self._pending:
+                w.wait()
+        self._pending = []
+
+
+class FusedAdamW:
+    """Per-group grad-norm clipping + AdamW as HIP kernels over a device table (hv_grad_norms,
+    hv_adamw); no host synchronisation."""
+
+    def __init__(self, named_params: Sequence, lr: float = 1e-3, weight_decay: float = 1e-4,
+                 betas=(0.9, 0.999), eps: float = 1e-8, max_norms=(0.5, 1.0)):
+        self.named = [(n, p) for n, p in named_params if p.requires_grad]
+        self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.max_norms = list(max_norms)
+        dev = self.named[0][1].device
+        self.exp_avg = [torch.zeros_like(p) for _, p in self.named]
+        self.exp_avg_sq = [torch.zeros_like(p) for _, p in self.named]
+        self.step_count = 0
+        self.norms = torch.zeros(len(self.max_norms), device=dev, dtype=torch.float32)
+        self.coefs = torch.ones(len(self.max_norms), device=dev, dtype=torch.float32)
+        self._table = None
+        self._key = None
+        self.device = dev
+
+    def _build(self):
+        lib = L.lib()
+        ents = (L.ParamEntry * len(self.named))()
+        blk = 0
+        for i, (name, p) in enumerate(self.named):
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise TypeError(f"{name}: FusedAdamW needs contiguous fp32 parameters")
+            e = ents[i]
+            e.param = p.data_ptr()
+            e.grad = p.grad.data_ptr() if p.grad is not None else None
+            e.exp_avg, e.exp_avg_sq = self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr()
+            e.n = p.numel()
+            e.group = mhc_group(name)
+            e.blk = blk
+            blk += lib.hv_param_blocks(p.numel())
+        self._blocks = blk
+        self._table = torch.frombuffer(bytearray(bytes(ents)), dtype=torch.uint8).to(self.device)
+        self._work = torch.empty(blk, device=self.device, dtype=torch.float32)
+
+    def step(self, clip: bool = True):
+        key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named)
+        if key != self._key:
+            self._build()
+            self._key = key
+        lib = L.lib()
+        self.step_count += 1
+        coefs = None
+        if clip:
+            mx = (C.c_float * len(self.max_norms))(*self.max_norms)
+            check(lib.hv_grad_norms(self._table.data_ptr(), len(self.named), self._blocks, len(self.max_norms), mx,
+                                    self.norms.data_ptr(), self.coefs.data_ptr(), self._work.data_ptr(),
+                                    stream_ptr()), "hv_grad_norms")
+            coefs = self.coefs.data_ptr()
+        b1, b2 = self.betas
+        check(lib.hv_adamw(self._table.data_ptr(), len(self.named), self._blocks, coefs, self.lr, b1, b2, self.eps,
+                           self.wd, self.step_count, stream_ptr()), "hv_adamw")
+
+    def total_norm(self) -> Tensor:
+        """sqrt(sum of squared group norms) (mhc_trainer.py:383), a device scalar."""
+        return self.norms.pow(2).sum().sqrt()
+
+
+class HVTrainer:
+    """One training step = forward (train mode) + YOLOLoss + backward + all-reduce + clip + AdamW."""
+
+    def __init__(self, model, lr: float = 1e-3, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 max_grad_norm: float = 1.0, mhc_max_norm: float = 0.5, bucket_mb: int = 64,
+                 broadcast_buffers: bool = True, group=None):
+        self.model = model
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.grads = GradBuckets(named, bucket_mb << 20, group)
+        self.opt = FusedAdamW(named, lr, weight_decay, betas, eps, (mhc_max_norm, max_grad_norm))
+        self.world = self.grads.world
+        self.group = group
+        self.broadcast_buffers = broadcast_buffers and self.world > 1
+        if self.world > 1:                         # DDP construction: replicas start identical
+            self._broadcast(list(model.parameters()) + list(model.buffers()))
+
+    def _broadcast(self, tensors):
+        float_ts = [t for t in tensors if t.is_floating_point()]
+        if float_ts:
+            flat = torch.cat([t.detach().reshape(-1).float() for t in float_ts])
+            dist.broadcast(flat, 0, group=self.group)
+            off = 0
+            with torch.no_grad():
+                for t in float_ts:
+                    t.copy_(flat[off:off + t.numel()].view_as(t))
+                    off += t.numel()
+        for t in tensors:
+            if not t.is_floating_point():
+                dist.broadcast(t, 0, group=self.group)
+
+    def step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
+        self.model.train()
+        if self.broadcast_buffers:
+            self._broadcast([b for b in self.model.buffers() if b.is_floating_point()])
+        self.grads.zero()
+        out = self.model(images, targets=targets, compute_loss=True)
+        loss = out["loss"]
+        loss["total_loss"].backward()
+        self.grads.finish()
+        self.opt.step(clip=True)
+        return loss

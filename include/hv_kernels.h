@@ -93,6 +93,23 @@ typedef struct hv_gemm_desc {
   /* with a_mean/a_rstd: b_colsum[n] = sum_k B[n,k] lets the LDS-DMA kernel apply the
      LayerNorm after the product, rstd (acc - mean colsum) (exact); NULL: LN on load */
   const float* b_colsum;
+  /* ---- training-step extensions ----
+     epi_mode 0: as above.
+     epi_mode 1 (forward, saves the pre-activation): aux[m, n] = pre-act value (aux_dtype),
+                then v = dropout(act(v)) with drop_p / drop_seed.
+     epi_mode 2 (gradient): v = acc * alpha * keep(m, n) / (1 - drop_p) * act'(aux[m, n])
+                (+ residual) -- the backward of act + dropout fused into the dgrad GEMM.
+     keep(m, n) = hv_drop_keep(drop_seed, m * N + n, drop_p), identical in every kernel. */
+  void* aux; long ld_aux; int aux_dtype;
+  int epi_mode;
+  float drop_p;
+  unsigned int drop_seed;
+  /* dgrad of a convolution: A is the output-gradient image [conv_n, conv_h, conv_w, conv_c]
+     (conv_h/conv_w = forward OUTPUT size, conv_c = forward cout), rows are the pixels of the
+     forward INPUT [conv_n, conv_oh, conv_ow]; B = W^T [cin, kh, kw, cout]; tap (kh, kw) of
+     input pixel (ih, iw) reads output pixel ((ih + pad - kh) / stride, ...) when divisible. */
+  int conv_transposed;
+  int pad1_;
 } hv_gemm_desc;
 
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
@@ -288,6 +305,165 @@ int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, in
                    const float* anchor_wh /* [A, 2] */, float* predictions, float* boxes,
                    float* scores, float* class_scores, int64_t* class_indices,
                    float* objectness, hv_stream_t stream);
+
+
+/* ====================================================================================
+ * Training step: backward kernels, BatchNorm batch statistics,
+ * dropout, YOLOLoss, clipping and AdamW.  Same conventions as above (caller-owned
+ * buffers, asynchronous, graph-capturable); gradients of parameters are fp32.
+ * Dropout masks are never stored: keep(idx) is regenerated from (seed, element index)
+ * by the forward and the backward kernels alike (hv_common.h hv_drop_scale).
+ * ==================================================================================== */
+
+/* Weight-gradient GEMM C[N1, N2] (+)= sum_p A[p, n1] * B[p, n2]  (both token-major).
+   B may be an implicit im2col of an NHWC image (conv_k > 0; columns ordered (kh, kw, ci),
+   rows = output pixels), i.e. dW = dY^T im2col(X) of a convolution, or dW = dY^T X of a
+   Linear / mHC coefficient matrix.  Split-K partials go to `work`
+   (hv_wgrad_work_floats), reduced in a fixed order.  Autograd of the conv/linear/matmul
+   calls listed at hv_gemm. */
+typedef struct hv_wgrad_desc {
+  int dtype;                 /* storage type of A and B */
+  int P, N1, N2;
+  const void* A; long lda;
+  const void* B; long ldb;
+  float* C; long ldc;
+  int accumulate;            /* 1: C += result */
+  int pad_;
+  float* work;
+  int conv_n, conv_h, conv_w, conv_c, conv_k, conv_stride, conv_pad, conv_oh, conv_ow;
+  int pad2_;
+} hv_wgrad_desc;
+size_t hv_wgrad_work_floats(int dtype, int P, int N1, int N2);
+int hv_wgrad(const hv_wgrad_desc* d, hv_stream_t stream);
+
+/* dgrad operand of a conv weight: w [cout, cin, k, k] fp32 -> y [cin, k, k, cout]
+   (flip: taps reversed, for the stride-1 dgrad as a plain convolution) */
+int hv_dgrad_weight_prep(const float* w, int cout, int cin, int k, int flip, int y_dtype, void* y,
+                         hv_stream_t stream);
+/* y[cols, rows] = x[rows, cols]^T  (fp32 -> y_dtype) */
+int hv_transpose_cast(const float* x, int rows, int cols, int y_dtype, void* y, hv_stream_t stream);
+/* conv weight gradient [cout, (kh, kw, cin)] -> parameter layout [cout, cin, kh, kw] (fp32) */
+int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, float* y, hv_stream_t stream);
+/* out[c] (+)= sum_r x[r, c]  (bias gradients); deterministic two-pass */
+size_t hv_colsum_work_floats(int rows, int cols);
+int hv_colsum(int dtype, const void* x, long ldx, int rows, int cols, float* out, int accumulate,
+              float* work, hv_stream_t stream);
+
+/* BatchNorm2d in training mode over NHWC rows (vision_backbone.py:113, feature_fusion.py:44,
+   yolo_head.py:122): batch mean / biased var -> rstd; running stats updated with momentum
+   and the unbiased variance (torch semantics). */
+size_t hv_bn_work_floats(int rows, int c);
+int hv_bn_stats(int dtype, const void* x, int rows, int c, float eps, float momentum,
+                float* mean, float* rstd, float* running_mean, float* running_var, float* work,
+                hv_stream_t stream);
+/* y = act((x - mean) rstd gamma + beta) */
+int hv_bn_apply(int dtype, const void* x, int rows, int c, const float* mean, const float* rstd,
+                const float* gamma, const float* beta, int act, void* y, hv_stream_t stream);
+/* backward of act(BN_train(x)): dx, dgamma, dbeta (work: hv_bn_work_floats) */
+int hv_bn_backward(int dtype, const void* x, const void* dy, int rows, int c, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, int act, void* dx,
+                   float* dgamma, float* dbeta, float* work, hv_stream_t stream);
+
+/* Row-norm training kernels.  mode 0 = LayerNorm (eps), 1 = RMSNorm (x / sqrt(mean x^2 + eps)).
+   forward: y = dropout(norm(x) * gamma + beta) (+ residual); saves mean (LN) and rstd. */
+int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, int cols, float eps,
+                     const float* gamma, const float* beta, float drop_p, unsigned int seed,
+                     int y_dtype, void* y, const void* residual, float* mean, float* rstd,
+                     hv_stream_t stream);
+/* backward: g = dy * keep; dx = norm'(x)^T (g * gamma) (+ dx_add); dgamma/dbeta (may be NULL)
+   = column sums of g * xhat / g.  gamma == NULL: no affine (the folded mHC LN_pre). */
+size_t hv_rownorm_work_floats(int rows, int cols);
+int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, const void* dy, int rows,
+                        int cols, const float* mean, const float* rstd, const float* gamma,
+                        float drop_p, unsigned int seed, int dx_dtype, void* dx, const void* dx_add,
+                        float* dgamma, float* dbeta, float* work, hv_stream_t stream);
+/* dpre[i] = dy[i] * keep(i) * act'(pre[i])  (elementwise; dy/pre/dpre share dtype) */
+int hv_act_backward(int dtype, const void* dy, const void* pre, long n, int act, float drop_p,
+                    unsigned int seed, void* dpre, hv_stream_t stream);
+/* y = dropout(x) (elementwise, idx = element index) */
+int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed, void* y,
+               hv_stream_t stream);
+
+/* Sinkhorn backward through every iteration, grouped (autograd of manifold_layers.py:56-73).
+   Uses the a_t / b_t scaling vectors the forward left in each entry's `work`; recomputes K
+   from raw.  draw = dL/draw for dL/dM = dout.  bwork: hv_sinkhorn_bwd_work_floats. */
+typedef struct hv_sinkhorn_bwd_entry {
+  hv_sinkhorn_entry fwd;
+  const float* dout;   /* [batch, n, m] */
+  float* draw;         /* [batch, n, m] */
+  float* bwork;
+} hv_sinkhorn_bwd_entry;
+size_t hv_sinkhorn_bwd_work_floats(int batch, int n, int m);
+int hv_sinkhorn_group_backward(const hv_sinkhorn_bwd_entry* dev_table, int count, int total_rows,
+                               int total_row_blocks, int total_cols, int max_iters,
+                               hv_stream_t stream);
+
+/* squeeze-excite backward (vision_backbone.py:76-85,126-128):
+   dgate[n, c] = sum_hw dout * y (b == NULL: sum_hw a) -> chan_dot;
+   MLP backward per image -> dpooled, parameter grads; dy = dout * gate + dpooled / hw */
+size_t hv_chan_dot_work_floats(int n, int hw, int c);
+int hv_chan_dot(int dtype, const void* a, const void* b, int n, int hw, int c, float* out, float* work,
+                hv_stream_t stream);
+int hv_se_mlp_backward(const float* pooled, const float* dgate, int n, int c, int cr, const float* w1,
+                       const float* b1, const float* w2, const float* b2, float* dpooled, float* dw1,
+                       float* db1, float* dw2, float* db2, float* work, hv_stream_t stream);
+int hv_se_backward_apply(int dtype, const void* dout, const float* gate, const float* dpooled, int n,
+                         int hw, int c, void* dy, hv_stream_t stream);
+/* MaxPool2d(2,2) backward (first maximum in scan order receives the gradient) */
+int hv_maxpool2x2_backward(int dtype, const void* x, const void* dy, int n, int h, int w, int c,
+                           void* dx, hv_stream_t stream);
+/* nearest-upsample backward: db[n, hb, wb, c] = sum of dy over each (h/hb x w/wb) block */
+int hv_upsample_backward(int dtype, const void* dy, int n, int h, int w, int c, int hb, int wb,
+                         void* db, hv_stream_t stream);
+/* z[b, 0] = cls + pos[0]; z[b, 1+i] = x[b, i] + pos[1+i]  (no norm; training form) */
+int hv_vit_assemble(int dtype, const void* x, const float* cls, const float* pos, int n, int tokens,
+                    int d, void* z, hv_stream_t stream);
+/* its backward: dx = dz[:, 1:], dcls = sum_b dz[b, 0], dpos = sum_b dz[b] (fp32) */
+int hv_vit_assemble_backward(int dtype, const void* dz, int n, int tokens, int d, void* dx, float* dcls,
+                             float* dpos, hv_stream_t stream);
+/* dx[b * stride_rows + r] = (r == 0) ? dy[b] : 0 */
+int hv_scatter_rows(int dtype, const void* dy, long stride_rows, int n, int c, void* dx,
+                    hv_stream_t stream);
+
+/* attention with dropout on the probabilities (manifold_layers.py:404-427, train mode):
+   forward writes o and lse [n, heads, L] (log-sum-exp of the scaled scores);
+   backward recomputes P from lse:  dq, dk, dv. */
+int hv_attention_train(int dtype, const void* q, const void* k, const void* v, void* o, float* lse,
+                       int n, int L, int heads, int hd, float sm_scale, float drop_p, unsigned int seed,
+                       hv_stream_t stream);
+/* work: n * heads * L floats (row dots dout . o) */
+int hv_attention_backward(int dtype, const void* q, const void* k, const void* v, const void* o,
+                          const void* dout, const float* lse, int n, int L, int heads, int hd,
+                          float sm_scale, float drop_p, unsigned int seed, void* dq, void* dk, void* dv,
+                          float* work, hv_stream_t stream);
+
+/* YOLOLoss for one scale (yolo_head.py:374-465): logits NHWC [n, h, w, A*P], targets
+   [n, A, h, w, P] fp32.  Writes sums[0..3] = raw coord / obj / noobj / cls sums, sums[4] =
+   this scale's contribution to total_loss, sums[5] = #objects, and dlogits (NHWC, d_dtype) =
+   d total_loss / d logits (all zero when the scale has no object, like the reference's
+   `continue`).  work: hv_yolo_loss_work_floats. */
+size_t hv_yolo_loss_work_floats(int n, int h, int w, int A);
+int hv_yolo_loss(int dtype, const void* logits, const float* targets, int n, int h, int w, int A, int P,
+                 float l_coord, float l_obj, float l_noobj, float l_cls, float* sums, int d_dtype,
+                 void* dlogits, float* work, hv_stream_t stream);
+
+/* Gradient clipping + AdamW over a device table of parameters (mhc_trainer.py:342-383 and
+   optimizer.py:131-191, i.e. torch.nn.utils.clip_grad_norm_ per group then AdamW). */
+typedef struct hv_param_entry {
+  float* param; float* grad; float* exp_avg; float* exp_avg_sq;
+  long n;
+  int group;          /* clipping group 0..3 */
+  int blk;            /* first block of this entry (prefix over entries) */
+} hv_param_entry;
+int hv_param_blocks(long n);
+/* norms[g] = ||grads of group g||_2 ; coefs[g] = min(1, max_norm[g] / (norms[g] + 1e-6)) */
+int hv_grad_norms(const hv_param_entry* dev_table, int count, int total_blocks, int groups,
+                  const float* max_norm /* host [groups] */, float* norms, float* coefs, float* work,
+                  hv_stream_t stream);
+/* AdamW step with the clip coefficient of each parameter's group (coefs may be NULL) */
+int hv_adamw(const hv_param_entry* dev_table, int count, int total_blocks, const float* coefs,
+             float lr, float beta1, float beta2, float eps, float weight_decay, int step,
+             hv_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -294,9 +294,55 @@ def gen_model(hv, only=None):
         del model, model64
 
 
+# ------------------------------------------------------------------ G5 training step
+def gen_train(hv):
+    """Tiny model, training mode (BN batch statistics), every dropout p=0 so the step is
+    deterministic, YOLOLoss on synthetic targets (hv_amd/targets.py builder), backward in
+    fp32 and fp64.  Records loss components, predictions and per-parameter gradient norms
+    plus full gradients of a few small parameters."""
+    print("G5 train")
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "humanoid-vision-system_amd"))
+    from hv_amd.targets import synthetic_targets
+    B, S = 2, 64
+    _TINY["on"] = True
+    torch.manual_seed(0)
+    model = hv.HybridVisionSystem({"image_size": S})
+    _TINY["on"] = False
+    W.load_formula_weights(model, "wc")
+    for mod in model.modules():
+        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            mod.p = 0.0
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+    tg = synthetic_targets(B, S, seed=3)
+    rec = {"B": B, "S": S}
+    for tag, dt in (("", torch.float32), ("_f64", torch.float64)):
+        m = model.to(dt).train()
+        m.zero_grad()
+        out = m(x.to(dt), targets=[t.to(dt) for t in tg], compute_loss=True)
+        loss = out["loss"]
+        loss["total_loss"].backward()
+        rec["total_loss" + tag] = loss["total_loss"].detach().float()
+        for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
+            rec[k + tag] = torch.tensor(float(loss[k]))
+        for sidx in range(3):
+            rec[f"pred{sidx}" + tag] = out["predictions"][f"scale_{sidx}"].detach().float()
+        names = [n for n, p in m.named_parameters()]
+        rec["grad_norm" + tag] = torch.tensor([p.grad.double().norm().item() if p.grad is not None else -1.0
+                                               for p in m.parameters()])
+        for n, p in m.named_parameters():
+            if p.grad is not None and p.numel() <= 4096 and ("norm_post" in n or "bn." in n or "H_res_raw" in n
+                                                              and p.numel() <= 1024 or "pred_conv.bias" in n):
+                rec["g:" + n + tag] = p.grad.detach().float()
+    import json
+    with open(os.path.join(OUT, "train_tiny_param_names.json"), "w") as f:
+        json.dump(names, f)
+    save("train_tiny_64_b2", **rec)
+    model.float()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout")
+    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train")
     ap.add_argument("--models", default="")
     a = ap.parse_args()
     torch.set_num_threads(8)
@@ -312,6 +358,8 @@ def main():
         gen_model(hv, [m for m in a.models.split(",") if m])
     if "layout" in parts:
         gen_layout(hv)
+    if "train" in parts:
+        gen_train(hv)
 
 
 

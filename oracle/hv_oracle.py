@@ -106,9 +106,54 @@ def rmsnorm(x: Tensor, scale: Tensor, eps: float = 1e-8) -> Tensor:
     return x / rms * scale
 
 
+_BN_TRAIN = {"on": False}
+
+
+class train_mode:
+    """Within this context BatchNorm uses batch statistics (nn.BatchNorm2d in training mode,
+    vision_backbone.py:113 / feature_fusion.py:44 / yolo_head.py:122); dropout stays off, so the
+    training forward is deterministic and comparable (autograd of this restatement is the
+    gradient oracle of the training step)."""
+
+    def __enter__(self):
+        _BN_TRAIN["on"] = True
+
+    def __exit__(self, *exc):
+        _BN_TRAIN["on"] = False
+        return False
+
+
 def batchnorm_eval(x: Tensor, sd, p: str, eps: float = 1e-5) -> Tensor:
+    if _BN_TRAIN["on"]:
+        return F.batch_norm(x, None, None, sd[p + "weight"], sd[p + "bias"], True, 0.0, eps)
     return F.batch_norm(x, sd[p + "running_mean"], sd[p + "running_var"],
                         sd[p + "weight"], sd[p + "bias"], False, 0.0, eps)
+
+
+def yolo_loss(preds: Dict[str, Tensor], targets: List[Tensor], lambdas=(5.0, 1.0, 0.5, 1.0)):
+    """YOLOLoss.forward (yolo_head.py:374-465): per scale, skipped without objects; coordinate
+    MSE, BCE-with-logits obj/noobj/cls, each sum divided by that scale's object count."""
+    lc, lo, ln, lcl = lambdas
+    total = 0.0
+    comps = {"coord_loss": 0.0, "obj_loss": 0.0, "noobj_loss": 0.0, "cls_loss": 0.0}
+    for s in range(len(targets)):
+        pred, tgt = preds[f"scale_{s}"], targets[s]
+        obj = tgt[..., 4] > 0.5
+        noobj = tgt[..., 4] < 0.5
+        n = int(obj.sum())
+        if n == 0:
+            continue
+        coord = F.mse_loss(pred[obj][:, :4], tgt[obj][:, :4], reduction="sum")
+        o = F.binary_cross_entropy_with_logits(pred[obj][:, 4:5], tgt[obj][:, 4:5], reduction="sum")
+        no = F.binary_cross_entropy_with_logits(pred[noobj][:, 4:5], tgt[noobj][:, 4:5], reduction="sum")
+        c = F.binary_cross_entropy_with_logits(pred[obj][:, 5:], tgt[obj][:, 5:], reduction="sum")
+        comps["coord_loss"] += float(coord.detach())
+        comps["obj_loss"] += float(o.detach())
+        comps["noobj_loss"] += float(no.detach())
+        comps["cls_loss"] += float(c.detach())
+        total = total + (lc * coord + lo * o + ln * no + lcl * c) / n
+    comps["total_loss"] = total
+    return comps
 
 
 # ----------------------------------------------------------------------------------------

@@ -1,0 +1,532 @@
+"""GPU parity of the training-step kernels against plain PyTorch fp32
+references of the same ops (torch autograd on the CPU), against the reference's own
+gradient fixtures (tests/golden sk_*/mhc_*: autograd of the imported reference), and the
+full tiny-model training step against autograd of the oracle restatement."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from oracle import cases
+
+pytestmark = pytest.mark.gpu
+
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+def rel(a, b) -> float:
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def OT():
+    from hv_amd import ops_train
+    return ops_train
+
+
+TOL = {"fp32": 1e-5, "bf16": 1.5e-2}
+
+
+# ------------------------------------------------------------------ GEMMs
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("P,N1,N2", [(64, 32, 32), (1000, 64, 136), (4096, 256, 512), (70001, 32, 128),
+                                     (333, 512, 24)])
+def test_wgrad_dense(gpu_device, prec, P, N1, N2):
+    g = torch.Generator().manual_seed(P + N1)
+    a = torch.randn(P, N1, generator=g)
+    b = torch.randn(P, N2, generator=g)
+    dt = DT[prec]
+    ad, bd = a.to(dt), b.to(dt)
+    out = OT().wgrad(ad.to(gpu_device), bd.to(gpu_device))
+    ref = ad.float().t() @ bd.float()
+    assert rel(out, ref) < (1e-5 if prec == "fp32" else 1e-5 * 10)
+
+
+def test_wgrad_accumulate(gpu_device):
+    a = torch.randn(512, 64)
+    b = torch.randn(512, 32)
+    c0 = torch.randn(64, 32)
+    out = c0.clone().to(gpu_device)
+    OT().wgrad(a.to(gpu_device), b.to(gpu_device), out=out, accumulate=True)
+    assert rel(out, c0 + a.t() @ b) < 1e-5
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("cin,cout,k,s,hw", [(32, 64, 3, 1, 16), (64, 128, 3, 2, 16), (64, 32, 1, 1, 12),
+                                             (3, 32, 3, 2, 32), (256, 256, 3, 1, 10), (128, 64, 3, 2, 15)])
+def test_conv_wgrad_dgrad(gpu_device, prec, cin, cout, k, s, hw):
+    from hv_amd import ops
+    T = OT()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = torch.randn(2, cin, hw, hw, generator=g).to(dt).float()
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(dt).float()
+    p = k // 2
+    y = F.conv2d(x, w, None, s, p)
+    dy = torch.randn(y.shape, generator=g).to(dt).float()
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dy, s, p)
+    dw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, s, p)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(dt).to(gpu_device)
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(dt).to(gpu_device)
+    dw = T.conv_grad_reorder(T.conv_wgrad(dyd, xd, k, s, p), cout, cin, k)
+    tol = 1e-5 if prec == "fp32" else 1e-2
+    assert rel(dw, dw_ref) < tol
+    if cin % 8 == 0 or prec == "fp32":
+        wd = w.to(gpu_device)
+        flip = s == 1
+        wt = T.dgrad_weight(wd, dt, flip)
+        dx = T.conv_dgrad(dyd, wt, k, s, p, (hw, hw), flipped=flip)
+        assert rel(dx.float().permute(0, 3, 1, 2), dx_ref) < tol
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("act", ["gelu", "silu", "relu", "leaky"])
+def test_gemm_train_modes(gpu_device, prec, act):
+    """mode 1 stores the pre-activation and applies act + dropout; mode 2 applies the
+    derivative and the SAME mask (regenerated from the seed)."""
+    T = OT()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 300, 128, 96
+    a = torch.randn(M, K, generator=g).to(dt)
+    b = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt)
+    bias = torch.randn(N, generator=g)
+    ad, bd = a.to(gpu_device), b.to(gpu_device)
+    pre = torch.empty(M, N, device=gpu_device, dtype=dt)
+    p = 0.25
+    y = T.gemm_train(ad, bd, mode=1, act=act, aux=pre, bias=bias.to(gpu_device), drop_p=p, seed=1234)
+    pre_ref = a.float() @ b.float().t() + bias
+    assert rel(pre.float(), pre_ref) < TOL[prec]
+    fa = {"gelu": F.gelu, "silu": F.silu, "relu": F.relu, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act]
+    yc = y.float().cpu()
+    act_ref = fa(pre.float().cpu())
+    kept = yc != 0
+    frac = 1 - kept.float().mean().item()
+    assert abs(frac - p) < 0.03 or act == "relu"
+    np.testing.assert_allclose(yc[kept].numpy(), (act_ref / (1 - p))[kept].numpy(), rtol=2e-2, atol=2e-2)
+    # mode 2 with the same seed reproduces the mask: dpre = dh * keep/(1-p) * act'(pre)
+    dh = torch.randn(M, K, generator=g).to(dt)
+    w2 = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt)
+    dpre = T.gemm_train(dh.to(gpu_device), w2.to(gpu_device), mode=2, act=act, aux=pre, drop_p=p, seed=1234)
+    z = pre.float().cpu().requires_grad_(True)
+    (fa(z) * (dh.float() @ w2.float().t())).sum().backward()
+    ref = z.grad * (kept.float() / (1 - p))
+    assert rel(dpre.float(), ref) < (1e-4 if prec == "fp32" else 2e-2)
+    # the elementwise kernel uses the same mask convention
+    dpre2 = T.act_backward((dh.to(gpu_device) @ w2.to(gpu_device).t()).to(dt).contiguous(), pre, act, p, 1234)
+    assert rel(dpre2.float(), ref) < (1e-4 if prec == "fp32" else 2e-2)
+
+
+# ------------------------------------------------------------------ norms
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("act", ["silu", "relu", "leaky"])
+def test_batchnorm_train(gpu_device, prec, act):
+    T = OT()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(5)
+    n, h, w, c = 4, 9, 7, 48
+    x = (torch.randn(n, h, w, c, generator=g) * 2 + 0.5).to(dt)
+    gamma = torch.rand(c, generator=g) + 0.5
+    beta = torch.randn(c, generator=g)
+    rm, rv = torch.zeros(c), torch.ones(c)
+    xd = x.to(gpu_device)
+    rmd, rvd = rm.clone().to(gpu_device), rv.clone().to(gpu_device)
+    mean, rstd = T.bn_stats(xd, 1e-5, 0.1, rmd, rvd)
+    y = T.bn_apply(xd, mean, rstd, gamma.to(gpu_device), beta.to(gpu_device), act)
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    fa = {"silu": F.silu, "relu": F.relu, "leaky": lambda t: F.leaky_relu(t, 0.1)}[act]
+    yr = fa(F.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5))
+    assert rel(y.float().permute(0, 3, 1, 2), yr.detach()) < TOL[prec]
+    assert rel(rmd, rm) < 1e-5 and rel(rvd, rv) < 1e-5
+    dy = torch.randn(n, c, h, w, generator=g).to(dt).float()
+    (yr * dy).sum().backward()
+    dx, dg, db = T.bn_backward(xd, dy.permute(0, 2, 3, 1).contiguous().to(dt).to(gpu_device), mean, rstd,
+                               gamma.to(gpu_device), beta.to(gpu_device), act)
+    assert rel(dx.float().permute(0, 3, 1, 2), xr.grad) < (1e-4 if prec == "fp32" else 3e-2)
+    assert rel(dg, gr.grad) < (1e-4 if prec == "fp32" else 2e-2)
+    assert rel(db, br.grad) < (1e-4 if prec == "fp32" else 2e-2)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("cols", [32, 256, 1792])
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_rownorm_train_backward(gpu_device, mode, cols, prec):
+    T = OT()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(cols + mode)
+    rows = 77
+    x = (torch.randn(rows, cols, generator=g) * 3 + 1).to(dt)
+    gamma = torch.rand(cols, generator=g) + 0.5
+    beta = torch.randn(cols, generator=g)
+    p = 0.2
+    y, mean, rstd = T.rownorm_train(mode, x.to(gpu_device), 1e-5, gamma.to(gpu_device),
+                                    beta.to(gpu_device) if mode == 0 else None, p, 99)
+    xr = x.float().clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    brr = beta.clone().requires_grad_(True)
+    if mode == 0:
+        yr = F.layer_norm(xr, (cols,), gr, brr, 1e-5)
+    else:
+        yr = xr / torch.sqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * gr
+    keep = (y.float().cpu() != 0).float()
+    assert abs(1 - keep.mean().item() - p) < 0.05
+    yr_d = yr * keep / (1 - p)
+    assert rel(y.float(), yr_d.detach()) < TOL[prec]
+    dy = torch.randn(rows, cols, generator=g).to(dt).float()
+    (yr_d * dy).sum().backward()
+    dx, dg, db = T.rownorm_backward(mode, x.to(gpu_device), dy.to(dt).to(gpu_device), mean, rstd,
+                                    gamma.to(gpu_device), p, 99, dx_dtype=torch.float32)
+    assert rel(dx, xr.grad) < (1e-4 if prec == "fp32" else 3e-2)
+    assert rel(dg, gr.grad) < (1e-4 if prec == "fp32" else 3e-2)
+    if mode == 0:
+        assert rel(db, brr.grad) < (1e-4 if prec == "fp32" else 3e-2)
+
+
+# ------------------------------------------------------------------ Sinkhorn backward
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,it", cases.SK_CASES)
+def test_sinkhorn_backward_matches_reference_fixture(gpu_device, fam, D, it):
+    from hv_amd import ops
+    from hv_amd.train_fn import SinkhornGroupFn
+    gld = golden(f"sk_{fam}_D{D}_it{it}")
+    raw = cases.sinkhorn_raw(D, it, fam).to(gpu_device).requires_grad_(True)
+    grp = ops.SinkhornGroup([raw.detach()], [it], gpu_device)
+    (M,) = SinkhornGroupFn.apply(grp, raw)
+    G = torch.randn(D, D, generator=cases.gen_seed(D, it, 3)).to(gpu_device)
+    (M * G).sum().backward()
+    gr = raw.grad.cpu()
+    idx = [0, 1, D // 2, D - 1]
+    ref = torch.from_numpy(gld["grad_rows"])
+    assert rel(gr[idx], ref) < 1e-3, rel(gr[idx], ref)
+    if "grad" in gld.files:
+        assert rel(gr, torch.from_numpy(gld["grad"])) < 1e-3
+
+
+def test_sinkhorn_backward_grouped_equals_single(gpu_device):
+    from hv_amd import ops
+    from hv_amd.train_fn import SinkhornGroupFn
+    Ds, its = (32, 64, 256, 1792), (20, 5, 20, 20)
+    raws = [cases.sinkhorn_raw(D, 20, "wc").to(gpu_device).requires_grad_(True) for D in Ds]
+    Gs = [torch.randn(D, D, device=gpu_device) for D in Ds]
+    grp = ops.SinkhornGroup([r.detach() for r in raws], list(its), gpu_device)
+    outs = SinkhornGroupFn.apply(grp, *raws)
+    sum((o * G).sum() for o, G in zip(outs, Gs)).backward()
+    grouped = [r.grad.clone() for r in raws]
+    for r, it, G, gg in zip(raws, its, Gs, grouped):
+        r2 = r.detach().clone().requires_grad_(True)
+        g1 = ops.SinkhornGroup([r2.detach()], [it], gpu_device)
+        (o,) = SinkhornGroupFn.apply(g1, r2)
+        (o * G).sum().backward()
+        assert torch.equal(r2.grad, gg)
+
+
+# ------------------------------------------------------------------ mHC
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e", cases.MHC_CASES)
+def test_mhc_backward_matches_reference_fixture(gpu_device, fam, D, e):
+    """Gradients of x and H_res_raw (through the Sinkhorn) vs autograd of the reference."""
+    from hv_amd import ManifoldHyperConnection
+    from oracle import weights as W
+    gld = golden(f"mhc_{fam}_D{D}_e{e}")
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=False)
+    W.load_formula_weights(m, fam)
+    m = m.to(gpu_device).train()
+    for d in (m.mlp[2], m.mlp[5], m.dropout):
+        d.p = 0.0
+    x = cases.mhc_input(D, e).to(gpu_device).requires_grad_(True)
+    y = m(x)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), gld["y64"], rtol=0, atol=1e-3)
+    G = torch.randn(64, D, generator=cases.gen_seed(D, e, 12)).to(gpu_device)
+    (y * G).sum().backward()
+    assert rel(x.grad, torch.from_numpy(gld["gx"])) < 2e-3
+    gh = m.H_res_raw.grad.cpu()
+    ref = torch.from_numpy(gld["g_hres"])
+    assert rel(gh[: ref.shape[0]], ref) < 5e-3
+    assert abs(m.H_pre_raw.grad.abs().sum().item() / float(gld["g_hpre_sum"]) - 1) < 5e-3
+    assert abs(m.mlp[0].weight.grad.abs().sum().item() / float(gld["g_w1_sum"]) - 1) < 5e-3
+
+
+@pytest.mark.parametrize("D,e", [(32, 4), (64, 4), (256, 2), (512, 2)])
+def test_mhc_all_param_grads_vs_oracle(gpu_device, D, e):
+    """Every parameter gradient of the training mHC vs torch autograd of the oracle (fp64)."""
+    from hv_amd import ManifoldHyperConnection
+    from oracle import hv_oracle as O
+    from oracle import weights as W
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=False)
+    W.load_formula_weights(m, "wc")
+    sd = {k: v.detach().double().clone().requires_grad_(True) for k, v in m.state_dict().items()
+          if v.is_floating_point()}
+    m = m.to(gpu_device).train()
+    for d in (m.mlp[2], m.mlp[5], m.dropout):
+        d.p = 0.0
+    x = cases.mhc_input(D, e)
+    G = torch.randn(64, D, generator=cases.gen_seed(D, e, 12))
+    y = m(x.to(gpu_device))
+    (y * G.to(gpu_device)).sum().backward()
+    yo = O.mhc(sd, "", x.double(), m.sinkhorn.num_iterations)
+    (yo * G.double()).sum().backward()
+    for name, p in m.named_parameters():
+        ref = sd[name].grad
+        assert ref is not None
+        assert rel(p.grad, ref) < 2e-3, (name, rel(p.grad, ref))
+
+
+@pytest.mark.parametrize("D,e,T", [(64, 4, 2000), (256, 2, 600)])
+def test_mhc_bf16_train_agreement(gpu_device, D, e, T):
+    from hv_amd import ManifoldHyperConnection
+    from oracle import weights as W
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=False)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).train()
+    for d in (m.mlp[2], m.mlp[5], m.dropout):
+        d.p = 0.0
+    x = torch.randn(T, D, device=gpu_device)
+    G = torch.randn(T, D, device=gpu_device)
+    y = m(x.clone().requires_grad_(True))
+    (y * G).sum().backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    m.use_mixed_precision = True
+    m.hv_precision = "bf16"
+    xb = x.to(torch.bfloat16).requires_grad_(True)
+    yb = m(xb)
+    (yb.float() * G).sum().backward()
+    assert rel(yb.float(), y.detach()) < 3e-2
+    for n, p in m.named_parameters():
+        assert rel(p.grad, ref[n]) < 0.1, (n, rel(p.grad, ref[n]))
+
+
+# ------------------------------------------------------------------ attention / SE / misc
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_attention_train_backward(gpu_device, prec):
+    T = OT()
+    dt = DT[prec]
+    n, L, H, hd = 2, 50, 8, 32
+    g = torch.Generator().manual_seed(11)
+    q, k, v, do = (torch.randn(n, L, H * hd, generator=g).to(dt) for _ in range(4))
+    o, lse = T.attention_train(q.to(gpu_device), k.to(gpu_device), v.to(gpu_device), H, 0.0, 0)
+    qr, kr, vr = (t.float().view(n, L, H, hd).transpose(1, 2).clone().requires_grad_(True) for t in (q, k, v))
+    att = torch.softmax(qr @ kr.transpose(-1, -2) * hd ** -0.5, -1)
+    orf = (att @ vr).transpose(1, 2).reshape(n, L, H * hd)
+    assert rel(o.float(), orf.detach()) < TOL[prec]
+    (orf * do.float()).sum().backward()
+    dq, dk, dv = T.attention_backward(q.to(gpu_device), k.to(gpu_device), v.to(gpu_device), o,
+                                      do.to(gpu_device), lse, H, 0.0, 0)
+    for a, r in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
+        assert rel(a.float(), r.transpose(1, 2).reshape(n, L, H * hd)) < (1e-4 if prec == "fp32" else 3e-2)
+
+
+def test_attention_dropout_consistent(gpu_device):
+    """With dropout the backward must see the forward's mask: check dv = (P*mask)^T do."""
+    T = OT()
+    n, L, H, hd = 1, 40, 8, 32
+    q, k, v = (torch.randn(n, L, H * hd, device=gpu_device) for _ in range(3))
+    p = 0.3
+    o, lse = T.attention_train(q, k, v, H, p, 77)
+    do = torch.randn_like(o)
+    dq, dk, dv = T.attention_backward(q, k, v, o, do, lse, H, p, 77)
+    # dv . v == do . o  (both equal sum_ij P_ij m_ij (do_i . v_j))
+    lhs = (dv * v).sum().item()
+    rhs = (do * o).sum().item()
+    assert abs(lhs - rhs) < 1e-3 * max(1.0, abs(rhs))
+
+
+def test_se_gate_backward(gpu_device):
+    from hv_amd.train_fn import SEGateFn
+    g = torch.Generator().manual_seed(2)
+    n, h, w, c, cr = 3, 6, 5, 64, 16
+    y = torch.randn(n, h, w, c, generator=g)
+    idn = torch.randn(n, h, w, c, generator=g)
+    w1, b1 = torch.randn(cr, c, 1, 1, generator=g) * 0.2, torch.randn(cr, generator=g) * 0.1
+    w2, b2 = torch.randn(c, cr, 1, 1, generator=g) * 0.2, torch.randn(c, generator=g) * 0.1
+    dout = torch.randn(n, h, w, c, generator=g)
+    ts = [t.clone().to(gpu_device).requires_grad_(True) for t in (y, idn, w1, b1, w2, b2)]
+    out = SEGateFn.apply(*ts)
+    (out * dout.to(gpu_device)).sum().backward()
+    rs = [t.clone().requires_grad_(True) for t in (y, idn, w1, b1, w2, b2)]
+    yy = rs[0].permute(0, 3, 1, 2)
+    gt = F.adaptive_avg_pool2d(yy, 1)
+    gt = torch.sigmoid(F.conv2d(F.silu(F.conv2d(gt, rs[2], rs[3])), rs[4], rs[5]))
+    ref = (yy * gt).permute(0, 2, 3, 1) + rs[1]
+    assert rel(out, ref.detach()) < 1e-5
+    (ref * dout).sum().backward()
+    for a, r in zip(ts, rs):
+        assert rel(a.grad, r.grad) < 1e-4
+
+
+def test_pool_upsample_tokens_backward(gpu_device):
+    T = OT()
+    x = torch.randn(2, 8, 6, 16)
+    dy = torch.randn(2, 4, 3, 16)
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    F.max_pool2d(xr, 2, 2).backward(dy.permute(0, 3, 1, 2))
+    dx = T.maxpool2x2_backward(x.to(gpu_device), dy.to(gpu_device))
+    assert rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-6
+    big = torch.randn(2, 8, 6, 16)
+    db = T.upsample_backward(big.to(gpu_device), 4, 3)
+    small = torch.zeros(2, 16, 4, 3, requires_grad=True)
+    F.interpolate(small, size=(8, 6), mode="nearest").backward(big.permute(0, 3, 1, 2))
+    assert rel(db.permute(0, 3, 1, 2), small.grad) < 1e-6
+    tok = torch.randn(2, 5, 8)
+    cls, pos = torch.randn(8), torch.randn(6, 8)
+    z = T.vit_assemble(tok.to(gpu_device), cls.to(gpu_device), pos.to(gpu_device))
+    zr = torch.cat([cls.expand(2, 1, 8), tok], 1) + pos
+    assert rel(z, zr) < 1e-6
+    dz = torch.randn(2, 6, 8)
+    dx, dcls, dpos = T.vit_assemble_backward(dz.to(gpu_device))
+    assert rel(dx, dz[:, 1:]) < 1e-6 and rel(dcls, dz[:, 0].sum(0)) < 1e-6 and rel(dpos, dz.sum(0)) < 1e-6
+
+
+# ------------------------------------------------------------------ loss / optimizer
+@pytest.mark.parametrize("empty_scale", [False, True])
+def test_yolo_loss_matches_oracle(gpu_device, empty_scale):
+    from hv_amd.targets import synthetic_targets
+    from oracle import hv_oracle as O
+    T = OT()
+    B, S, A = 2, 128, 3
+    tg = synthetic_targets(B, S, seed=5)
+    if empty_scale:
+        tg[2].zero_()
+    g = torch.Generator().manual_seed(9)
+    preds, lgs = {}, []
+    for s, t in enumerate(tg):
+        h, w = t.shape[2], t.shape[3]
+        p = torch.randn(B, A, h, w, 85, generator=g)
+        preds[f"scale_{s}"] = p.clone().requires_grad_(True)
+        lgs.append(p.permute(0, 2, 3, 1, 4).reshape(B, h, w, A * 85).contiguous())
+    ref = O.yolo_loss(preds, tg)
+    ref["total_loss"].backward()
+    total = 0.0
+    for s, (lg, t) in enumerate(zip(lgs, tg)):
+        sums, dl = T.yolo_loss(lg.to(gpu_device), t.to(gpu_device), A, (5.0, 1.0, 0.5, 1.0))
+        total += sums[4].item()
+        B_, h, w, _ = lg.shape
+        gr = preds[f"scale_{s}"].grad
+        if gr is None:                       # scale without objects: the reference skips it
+            assert dl.abs().max().item() == 0 and sums[4].item() == 0
+            continue
+        dref = gr.permute(0, 2, 3, 1, 4).reshape(B_, h, w, -1)
+        assert rel(dl, dref) < 1e-5
+    assert abs(total - ref["total_loss"].item()) < 1e-4 * abs(ref["total_loss"].item())
+
+
+def test_fused_adamw_and_clipping_match_torch(gpu_device):
+    from hv_amd.trainer import FusedAdamW, mhc_group
+    torch.manual_seed(0)
+    named = [("a.mhc.w", torch.randn(1000)), ("b.H_res_raw", torch.randn(33, 7)), ("c.conv.weight", torch.randn(4097)),
+             ("d.bias", torch.randn(5))]
+    mine = [(n, t.clone().to(gpu_device).requires_grad_(True)) for n, t in named]
+    ref = [(n, t.clone().requires_grad_(True)) for n, t in named]
+    opt = FusedAdamW(mine, lr=1e-2, weight_decay=1e-2, max_norms=(0.5, 1.0))
+    topt = torch.optim.AdamW([p for _, p in ref], lr=1e-2, weight_decay=1e-2, eps=1e-8)
+    for step in range(3):
+        gs = [torch.randn_like(t) * (3.0 if i % 2 else 0.1) for i, (_, t) in enumerate(named)]
+        for (_, p), gr in zip(mine, gs):
+            p.grad = gr.clone().to(gpu_device)
+        for (_, p), gr in zip(ref, gs):
+            p.grad = gr.clone()
+        opt.step(clip=True)
+        for grp in (0, 1):
+            torch.nn.utils.clip_grad_norm_([p for n, p in ref if mhc_group(n) == grp], 0.5 if grp == 0 else 1.0)
+        topt.step()
+    for (_, a), (_, b) in zip(mine, ref):
+        assert rel(a.detach(), b.detach()) < 1e-5
+
+
+# ------------------------------------------------------------------ full model
+def _tiny_model(gpu_device, precision="fp32"):
+    from hv_amd import HybridVisionSystem
+    from oracle import weights as W
+    m = HybridVisionSystem(dict(num_blocks=[1, 1, 1, 1], vit_depth=1, sk_iters=5, verbose=False,
+                                precision=precision))
+    W.load_formula_weights(m, "wc")
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(gpu_device).train()
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            mod.p = 0.0
+    return m, sd
+
+
+def test_tiny_train_step_grads_match_oracle(gpu_device):
+    """Loss and every parameter gradient of one tiny-config training step (BN batch stats,
+    dropout off) vs autograd of the oracle in fp64.  This configuration is ill-conditioned
+    (BatchNorm over 8 values at stage 4): the oracle's OWN fp32 gradients sit ~1% (median)
+    from its fp64 ones, so each parameter must be within 3x the oracle-fp32 error (+1e-3)."""
+    from hv_amd.targets import synthetic_targets
+    from oracle import hv_oracle as O
+    m, sd = _tiny_model(gpu_device)
+    B, S = 2, 64
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+    tg = synthetic_targets(B, S, seed=3)
+    out = m(x.to(gpu_device), targets=[t.to(gpu_device) for t in tg], compute_loss=True)
+    out["loss"]["total_loss"].backward()
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        sdo = {k: (v.to(dt).requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+        with O.train_mode():
+            ref = O.system_forward(sdo, x.to(dt), O.TINY)
+        lref = O.yolo_loss(ref["predictions"], [t.to(dt) for t in tg])
+        lref["total_loss"].backward()
+        grads[dt] = {k: v.grad for k, v in sdo.items() if v.is_floating_point()}
+        if dt == torch.float64:
+            assert abs(out["loss"]["total_loss"].item() / lref["total_loss"].item() - 1) < 1e-4
+            for s in range(3):
+                a = out["predictions"][f"scale_{s}"].detach().cpu()
+                assert (a - ref["predictions"][f"scale_{s}"].detach()).abs().max().item() < 1e-3
+    bad = []
+    gmax = max(g.norm().item() for g in grads[torch.float64].values() if g is not None)
+    for name, p in m.named_parameters():
+        r = grads[torch.float64][name]
+        if r is None:
+            assert p.grad is None or p.grad.abs().max().item() < 1e-6, name
+            continue
+        if r.norm().item() < 1e-7 * gmax:
+            # structurally zero (conv bias before BatchNorm, a bias shared by every key of a
+            # softmax): only rounding noise is left -- it must stay at the noise level
+            assert p.grad.norm().item() < 1e-5 * gmax, name
+            continue
+        r32 = grads[torch.float32][name].double()
+        mine = p.grad.double().cpu()
+        e_ref = (r32 - r).norm().item()
+        e = (mine - r).norm().item()
+        if e > 3 * e_ref + 1e-3 * r.norm().item() + 1e-9:
+            bad.append((name, e / (r.norm().item() + 1e-30), e_ref / (r.norm().item() + 1e-30)))
+    assert not bad, bad[:10]
+
+
+def test_tiny_train_step_bf16_runs_and_agrees(gpu_device):
+    """bf16 activations through the whole training step.  The model's gradient at init is so
+    ill-conditioned that the oracle's own fp32 gradients are ~1% (median) away from fp64
+    (see test above) -- bf16 rounding (2^16 x larger) leaves no per-parameter agreement to
+    test at model level, so this checks finiteness and the loss; per-op bf16 gradients are
+    pinned by the kernel/layer tests above (e.g. test_mhc_bf16_train_agreement)."""
+    from hv_amd.targets import synthetic_targets
+    m32, _ = _tiny_model(gpu_device, "fp32")
+    m16, _ = _tiny_model(gpu_device, "bf16")
+    B, S = 2, 64
+    x = torch.randn(B, 3, S, S, device=gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=3)]
+    l32 = m32(x, targets=tg, compute_loss=True)["loss"]["total_loss"]
+    l32.backward()
+    l16 = m16(x, targets=tg, compute_loss=True)["loss"]["total_loss"]
+    l16.backward()
+    assert abs(l16.item() / l32.item() - 1) < 0.15
+    for p in m16.parameters():
+        if p.grad is not None:
+            assert torch.isfinite(p.grad).all()
+
+
+def test_trainer_step_reduces_loss(gpu_device):
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer
+    m, _ = _tiny_model(gpu_device, "bf16")
+    tr = HVTrainer(m, lr=1e-3)
+    B, S = 2, 64
+    x = torch.randn(B, 3, S, S, device=gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=3)]
+    losses = [tr.step(x, tg)["total_loss"].item() for _ in range(6)]
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0]

@@ -153,3 +153,43 @@ def _check_model(tag, tiny, fam, S, B, sub):
         sure = g[f"margin{s}"] >= 1e-4
         assert (ci[sure] == g[f"cls{s}_f64"][sure]).all()
     np.testing.assert_allclose(out["final_features"].numpy(), g["final_features_f64"], rtol=0, atol=1e-4)
+
+
+def test_train_step_oracle_matches_reference():
+    """Row T: the oracle's training-mode forward (BN batch statistics), YOLOLoss and autograd
+    against the reference itself (tests/golden/train_tiny_64_b2: oracle/gen_golden.py G5)."""
+    import json
+    import os
+    import sys
+    from conftest import GOLDEN, PKG
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    from hv_amd.targets import synthetic_targets
+    g = golden("train_tiny_64_b2")
+    names = json.load(open(os.path.join(GOLDEN, "train_tiny_param_names.json")))
+    sd = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v)
+          for k, v in formula_state_dict("tiny", "wc").items()}
+    B, S = int(g["B"]), int(g["S"])
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1)).double()
+    tg = [t.double() for t in synthetic_targets(B, S, seed=3)]
+    with O.train_mode():
+        out = O.system_forward(sd, x, O.TINY)
+    loss = O.yolo_loss(out["predictions"], tg)
+    loss["total_loss"].backward()
+    assert abs(loss["total_loss"].item() / float(g["total_loss_f64"]) - 1) < 1e-6  # fixture stored as fp32
+    for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
+        assert abs(loss[k] - float(g[k + "_f64"])) <= 1e-6 * max(1.0, abs(float(g[k + "_f64"])))
+    for s in range(3):
+        np.testing.assert_allclose(out["predictions"][f"scale_{s}"].detach().numpy(), g[f"pred{s}_f64"],
+                                   rtol=0, atol=1e-5)
+    gn = g["grad_norm_f64"]
+    for i, n in enumerate(names):
+        mine = sd[n].grad
+        if gn[i] < 0:
+            assert mine is None or float(mine.abs().max()) == 0.0, n
+            continue
+        assert abs(float(mine.norm()) - gn[i]) <= 1e-6 * max(gn[i], 1e-3), (n, float(mine.norm()), gn[i])
+    for key in g.files:
+        if key.startswith("g:") and key.endswith("_f64"):
+            n = key[2:-4]
+            np.testing.assert_allclose(sd[n].grad.numpy(), g[key], rtol=1e-6, atol=1e-9)
