@@ -7,6 +7,8 @@
 // All reductions are two-pass with a fixed order (bitwise reproducible run to run).
 #include "hv_common.h"
 
+#define HV_CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
 namespace {
 
 template <typename T> __device__ __forceinline__ float ld(const T* p, long i);
@@ -68,7 +70,7 @@ __global__ void k_conv_grad_reorder(const float* __restrict__ g, int cout, int c
 }
 
 // ------------------------------------------------------------------ column reductions
-// chunking of `rows` for two-pass column reductions (shared by colsum / BN / chan_dot)
+// chunking of `rows` for the simple two-pass column reduction (wide rows only)
 __host__ __device__ inline int red_chunks(long rows) {
   long c = (rows + 63) / 64;
   return (int)(c > 1024 ? 1024 : (c < 1 ? 1 : c));
@@ -95,36 +97,207 @@ __global__ void k_colsum_final(const float* part, int nchunk, int cols, float* o
   out[col] = accumulate ? out[col] + s : s;
 }
 
-// ------------------------------------------------------------------ BatchNorm (train)
-template <typename T>
-__global__ void __launch_bounds__(256) k_bn_part(const T* __restrict__ x, long rows, int c, int nchunk,
-                                                 float* part) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  const int ch = blockIdx.y;
-  if (col >= c) return;
-  const long per = (rows + nchunk - 1) / nchunk;
-  const long r0 = ch * per, r1 = min(rows, r0 + per);
-  float s = 0.f, ss = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    const float v = ld<T>(x, r * c + col);
-    s += v;
-    ss += v * v;
-  }
-  part[((long)ch * 2) * c + col] = s;
-  part[((long)ch * 2 + 1) * c + col] = ss;
+// Generic coalesced column reduction over token-major [rows, cols] tensors: each thread owns
+// 4 consecutive columns (8-byte bf16 / 16-byte fp32 loads), RPI = 256 / (cols/4) rows advance
+// together, block partials are combined in LDS, and k_colred_final sums the block partials
+// (8 row-groups x 32 columns per block) in a fixed order.
+//   CR_SUM     sum a                                  (bias gradients)
+//   CR_SUMSQ   sum a, sum a^2                         (BatchNorm batch statistics)
+//   CR_BNBWD   sum g, sum g*xhat,  g = dy act'(xhat gamma + beta), xhat = (x - mean) rstd
+//   CR_DOT     sum a*b (b NULL: sum a) per image       (SE gate / broadcast-add backward)
+//   CR_ROWN    sum g*xhat, sum g,  g = dy keep, xhat = (x - mean_row) rstd_row  (LN/RMS params)
+enum { CR_SUM = 0, CR_SUMSQ = 1, CR_BNBWD = 2, CR_DOT = 3, CR_ROWN = 4 };
+
+struct ColRed {
+  const void* a;       // x (or dy for CR_SUM / CR_DOT)
+  const void* b;       // dy (CR_BNBWD / CR_ROWN) or the second factor (CR_DOT)
+  long rows;           // rows per image (CR_DOT) or total
+  int cols;
+  const float* mean;   // per column (BN) or per row (ROWN, may be NULL for RMS)
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  float p;
+  uint32_t seed;
+};
+
+template <typename T> __device__ __forceinline__ void ld4(const T* p, long i, float (&v)[4]);
+template <> __device__ __forceinline__ void ld4<float>(const float* p, long i, float (&v)[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p + i);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+template <> __device__ __forceinline__ void ld4<unsigned short>(const unsigned short* p, long i, float (&v)[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p + i);
+  v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+  v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
 }
 
-__global__ void k_bn_final(const float* part, int nchunk, int c, long rows, float eps, float momentum,
-                           float* mean, float* rstd, float* rmean, float* rvar) {
+template <int MODE> struct CrNV { static constexpr int V = (MODE == CR_SUM || MODE == CR_DOT) ? 1 : 2; };
+
+template <typename TA, typename TB, int MODE, int NCH>
+__global__ void __launch_bounds__(256) k_colred(const ColRed r, int nblk, float* part) {
+  constexpr int NV = CrNV<MODE>::V;
+  __shared__ float sm[NV * 1024];
+  const int cpr = r.cols >> 2;
+  const int rpi = cpr <= 256 ? 256 / cpr : 1;
+  const int tid = threadIdx.x;
+  const int rsub = cpr <= 256 ? tid / cpr : 0;
+  const int img = blockIdx.y;
+  const long base = (long)img * r.rows * r.cols;
+  float acc[NV][NCH][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[v][c][j] = 0.f;
+  if (rsub < rpi) {
+    for (long r0 = (long)blockIdx.x * rpi; r0 < r.rows; r0 += (long)nblk * rpi) {
+      const long row = r0 + rsub;
+      if (row >= r.rows) break;
+      float rmu = 0.f, rrs = 1.f;
+      if constexpr (MODE == CR_ROWN) {
+        rmu = r.mean ? r.mean[row] : 0.f;
+        rrs = r.rstd[row];
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
+        if (ch >= cpr) continue;
+        const int col = ch * 4;
+        const long o = base + row * r.cols + col;
+        float a[4];
+        ld4<TA>((const TA*)r.a, o, a);
+        if constexpr (MODE == CR_SUM) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
+        } else if constexpr (MODE == CR_SUMSQ) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { acc[0][c][j] += a[j]; acc[1][c][j] += a[j] * a[j]; }
+        } else if constexpr (MODE == CR_DOT) {
+          if (r.b) {
+            float b[4];
+            ld4<TB>((const TB*)r.b, o, b);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j] * b[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
+          }
+        } else if constexpr (MODE == CR_BNBWD) {
+          float b[4];
+          ld4<TB>((const TB*)r.b, o, b);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = col + j;
+            const float xh = (a[j] - r.mean[cc]) * r.rstd[cc];
+            const float g = b[j] * hv_act_grad(xh * (r.gamma ? r.gamma[cc] : 1.f) + (r.beta ? r.beta[cc] : 0.f), r.act);
+            acc[0][c][j] += g;
+            acc[1][c][j] += g * xh;
+          }
+        } else {  // CR_ROWN
+          float b[4];
+          ld4<TB>((const TB*)r.b, o, b);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xh = (a[j] - rmu) * rrs;
+            const float g = b[j] * hv_drop_scale(r.seed, (unsigned long long)(o + j), r.p);
+            acc[0][c][j] += g * xh;
+            acc[1][c][j] += g;
+          }
+        }
+      }
+    }
+  }
+  float* out = part + ((long)img * nblk + blockIdx.x) * NV * r.cols;
+  if (cpr <= 256) {
+    // combine the rpi row groups of the block in LDS (rpi * cols <= 1024)
+    if (rsub < rpi) {
+      const int col = (tid % cpr) * 4;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[v * 1024 + rsub * r.cols + col + j] = acc[v][0][j];
+    }
+    __syncthreads();
+    for (int i = tid; i < NV * r.cols; i += 256) {
+      const int v = i / r.cols, col = i - v * r.cols;
+      float t = 0.f;
+      for (int q = 0; q < rpi; ++q) t += sm[v * 1024 + q * r.cols + col];
+      out[i] = t;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ch = tid + 256 * c;
+      if (ch >= cpr) continue;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[v * r.cols + ch * 4 + j] = acc[v][c][j];
+    }
+  }
+}
+
+// sums[img][i] (+)= sum over the nblk partials of column i (i < width); 8 row groups x 32 columns
+__global__ void __launch_bounds__(256) k_colred_final(const float* part, int nblk, int width, float* sums,
+                                                      int accumulate) {
+  __shared__ float sm[8][33];
+  const int img = blockIdx.y;
+  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + c;
+  float t = 0.f;
+  if (col < width)
+    for (int b = g; b < nblk; b += 8) t += part[((long)img * nblk + b) * width + col];
+  sm[g][c] = t;
+  __syncthreads();
+  if (g == 0 && col < width) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += sm[q][c];
+    float* o = sums + (long)img * width + col;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+inline int colred_blocks(long rows, int cols, int imgs) {
+  const int cpr = cols / 4;
+  const int rpi = cpr <= 256 ? 256 / cpr : 1;
+  long b = (rows + (long)rpi * 8 - 1) / ((long)rpi * 8);
+  const long cap = imgs > 1 ? (512 / imgs > 8 ? 512 / imgs : 8) : 512;
+  b = b > cap ? cap : (b < 1 ? 1 : b);
+  return (int)b;
+}
+
+inline bool colred_ok(int cols) { return cols % 4 == 0 && cols / 4 <= 1024; }
+
+inline size_t colred_work(long rows, int cols, int imgs, int nv) {
+  return (size_t)imgs * colred_blocks(rows, cols, imgs) * nv * cols;
+}
+
+// launch part + final; sums receives [imgs][NV*cols] (NV-major per image)
+template <typename TA, typename TB, int MODE>
+int colred_run(const ColRed& r, int imgs, float* work, float* sums, int accumulate, hipStream_t s) {
+  constexpr int NV = CrNV<MODE>::V;
+  const int nblk = colred_blocks(r.rows, r.cols, imgs);
+  const int cpr = r.cols / 4;
+  dim3 grid(nblk, imgs);
+  if (cpr <= 256) k_colred<TA, TB, MODE, 1><<<grid, 256, 0, s>>>(r, nblk, work);
+  else if (cpr <= 512) k_colred<TA, TB, MODE, 2><<<grid, 256, 0, s>>>(r, nblk, work);
+  else k_colred<TA, TB, MODE, 4><<<grid, 256, 0, s>>>(r, nblk, work);
+  k_colred_final<<<dim3(hv_cdiv(NV * r.cols, 32), imgs), 256, 0, s>>>(work, nblk, NV * r.cols, sums, accumulate);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+// ------------------------------------------------------------------ BatchNorm (train)
+__global__ void k_bn_stats_post(const float* sums, int c, long rows, float eps, float momentum, float* mean,
+                                float* rstd, float* rmean, float* rvar) {
   const int col = blockIdx.x * 256 + threadIdx.x;
   if (col >= c) return;
-  double s = 0.0, ss = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    s += part[((long)k * 2) * c + col];
-    ss += part[((long)k * 2 + 1) * c + col];
-  }
-  const double m = s / (double)rows;
-  double var = ss / (double)rows - m * m;
+  const double m = (double)sums[col] / (double)rows;
+  double var = (double)sums[c + col] / (double)rows - m * m;
   var = var < 0.0 ? 0.0 : var;
   mean[col] = (float)m;
   rstd[col] = (float)(1.0 / sqrt(var + (double)eps));
@@ -135,6 +308,13 @@ __global__ void k_bn_final(const float* part, int nchunk, int c, long rows, floa
   }
 }
 
+__global__ void k_bn_bwd_post(const float* sums, int c, float* dgamma, float* dbeta) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= c) return;
+  if (dbeta) dbeta[col] = sums[col];
+  if (dgamma) dgamma[col] = sums[c + col];
+}
+
 template <typename T>
 __global__ void k_bn_apply(const T* __restrict__ x, long total, int c, const float* mean, const float* rstd,
                            const float* g, const float* b, int act, T* y) {
@@ -143,41 +323,6 @@ __global__ void k_bn_apply(const T* __restrict__ x, long total, int c, const flo
     const float z = (ld<T>(x, i) - mean[col]) * rstd[col] * (g ? g[col] : 1.f) + (b ? b[col] : 0.f);
     st<T>(y, i, hv_act(z, act));
   }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) k_bn_bwd_part(const T* __restrict__ x, const T* __restrict__ dy, long rows,
-                                                     int c, const float* mean, const float* rstd, const float* g,
-                                                     const float* b, int act, int nchunk, float* part) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  const int ch = blockIdx.y;
-  if (col >= c) return;
-  const long per = (rows + nchunk - 1) / nchunk;
-  const long r0 = ch * per, r1 = min(rows, r0 + per);
-  const float mu = mean[col], rs = rstd[col], gg = g ? g[col] : 1.f, bb = b ? b[col] : 0.f;
-  float sg = 0.f, sgx = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    const float xh = (ld<T>(x, r * c + col) - mu) * rs;
-    const float gr = ld<T>(dy, r * c + col) * hv_act_grad(xh * gg + bb, act);
-    sg += gr;
-    sgx += gr * xh;
-  }
-  part[((long)ch * 2) * c + col] = sg;
-  part[((long)ch * 2 + 1) * c + col] = sgx;
-}
-
-__global__ void k_bn_bwd_final(const float* part, int nchunk, int c, float* dgamma, float* dbeta, float* sums) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= c) return;
-  float sg = 0.f, sgx = 0.f;
-  for (int k = 0; k < nchunk; ++k) {
-    sg += part[((long)k * 2) * c + col];
-    sgx += part[((long)k * 2 + 1) * c + col];
-  }
-  if (dgamma) dgamma[col] = sgx;
-  if (dbeta) dbeta[col] = sg;
-  sums[col] = sg;
-  sums[c + col] = sgx;
 }
 
 template <typename T>
@@ -286,18 +431,6 @@ __global__ void __launch_bounds__(256) k_rownorm_bwd(int mode, const TX* __restr
   }
 }
 
-__global__ void k_rownorm_param_final(const float* wpart, int nwaves, int cols, float* dgamma, float* dbeta) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
-  float a = 0.f, b = 0.f;
-  for (int w = 0; w < nwaves; ++w) {
-    a += wpart[(long)w * 2 * cols + col];
-    b += wpart[(long)w * 2 * cols + cols + col];
-  }
-  if (dgamma) dgamma[col] = a;
-  if (dbeta) dbeta[col] = b;
-}
-
 // ------------------------------------------------------------------ elementwise
 template <typename T>
 __global__ void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ pre, long n, int act, float p,
@@ -313,31 +446,6 @@ __global__ void k_dropout(const T* __restrict__ x, long n, float p, uint32_t see
 }
 
 // ------------------------------------------------------------------ SE / pooling / upsample
-template <typename T>
-__global__ void __launch_bounds__(256) k_chan_dot_part(const T* __restrict__ a, const T* __restrict__ b, int hw,
-                                                       int c, int nchunk, float* part) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  const int img = blockIdx.z, ch = blockIdx.y;
-  if (col >= c) return;
-  const long per = (hw + nchunk - 1) / nchunk;
-  const long r0 = ch * per, r1 = min((long)hw, r0 + per);
-  const long base = (long)img * hw * c;
-  float s = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    const long i = base + r * c + col;
-    s += b ? ld<T>(a, i) * ld<T>(b, i) : ld<T>(a, i);
-  }
-  part[((long)img * nchunk + ch) * c + col] = s;
-}
-
-__global__ void k_chan_dot_final(const float* part, int n, int nchunk, int c, float* out) {
-  const int col = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
-  if (col >= c) return;
-  float s = 0.f;
-  for (int k = 0; k < nchunk; ++k) s += part[((long)img * nchunk + k) * c + col];
-  out[(long)img * c + col] = s;
-}
-
 // per image: recompute the SE MLP and backpropagate dgate -> dpooled; keep ds / act / dh for
 // the parameter reductions.  work per image: [c ds][cr act][cr dh]
 __global__ void __launch_bounds__(256) k_se_bwd_img(const float* pooled, const float* dgate, int c, int cr,
@@ -603,21 +711,28 @@ __global__ void __launch_bounds__(256) k_grad_sq(const hv_param_entry* tab, int 
     }
   }
   s = block_sum(s, scratch);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s;
+    reinterpret_cast<int*>(part)[gridDim.x + blockIdx.x] = e.group;   // group of this block
+  }
 }
 
-__global__ void __launch_bounds__(256) k_grad_norm_final(const hv_param_entry* tab, int count, int nblk,
-                                                         const float* part, int groups, float m0, float m1, float m2,
-                                                         float m3, float* norms, float* coefs) {
+__global__ void __launch_bounds__(256) k_grad_norm_final(int nblk, const float* part, int groups, float m0,
+                                                         float m1, float m2, float m3, float* norms, float* coefs) {
   __shared__ float scratch[16];
   const float mx[4] = {m0, m1, m2, m3};
+  const int* grp = reinterpret_cast<const int*>(part) + nblk;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nblk; b += 256) {
+    const int g = grp[b];
+    const double v = part[b];
+    acc[0] += g == 0 ? v : 0.0;
+    acc[1] += g == 1 ? v : 0.0;
+    acc[2] += g == 2 ? v : 0.0;
+    acc[3] += g == 3 ? v : 0.0;
+  }
   for (int g = 0; g < groups; ++g) {
-    double s = 0.0;
-    for (int b = threadIdx.x; b < nblk; b += 256) {
-      const int ei = find_param(tab, count, b);
-      if (tab[ei].group == g) s += part[b];
-    }
-    const float tot = block_sum((float)s, scratch);
+    const float tot = block_sum((float)acc[g], scratch);
     if (threadIdx.x == 0) {
       const float nrm = sqrtf(tot);
       norms[g] = nrm;
@@ -679,12 +794,20 @@ extern "C" int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, fl
   return HV_OK;
 }
 
-extern "C" size_t hv_colsum_work_floats(int rows, int cols) { return (size_t)red_chunks(rows) * cols; }
+extern "C" size_t hv_colsum_work_floats(int rows, int cols) {
+  return colred_ok(cols) ? colred_work(rows, cols, 1, 1) : (size_t)red_chunks(rows) * cols;
+}
 
 extern "C" int hv_colsum(int dtype, const void* x, long ldx, int rows, int cols, float* out, int accumulate,
                          float* work, hv_stream_t stream) {
   if (!x || !out || !work || rows <= 0 || cols <= 0) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (colred_ok(cols) && ldx == cols) {
+    ColRed r{};
+    r.a = x; r.rows = rows; r.cols = cols;
+    HV_DISPATCH(dtype, (colred_run<T, T, CR_SUM>(r, 1, work, out, accumulate, s)));
+    return HV_OK;
+  }
   const int nch = red_chunks(rows);
   dim3 grid(hv_cdiv(cols, 256), nch);
   HV_DISPATCH(dtype, (k_colsum_part<T><<<grid, 256, 0, s>>>((const T*)x, ldx, rows, cols, nch, work)));
@@ -693,16 +816,17 @@ extern "C" int hv_colsum(int dtype, const void* x, long ldx, int rows, int cols,
   return HV_OK;
 }
 
-extern "C" size_t hv_bn_work_floats(int rows, int c) { return (size_t)red_chunks(rows) * 2 * c + 2 * (size_t)c; }
+extern "C" size_t hv_bn_work_floats(int rows, int c) { return colred_work(rows, c, 1, 2) + 2 * (size_t)c; }
 
 extern "C" int hv_bn_stats(int dtype, const void* x, int rows, int c, float eps, float momentum, float* mean,
                            float* rstd, float* running_mean, float* running_var, float* work, hv_stream_t stream) {
-  if (!x || !mean || !rstd || !work || rows <= 0 || c <= 0) return HV_EINVAL;
+  if (!x || !mean || !rstd || !work || rows <= 0 || c <= 0 || !colred_ok(c)) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const int nch = red_chunks(rows);
-  dim3 grid(hv_cdiv(c, 256), nch);
-  HV_DISPATCH(dtype, (k_bn_part<T><<<grid, 256, 0, s>>>((const T*)x, rows, c, nch, work)));
-  k_bn_final<<<hv_cdiv(c, 256), 256, 0, s>>>(work, nch, c, rows, eps, momentum, mean, rstd, running_mean, running_var);
+  float* sums = work + colred_work(rows, c, 1, 2);
+  ColRed r{};
+  r.a = x; r.rows = rows; r.cols = c;
+  HV_DISPATCH(dtype, (colred_run<T, T, CR_SUMSQ>(r, 1, work, sums, 0, s)));
+  k_bn_stats_post<<<hv_cdiv(c, 256), 256, 0, s>>>(sums, c, rows, eps, momentum, mean, rstd, running_mean, running_var);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -720,14 +844,14 @@ extern "C" int hv_bn_apply(int dtype, const void* x, int rows, int c, const floa
 extern "C" int hv_bn_backward(int dtype, const void* x, const void* dy, int rows, int c, const float* mean,
                               const float* rstd, const float* gamma, const float* beta, int act, void* dx,
                               float* dgamma, float* dbeta, float* work, hv_stream_t stream) {
-  if (!x || !dy || !dx || !work || rows <= 0 || c <= 0) return HV_EINVAL;
+  if (!x || !dy || !dx || !work || rows <= 0 || c <= 0 || !colred_ok(c)) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const int nch = red_chunks(rows);
-  float* sums = work + (size_t)nch * 2 * c;
-  dim3 grid(hv_cdiv(c, 256), nch);
-  HV_DISPATCH(dtype, (k_bn_bwd_part<T><<<grid, 256, 0, s>>>((const T*)x, (const T*)dy, rows, c, mean, rstd, gamma,
-                                                            beta, act, nch, work)));
-  k_bn_bwd_final<<<hv_cdiv(c, 256), 256, 0, s>>>(work, nch, c, dgamma, dbeta, sums);
+  float* sums = work + colred_work(rows, c, 1, 2);     // [sum g | sum g xhat]
+  ColRed r{};
+  r.a = x; r.b = dy; r.rows = rows; r.cols = c;
+  r.mean = mean; r.rstd = rstd; r.gamma = gamma; r.beta = beta; r.act = act;
+  HV_DISPATCH(dtype, (colred_run<T, T, CR_BNBWD>(r, 1, work, sums, 0, s)));
+  k_bn_bwd_post<<<hv_cdiv(c, 256), 256, 0, s>>>(sums, c, dgamma, dbeta);
   const long total = (long)rows * c;
   HV_DISPATCH(dtype, (k_bn_bwd_apply<T><<<grid_for(total), 256, 0, s>>>((const T*)x, (const T*)dy, rows, c, mean,
                                                                         rstd, gamma, beta, act, sums, (T*)dx)));
@@ -754,16 +878,14 @@ extern "C" int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, 
 }
 
 static void rownorm_split(int rows, int* rows_per_wave, int* nwaves) {
-  int rpw = (rows + 4095) / 4096;           // <= 4096 waves
+  int rpw = (rows + 16383) / 16384;          // <= 16384 waves
   if (rpw < 1) rpw = 1;
   *rows_per_wave = rpw;
   *nwaves = (rows + rpw - 1) / rpw;
 }
 
 extern "C" size_t hv_rownorm_work_floats(int rows, int cols) {
-  int rpw, nw;
-  rownorm_split(rows, &rpw, &nw);
-  return (size_t)((nw + 3) / 4 * 4) * 2 * cols;
+  return colred_ok(cols) ? colred_work(rows, cols, 1, 2) + 2 * (size_t)cols : 0;
 }
 
 extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, const void* dy, int rows,
@@ -773,15 +895,14 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
   if (!x || !dy || !dx || !rstd || rows <= 0 || cols <= 0 || cols > 64 * RQ || (mode == 0 && !mean))
     return HV_EINVAL;
   const bool params = dgamma || dbeta;
-  if (params && !work) return HV_EINVAL;
+  if (params && (!work || !colred_ok(cols))) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   int rpw, nw;
   rownorm_split(rows, &rpw, &nw);
   const unsigned grid = hv_cdiv(nw, 4);
-  float* wp = params ? work : nullptr;
   // (x, dy, dx) dtype combinations used by the mHC / transformer paths
 #define RB_LAUNCH(TX, TD, TO) k_rownorm_bwd<TX, TD, TO><<<grid, 256, 0, s>>>(mode, (const TX*)x, (const TD*)dy, rows, \
-      cols, rpw, mean, rstd, gamma, drop_p, seed, (TO*)dx, (const TO*)dx_add, wp)
+      cols, rpw, mean, rstd, gamma, drop_p, seed, (TO*)dx, (const TO*)dx_add, nullptr)
   const int key = x_dtype * 4 + dy_dtype * 2 + dx_dtype;
   switch (key) {
     case 0: RB_LAUNCH(float, float, float); break;
@@ -797,9 +918,18 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
 #undef RB_LAUNCH
   HV_CHECK_LAUNCH();
   if (params) {
-    // waves of the last block past nw wrote nothing: only the first nw slots are summed
-    k_rownorm_param_final<<<hv_cdiv(cols, 256), 256, 0, s>>>(work, nw, cols, dgamma, dbeta);
-    HV_CHECK_LAUNCH();
+    float* sums = work + colred_work(rows, cols, 1, 2);   // [sum g xhat | sum g]
+    ColRed r{};
+    r.a = x; r.b = dy; r.rows = rows; r.cols = cols;
+    r.mean = mode == 0 ? mean : nullptr; r.rstd = rstd; r.p = drop_p; r.seed = seed;
+    int rc;
+    if (x_dtype == HV_F32 && dy_dtype == HV_F32) rc = colred_run<float, float, CR_ROWN>(r, 1, work, sums, 0, s);
+    else if (x_dtype == HV_F32) rc = colred_run<float, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
+    else if (dy_dtype == HV_F32) rc = colred_run<unsigned short, float, CR_ROWN>(r, 1, work, sums, 0, s);
+    else rc = colred_run<unsigned short, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
+    if (rc) return rc;
+    if (dgamma) HV_CHECK(hipMemcpyAsync(dgamma, sums, cols * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (dbeta) HV_CHECK(hipMemcpyAsync(dbeta, sums + cols, cols * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
   return HV_OK;
 }
@@ -821,17 +951,14 @@ extern "C" int hv_dropout(int dtype, const void* x, long n, float drop_p, unsign
   return HV_OK;
 }
 
-extern "C" size_t hv_chan_dot_work_floats(int n, int hw, int c) { return (size_t)n * red_chunks(hw) * c; }
+extern "C" size_t hv_chan_dot_work_floats(int n, int hw, int c) { return colred_work(hw, c, n, 1); }
 
 extern "C" int hv_chan_dot(int dtype, const void* a, const void* b, int n, int hw, int c, float* out, float* work,
                            hv_stream_t stream) {
-  if (!a || !out || !work || n <= 0 || hw <= 0 || c <= 0) return HV_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
-  const int nch = red_chunks(hw);
-  dim3 grid(hv_cdiv(c, 256), nch, n);
-  HV_DISPATCH(dtype, (k_chan_dot_part<T><<<grid, 256, 0, s>>>((const T*)a, (const T*)b, hw, c, nch, work)));
-  k_chan_dot_final<<<dim3(hv_cdiv(c, 256), n), 256, 0, s>>>(work, n, nch, c, out);
-  HV_CHECK_LAUNCH();
+  if (!a || !out || !work || n <= 0 || hw <= 0 || c <= 0 || !colred_ok(c)) return HV_EINVAL;
+  ColRed r{};
+  r.a = a; r.b = b; r.rows = hw; r.cols = c;
+  HV_DISPATCH(dtype, (colred_run<T, T, CR_DOT>(r, n, work, out, 0, (hipStream_t)stream)));
   return HV_OK;
 }
 
@@ -938,7 +1065,7 @@ extern "C" int hv_grad_norms(const hv_param_entry* tab, int count, int total_blo
   k_grad_sq<<<total_blocks, 256, 0, s>>>(tab, count, work);
   float m[4] = {1.f, 1.f, 1.f, 1.f};
   for (int g = 0; g < groups; ++g) m[g] = max_norm[g];
-  k_grad_norm_final<<<1, 256, 0, s>>>(tab, count, total_blocks, work, groups, m[0], m[1], m[2], m[3], norms, coefs);
+  k_grad_norm_final<<<1, 256, 0, s>>>(total_blocks, work, groups, m[0], m[1], m[2], m[3], norms, coefs);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -155,7 +155,7 @@ class FusedAdamW:
             blk += lib.hv_param_blocks(p.numel())
         self._blocks = blk
         self._table = torch.frombuffer(bytearray(bytes(ents)), dtype=torch.uint8).to(self.device)
-        self._work = torch.empty(blk, device=self.device, dtype=torch.float32)
+        self._work = torch.empty(2 * blk, device=self.device, dtype=torch.float32)
 
     def step(self, clip: bool = True):
         key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named)

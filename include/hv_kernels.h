@@ -456,7 +456,8 @@ typedef struct hv_param_entry {
   int blk;            /* first block of this entry (prefix over entries) */
 } hv_param_entry;
 int hv_param_blocks(long n);
-/* norms[g] = ||grads of group g||_2 ; coefs[g] = min(1, max_norm[g] / (norms[g] + 1e-6)) */
+/* norms[g] = ||grads of group g||_2 ; coefs[g] = min(1, max_norm[g] / (norms[g] + 1e-6));
+   work: 2 * total_blocks floats */
 int hv_grad_norms(const hv_param_entry* dev_table, int count, int total_blocks, int groups,
                   const float* max_norm /* host [groups] */, float* norms, float* coefs, float* work,
                   hv_stream_t stream);

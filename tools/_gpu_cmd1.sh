@@ -1,8 +1,8 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/t3
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py -v --timeout 300 --timeout-method thread -k "tiny or trainer" > gpurun_out/t3/train_tests.log 2>&1
+mkdir -p gpurun_out/t5
+timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py -q --timeout 300 --timeout-method thread > gpurun_out/t5/train_tests.log 2>&1
 echo "train tests rc=$?"
-grep -E "FAIL|passed|failed|Error" gpurun_out/t3/train_tests.log | tail -30
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-latency > gpurun_out/t3/bench.json 2> gpurun_out/t3/bench.err; echo "bench rc=$?"; cut -c1-200 gpurun_out/t3/bench.json
-timeout -k 10 300 python -u tools/train_diag.py grads > gpurun_out/t3/diag.log 2>&1; echo "diag rc=$?"; cat gpurun_out/t3/diag.log | tail -32
-timeout -k 10 300 python -u tools/train_diag.py time 2 640 > gpurun_out/t3/time.log 2>&1; echo "time rc=$?"; tail -5 gpurun_out/t3/time.log
+grep -E "FAIL|passed|failed|Error" gpurun_out/t5/train_tests.log | tail -10
+timeout -k 10 300 python -u tools/train_diag.py time 8 640 > gpurun_out/t5/time8.log 2>&1; echo "time rc=$?"; tail -2 gpurun_out/t5/time8.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/t5/prof -o run --output-format csv -- python tools/train_diag.py time 8 640 > gpurun_out/t5/prof.log 2>&1; echo "prof rc=$?"
+f=$(find gpurun_out/t5/prof -name 'run_kernel_stats.csv' | head -1); python tools/prof_summary.py $(dirname $f) 5 40 > gpurun_out/t5/prof_summary.txt; head -42 gpurun_out/t5/prof_summary.txt
