@@ -45,6 +45,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--eager", dest="graph", action="store_false",
                     help="time host-launched steps instead of HIP-graph replays")
+    ap.add_argument("--train", dest="train", action="store_true", default=None,
+                    help="also time the training step (config C: base 640, bf16, DDP over RCCL when N>1); "
+                         "default: on at N=1, off at N>1")
+    ap.add_argument("--no-train", dest="train", action="store_false")
+    ap.add_argument("--train-batch", type=int, default=16)
+    ap.add_argument("--train-steps", type=int, default=4)
     return ap.parse_args()
 
 
@@ -113,6 +119,48 @@ def cpu_baseline(model_cpu_sd, size, threads):
     return {"value": round(n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n} single-image {size}x{size} fp32 forwards of the oracle (oracle/hv_oracle.py), "
                       f"same random-init weights, after 1 warmup"}
+
+
+def train_bench(a, dev, world, rank):
+    """Config C: base 640x640 bf16 training step -- train-mode forward, YOLOLoss on
+    synthetic COCO targets, backward (Sinkhorn autograd included), bucketed gradient all-reduce
+    over RCCL overlapped with the backward when N>1, per-group clipping, AdamW."""
+    from hv_amd import HybridVisionSystem
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer
+    torch.manual_seed(0)
+    model = HybridVisionSystem({"image_size": a.size, "precision": a.precision, "verbose": False}).to(dev).train()
+    tr = HVTrainer(model)
+    B = a.train_batch
+    x = torch.randn(B, 3, a.size, a.size, device=dev)
+    tg = [t.to(dev) for t in synthetic_targets(B, a.size, seed=1000 + rank)]
+    for _ in range(2):
+        tr.step(x, tg)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.train_steps):
+        loss = tr.step(x, tg)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    out = {"metric": "train images/s (forward + YOLOLoss + backward + all-reduce + clip + AdamW)",
+           "value": round(world * B * a.train_steps / el, 3), "unit": "images/s",
+           "ms_per_step": round(el / a.train_steps * 1e3, 2), "per_gpu_batch": B, "steps": a.train_steps,
+           "workload": f"hybrid_vision base {a.size}x{a.size} training, bf16 activations, fp32 params, "
+                       f"{'DDP RCCL' if world > 1 else 'single GPU'}",
+           "loss": round(loss["total_loss"].item(), 3),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+           "model_tflops_reference_graph": round(2095.9 * world * B * a.train_steps / el / 1e3, 2)}
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -200,6 +248,10 @@ def main():
         lat["note"] = ("hipGraph replay; 'recompute' re-runs Sinkhorn + coefficient prep per frame like the "
                        "reference, 'frozen' reuses them until a parameter changes (eval streaming)")
 
+    train = None
+    if a.train if a.train is not None else world == 1:
+        train = train_bench(a, dev, world, rank)
+
     imgs = world * a.batch * a.steps
     value = imgs / elapsed
     ms_step = elapsed / a.steps * 1e3
@@ -227,6 +279,7 @@ def main():
                          if a.graph else "eager",
             "eager_ms_per_step": round(eager_ms, 3),
             "latency": lat,
+            "training": train,
             "cpu_baseline": base,
         }
         print(json.dumps(line))

@@ -13,29 +13,67 @@
 #pragma once
 #include "hv_common.h"
 
-// Training epilogue modes (hv_gemm_desc.epi_mode 1/2, see hv_kernels.h).
+// Training epilogue modes (hv_gemm_desc.epi_mode 1/2, see hv_kernels.h).  A lane holds 4
+// consecutive columns: the pre-activation is stored / loaded as one 8-byte (bf16) or 16-byte
+// (fp32) vector when the row allows it.
 __device__ __forceinline__ void epi_train(const hv_gemm_desc& d, const f32x4& acc, float (&v)[4], int row, int col,
-                                       const float (&sc)[4], const float (&bi)[4], const float (&cs)[4],
-                                       float mean, float rstd, bool ln_epi) {
+                                          const float (&sc)[4], const float (&bi)[4], const float (&cs)[4],
+                                          float mean, float rstd, bool ln_epi) {
   const bool aux_bf = d.aux_dtype == HV_BF16;
+  const bool vec = col + 4 <= d.N && (d.ld_aux & 3) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
+  const long ai = (long)row * d.ld_aux + col;
+  const unsigned long long idx0 = (unsigned long long)row * d.N + col;
+  float z[4];
+  if (d.epi_mode == 1) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (col + j >= d.N) { v[j] = 0.f; continue; }
-    const unsigned long long idx = (unsigned long long)row * d.N + col + j;
-    const long ai = (long)row * d.ld_aux + col + j;
-    float x = acc[j];
-    if (d.epi_mode == 1) {
+    for (int j = 0; j < 4; ++j) {
+      float x = acc[j];
       if (ln_epi) x = rstd * (x - mean * cs[j]);
-      x = x * sc[j] + bi[j];
-      if (aux_bf) ((unsigned short*)d.aux)[ai] = f2bf(x);
-      else ((float*)d.aux)[ai] = x;
-      // the activation sees the value the backward will see (rounded when stored in bf16)
-      const float z = aux_bf ? bf2f(f2bf(x)) : x;
-      v[j] = hv_act(z, d.act) * hv_drop_scale(d.drop_seed, idx, d.drop_p);
-    } else {
-      const float z = aux_bf ? bf2f(((const unsigned short*)d.aux)[ai]) : ((const float*)d.aux)[ai];
-      v[j] = x * d.alpha * hv_drop_scale(d.drop_seed, idx, d.drop_p) * hv_act_grad(z, d.act);
+      z[j] = x * sc[j] + bi[j];
     }
+    if (vec) {
+      if (aux_bf) {
+        const uint2 pk = make_uint2(pack_bf16x2(z[0], z[1]), pack_bf16x2(z[2], z[3]));
+        *reinterpret_cast<uint2*>((unsigned short*)d.aux + ai) = pk;
+        // the activation sees the value the backward will see (rounded when stored in bf16)
+        z[0] = __uint_as_float(pk.x << 16); z[1] = __uint_as_float(pk.x & 0xffff0000u);
+        z[2] = __uint_as_float(pk.y << 16); z[3] = __uint_as_float(pk.y & 0xffff0000u);
+      } else {
+        *reinterpret_cast<float4*>((float*)d.aux + ai) = make_float4(z[0], z[1], z[2], z[3]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (col + j >= d.N) break;
+        if (aux_bf) {
+          ((unsigned short*)d.aux)[ai + j] = f2bf(z[j]);
+          z[j] = bf2f(f2bf(z[j]));
+        } else {
+          ((float*)d.aux)[ai + j] = z[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
+  } else {
+    if (vec) {
+      if (aux_bf) {
+        const uint2 t = *reinterpret_cast<const uint2*>((const unsigned short*)d.aux + ai);
+        z[0] = __uint_as_float(t.x << 16); z[1] = __uint_as_float(t.x & 0xffff0000u);
+        z[2] = __uint_as_float(t.y << 16); z[3] = __uint_as_float(t.y & 0xffff0000u);
+      } else {
+        const float4 t = *reinterpret_cast<const float4*>((const float*)d.aux + ai);
+        z[0] = t.x; z[1] = t.y; z[2] = t.z; z[3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        z[j] = col + j < d.N ? (aux_bf ? bf2f(((const unsigned short*)d.aux)[ai + j]) : ((const float*)d.aux)[ai + j])
+                             : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      v[j] = acc[j] * d.alpha * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
   }
 }
 

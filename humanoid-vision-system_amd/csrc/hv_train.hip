@@ -341,94 +341,176 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy
 }
 
 // ------------------------------------------------------------------ row norms (train)
-constexpr int RQ = 32;     // up to 2048 columns per row held per lane
+constexpr int RQ = 32;     // columns per row supported: up to 64 * RQ = 2048
 
-// mode 0 LayerNorm, 1 RMSNorm; one wave per row
-template <typename TX, typename TY>
+// Row kernels use a G-lane group per row (G = pow2 >= cols/4, <= 64): each lane owns 4
+// consecutive columns per pass (8-byte bf16 / 16-byte fp32 vector access), NP passes cover the
+// row, 64/G rows share a wave, group reductions are xor-shuffles inside the group.
+template <typename T> __device__ __forceinline__ void st4(T* p, long i, const float (&v)[4]);
+template <> __device__ __forceinline__ void st4<float>(float* p, long i, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void st4<unsigned short>(unsigned short* p, long i, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p + i) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+}
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// mode 0 LayerNorm, 1 RMSNorm
+template <typename TX, typename TY, int G, int NP>
 __global__ void __launch_bounds__(256) k_rownorm_train(int mode, const TX* __restrict__ x, int rows, int cols,
                                                        float eps, const float* g, const float* b, float p,
                                                        uint32_t seed, TY* y, const TY* res, float* mean,
                                                        float* rstd) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const TX* xr = x + (long)row * cols;
-  float s = 0.f;
-  if (mode == 0) {
-    for (int j = lane; j < cols; j += 64) s += ld<TX>(xr, j);
-    s = wave_sum(s);
+  constexpr int RPW = 64 / G;
+  const int lane = threadIdx.x & 63, gl = lane % G;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
+  const bool ok = row < rows;
+  const long base = (ok ? row : 0) * cols;
+  float v[NP][4];
+  float sm = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int col = (q * G + gl) * 4;
+    if (ok && col < cols) ld4<TX>(x, base + col, v[q]);
+    else v[q][0] = v[q][1] = v[q][2] = v[q][3] = 0.f;
+    sm += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
   }
-  const float mu = mode == 0 ? s / cols : 0.f;
-  float v = 0.f;
-  for (int j = lane; j < cols; j += 64) {
-    const float d = ld<TX>(xr, j) - mu;
-    v += d * d;
+  const float mu = mode == 0 ? group_sum<G>(sm) / cols : 0.f;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int col = (q * G + gl) * 4;
+    if (col < cols) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[q][j] - mu; var += d * d; }
+    }
   }
-  v = wave_sum(v);
-  const float rs = 1.0f / sqrtf(v / cols + eps);
-  if (lane == 0) {
+  var = group_sum<G>(var);
+  const float rs = 1.0f / sqrtf(var / cols + eps);
+  if (!ok) return;
+  if (gl == 0) {
     if (mean) mean[row] = mu;
     rstd[row] = rs;
   }
-  for (int j = lane; j < cols; j += 64) {
-    const long o = (long)row * cols + j;
-    float val = (ld<TX>(xr, j) - mu) * rs * (g ? g[j] : 1.f) + (b ? b[j] : 0.f);
-    val *= hv_drop_scale(seed, (unsigned long long)o, p);
-    if (res) val += ld<TY>(res, o);
-    st<TY>(y, o, val);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int col = (q * G + gl) * 4;
+    if (col >= cols) continue;
+    float o[4];
+    float r4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (res) ld4<TY>(res, base + col, r4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float val = (v[q][j] - mu) * rs * (g ? g[col + j] : 1.f) + (b ? b[col + j] : 0.f);
+      o[j] = val * hv_drop_scale(seed, (unsigned long long)(base + col + j), p) + r4[j];
+    }
+    st4<TY>(y, base + col, o);
   }
 }
 
-// backward: one wave per row; per-wave column partials of g*xhat and g (for dgamma/dbeta)
-template <typename TX, typename TD, typename TO>
+template <typename TX, typename TD, typename TO, int G, int NP>
 __global__ void __launch_bounds__(256) k_rownorm_bwd(int mode, const TX* __restrict__ x, const TD* __restrict__ dy,
-                                                     int rows, int cols, int rows_per_wave, const float* mean,
-                                                     const float* rstd, const float* g, float p, uint32_t seed,
-                                                     TO* dx, const TO* dx_add, float* wpart) {
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int nq = (cols + 63) >> 6;
-  float agx[RQ], ag[RQ];
+                                                     int rows, int cols, const float* mean, const float* rstd,
+                                                     const float* g, float p, uint32_t seed, TO* dx,
+                                                     const TO* dx_add) {
+  constexpr int RPW = 64 / G;
+  const int lane = threadIdx.x & 63, gl = lane % G;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
+  const bool ok = row < rows;
+  const long base = (ok ? row : 0) * cols;
+  const float mu = (ok && mode == 0) ? mean[row] : 0.f, rs = ok ? rstd[row] : 1.f;
+  float xh[NP][4], gg[NP][4];
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int q = 0; q < RQ; ++q) { agx[q] = 0.f; ag[q] = 0.f; }
-  const int r0 = wave * rows_per_wave, r1 = min(rows, r0 + rows_per_wave);
-  for (int row = r0; row < r1; ++row) {
-    const long base = (long)row * cols;
-    const float mu = mode == 0 ? mean[row] : 0.f, rs = rstd[row];
-    float xh[RQ], gg[RQ];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int j = lane + 64 * q;
-      xh[q] = 0.f; gg[q] = 0.f;
-      if (q < nq && j < cols) {
-        xh[q] = (ld<TX>(x, base + j) - mu) * rs;
-        const float gr = ld<TD>(dy, base + j) * hv_drop_scale(seed, (unsigned long long)(base + j), p);
-        agx[q] += gr * xh[q];
-        ag[q] += gr;
-        gg[q] = gr * (g ? g[j] : 1.f);
-        s1 += gg[q];
-        s2 += gg[q] * xh[q];
-      }
+  for (int q = 0; q < NP; ++q) {
+    const int col = (q * G + gl) * 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, d[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ok && col < cols) {
+      ld4<TX>(x, base + col, a);
+      ld4<TD>(dy, base + col, d);
     }
-    s1 = wave_sum(s1) / cols;
-    s2 = wave_sum(s2) / cols;
 #pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int j = lane + 64 * q;
-      if (q < nq && j < cols) {
-        float d = mode == 0 ? rs * (gg[q] - s1 - xh[q] * s2) : rs * (gg[q] - xh[q] * s2);
-        if (dx_add) d += ld<TO>(dx_add, base + j);
-        st<TO>(dx, base + j, d);
-      }
+    for (int j = 0; j < 4; ++j) {
+      xh[q][j] = (a[j] - mu) * rs;
+      const bool in = ok && col < cols;
+      const float gr = in ? d[j] * hv_drop_scale(seed, (unsigned long long)(base + col + j), p) : 0.f;
+      gg[q][j] = gr * ((g && in) ? g[col + j] : 1.f);
+      s1 += gg[q][j];
+      s2 += gg[q][j] * xh[q][j];
     }
   }
-  if (wpart) {
-    float* o = wpart + (long)wave * 2 * cols;
+  s1 = group_sum<G>(s1) / cols;
+  s2 = group_sum<G>(s2) / cols;
+  if (!ok) return;
 #pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int j = lane + 64 * q;
-      if (q < nq && j < cols) { o[j] = agx[q]; o[cols + j] = ag[q]; }
-    }
+  for (int q = 0; q < NP; ++q) {
+    const int col = (q * G + gl) * 4;
+    if (col >= cols) continue;
+    float o[4];
+    float ad[4] = {0.f, 0.f, 0.f, 0.f};
+    if (dx_add) ld4<TO>(dx_add, base + col, ad);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = (mode == 0 ? rs * (gg[q][j] - s1 - xh[q][j] * s2) : rs * (gg[q][j] - xh[q][j] * s2)) + ad[j];
+    st4<TO>(dx, base + col, o);
   }
+}
+
+// (G, NP) for a row of `cols` columns
+inline void rown_shape(int cols, int* G, int* NP) {
+  const int q = (cols + 3) / 4;
+  int g = 1;
+  while (g < q && g < 64) g <<= 1;
+  *G = g;
+  *NP = (q + g - 1) / g;
+}
+
+template <typename TX, typename TY>
+int rown_train_launch(int mode, const void* x, int rows, int cols, float eps, const float* gamma, const float* beta,
+                      float p, uint32_t seed, void* y, const void* res, float* mean, float* rstd, hipStream_t s) {
+  int G, NP;
+  rown_shape(cols, &G, &NP);
+  const unsigned grid = hv_cdiv(rows, 4 * (64 / G));
+#define RT(GG, PP) k_rownorm_train<TX, TY, GG, PP><<<grid, 256, 0, s>>>(mode, (const TX*)x, rows, cols, eps, gamma, \
+      beta, p, seed, (TY*)y, (const TY*)res, mean, rstd)
+  if (G == 8) RT(8, 1);
+  else if (G == 16) RT(16, 1);
+  else if (G == 32) RT(32, 1);
+  else if (G == 64 && NP == 1) RT(64, 1);
+  else if (G == 64 && NP == 2) RT(64, 2);
+  else if (G == 64 && NP <= 4) RT(64, 4);
+  else if (G == 64 && NP <= 8) RT(64, 8);
+  else return HV_EUNSUPPORTED;
+#undef RT
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+template <typename TX, typename TD, typename TO>
+int rown_bwd_launch(int mode, const void* x, const void* dy, int rows, int cols, const float* mean, const float* rstd,
+                    const float* gamma, float p, uint32_t seed, void* dx, const void* dx_add, hipStream_t s) {
+  int G, NP;
+  rown_shape(cols, &G, &NP);
+  const unsigned grid = hv_cdiv(rows, 4 * (64 / G));
+#define RBK(GG, PP) k_rownorm_bwd<TX, TD, TO, GG, PP><<<grid, 256, 0, s>>>(mode, (const TX*)x, (const TD*)dy, rows, \
+      cols, mean, rstd, gamma, p, seed, (TO*)dx, (const TO*)dx_add)
+  if (G == 8) RBK(8, 1);
+  else if (G == 16) RBK(16, 1);
+  else if (G == 32) RBK(32, 1);
+  else if (G == 64 && NP == 1) RBK(64, 1);
+  else if (G == 64 && NP == 2) RBK(64, 2);
+  else if (G == 64 && NP <= 4) RBK(64, 4);
+  else if (G == 64 && NP <= 8) RBK(64, 8);
+  else return HV_EUNSUPPORTED;
+#undef RBK
+  HV_CHECK_LAUNCH();
+  return HV_OK;
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -862,26 +944,21 @@ extern "C" int hv_bn_backward(int dtype, const void* x, const void* dy, int rows
 extern "C" int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, int cols, float eps,
                                 const float* gamma, const float* beta, float drop_p, unsigned int seed, int y_dtype,
                                 void* y, const void* residual, float* mean, float* rstd, hv_stream_t stream) {
-  if (!x || !y || !rstd || rows <= 0 || cols <= 0 || cols > 64 * RQ || (mode == 0 && !mean)) return HV_EINVAL;
+  if (!x || !y || !rstd || rows <= 0 || cols <= 0 || cols % 4 || cols > 64 * RQ || (mode == 0 && !mean))
+    return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const unsigned grid = hv_cdiv(rows, 4);
-#define RN_LAUNCH(TX, TY) k_rownorm_train<TX, TY><<<grid, 256, 0, s>>>(mode, (const TX*)x, rows, cols, eps, gamma, \
-      beta, drop_p, seed, (TY*)y, (const TY*)residual, mean, rstd)
-  if (x_dtype == HV_F32 && y_dtype == HV_F32) RN_LAUNCH(float, float);
-  else if (x_dtype == HV_F32 && y_dtype == HV_BF16) RN_LAUNCH(float, unsigned short);
-  else if (x_dtype == HV_BF16 && y_dtype == HV_BF16) RN_LAUNCH(unsigned short, unsigned short);
-  else if (x_dtype == HV_BF16 && y_dtype == HV_F32) RN_LAUNCH(unsigned short, float);
-  else return HV_EINVAL;
-#undef RN_LAUNCH
-  HV_CHECK_LAUNCH();
-  return HV_OK;
-}
-
-static void rownorm_split(int rows, int* rows_per_wave, int* nwaves) {
-  int rpw = (rows + 16383) / 16384;          // <= 16384 waves
-  if (rpw < 1) rpw = 1;
-  *rows_per_wave = rpw;
-  *nwaves = (rows + rpw - 1) / rpw;
+  if (x_dtype == HV_F32 && y_dtype == HV_F32)
+    return rown_train_launch<float, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual, mean, rstd, s);
+  if (x_dtype == HV_F32 && y_dtype == HV_BF16)
+    return rown_train_launch<float, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual,
+                                                    mean, rstd, s);
+  if (x_dtype == HV_BF16 && y_dtype == HV_BF16)
+    return rown_train_launch<unsigned short, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y,
+                                                             residual, mean, rstd, s);
+  if (x_dtype == HV_BF16 && y_dtype == HV_F32)
+    return rown_train_launch<unsigned short, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual,
+                                                    mean, rstd, s);
+  return HV_EINVAL;
 }
 
 extern "C" size_t hv_rownorm_work_floats(int rows, int cols) {
@@ -897,13 +974,11 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
   const bool params = dgamma || dbeta;
   if (params && (!work || !colred_ok(cols))) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  int rpw, nw;
-  rownorm_split(rows, &rpw, &nw);
-  const unsigned grid = hv_cdiv(nw, 4);
-  // (x, dy, dx) dtype combinations used by the mHC / transformer paths
-#define RB_LAUNCH(TX, TD, TO) k_rownorm_bwd<TX, TD, TO><<<grid, 256, 0, s>>>(mode, (const TX*)x, (const TD*)dy, rows, \
-      cols, rpw, mean, rstd, gamma, drop_p, seed, (TO*)dx, (const TO*)dx_add, nullptr)
+  if (cols % 4) return HV_EINVAL;
   const int key = x_dtype * 4 + dy_dtype * 2 + dx_dtype;
+  int rc;
+#define RB_LAUNCH(TX, TD, TO) rc = rown_bwd_launch<TX, TD, TO>(mode, x, dy, rows, cols, mean, rstd, gamma, drop_p, seed, \
+      dx, dx_add, s)
   switch (key) {
     case 0: RB_LAUNCH(float, float, float); break;
     case 1: RB_LAUNCH(float, float, unsigned short); break;
@@ -916,7 +991,7 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
     default: return HV_EINVAL;
   }
 #undef RB_LAUNCH
-  HV_CHECK_LAUNCH();
+  if (rc) return rc;
   if (params) {
     float* sums = work + colred_work(rows, cols, 1, 2);   // [sum g xhat | sum g]
     ColRed r{};
