@@ -62,6 +62,10 @@ class SinkhornBwdEntry(C.Structure):
     _fields_ = [("fwd", SinkhornEntry), ("dout", vp), ("draw", vp), ("bwork", vp)]
 
 
+class NmsScale(C.Structure):
+    _fields_ = [("boxes", vp), ("class_scores", vp), ("class_indices", vp), ("cells", i64)]
+
+
 class ParamEntry(C.Structure):
     _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp),
                 ("n", i64), ("group", i32), ("blk", i32)]
@@ -125,6 +129,8 @@ _SIGS = {
     "hv_attention_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),
+    "hv_nms": ([vp, i32, i32, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
     # ---- training step
     "hv_wgrad_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_wgrad": ([vp, vp], i32),

@@ -207,38 +207,22 @@ class YOLODetectionHead(nn.Module):
             out["loss"] = self.loss_fn(preds, targets)
         return out
 
-    # ---- post-processing (yolo_head.py:571-731): host-side greedy NMS, "next" row §8f-1
+    # ---- post-processing (yolo_head.py:571-731) on the GPU: hv_nms, two launches per batch
     def post_process(self, decoded_outputs, confidence_threshold: float = 0.5, iou_threshold: float = 0.5,
                      max_detections: int = 100):
-        per_scale = []
-        B = None
-        for _, out in decoded_outputs.items():
-            boxes, scores, cls = out["boxes"], out["class_scores"], out["class_indices"]
-            B = scores.shape[0]
-            bf, sf, cf = boxes.reshape(B, -1, 4), scores.reshape(B, -1), cls.reshape(B, -1)
-            dets = []
-            for b in range(B):
-                m = sf[b] > confidence_threshold
-                if not m.any():
-                    dets.append({"boxes": torch.tensor([], device=boxes.device),
-                                 "scores": torch.tensor([], device=boxes.device),
-                                 "labels": torch.tensor([], device=boxes.device, dtype=torch.long)})
-                    continue
-                bb, ss, cc = bf[b][m], sf[b][m], cf[b][m]
-                keep = self.non_max_suppression(bb, ss, iou_threshold, max_detections)
-                dets.append({"boxes": bb[keep], "scores": ss[keep], "labels": cc[keep]})
-            per_scale.append(dets)
-        combined = []
-        for b in range(B or 0):
-            ab = torch.cat([d[b]["boxes"] for d in per_scale], 0)
-            asc = torch.cat([d[b]["scores"] for d in per_scale], 0)
-            al = torch.cat([d[b]["labels"] for d in per_scale], 0)
-            if len(ab) > 0:
-                keep = self.non_max_suppression(ab, asc, iou_threshold, max_detections)
-                combined.append({"boxes": ab[keep], "scores": asc[keep], "labels": al[keep]})
+        """Per scale: class_score > threshold, greedy NMS; then NMS across scales.
+        One host synchronisation for the whole batch (to cut the per-image lists)."""
+        boxes, scores, labels, count = ops.nms_batched(decoded_outputs, confidence_threshold, iou_threshold,
+                                                       max_detections)
+        out = []
+        for b, n in enumerate(count.tolist()):
+            if n == 0:
+                dev = boxes.device
+                out.append({"boxes": torch.tensor([], device=dev), "scores": torch.tensor([], device=dev),
+                            "labels": torch.tensor([], device=dev, dtype=torch.long)})
             else:
-                combined.append({"boxes": ab, "scores": asc, "labels": al})
-        return combined
+                out.append({"boxes": boxes[b, :n], "scores": scores[b, :n], "labels": labels[b, :n]})
+        return out
 
     def non_max_suppression(self, boxes, scores, iou_threshold: float = 0.5, max_detections: int = 100):
         if boxes.numel() == 0:

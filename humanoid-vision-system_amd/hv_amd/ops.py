@@ -496,6 +496,43 @@ def yolo_decode(logits: Tensor, A: int, nc: int, anchor_wh: Tensor):
             "objectness": obj, "raw_predictions": pred}, pred
 
 
+# ---------------------------------------------------------------------------- post-processing
+def nms_batched(decoded, conf_thr: float, iou_thr: float, max_det: int):
+    """GPU post_process (hv_nms): per-scale threshold + greedy NMS, then cross-scale NMS.
+    decoded: {scale_key: {'boxes' [B,A,H,W,4], 'class_scores' [B,A,H,W], 'class_indices'}}.
+    Returns device tensors boxes [B, max_det, 4], scores [B, max_det], labels [B, max_det],
+    count [B] (int32)."""
+    keys = sorted(decoded)
+    ents = (L.NmsScale * len(keys))()
+    keep = []
+    B = None
+    dev = None
+    for i, k in enumerate(keys):
+        o = decoded[k]
+        bx = o["boxes"].detach().float().contiguous()
+        sc = o["class_scores"].detach().float().contiguous()
+        ci = o["class_indices"].detach().to(torch.int64).contiguous()
+        _cuda(bx, sc, ci)
+        B = sc.shape[0]
+        dev = sc.device
+        cells = sc.numel() // B
+        if bx.numel() != B * cells * 4 or ci.numel() != B * cells:
+            raise ValueError("nms_batched: boxes / scores / indices shapes disagree")
+        ents[i].boxes, ents[i].class_scores, ents[i].class_indices, ents[i].cells = \
+            bx.data_ptr(), sc.data_ptr(), ci.data_ptr(), cells
+        keep += [bx, sc, ci]
+    table = torch.frombuffer(bytearray(bytes(ents)), dtype=torch.uint8).to(dev)
+    boxes = torch.empty((B, max_det, 4), device=dev, dtype=torch.float32)
+    scores = torch.empty((B, max_det), device=dev, dtype=torch.float32)
+    labels = torch.empty((B, max_det), device=dev, dtype=torch.int64)
+    count = torch.empty(B, device=dev, dtype=torch.int32)
+    work = torch.empty(L.lib().hv_nms_work_bytes(B, len(keys), max_det), device=dev, dtype=torch.uint8)
+    check(L.lib().hv_nms(table.data_ptr(), len(keys), B, float(conf_thr), float(iou_thr), int(max_det),
+                         boxes.data_ptr(), scores.data_ptr(), labels.data_ptr(), count.data_ptr(), work.data_ptr(),
+                         stream_ptr()), "hv_nms")
+    return boxes, scores, labels, count
+
+
 # ---------------------------------------------------------------------------- debug tracing
 def _install_sync_check():
     """HV_SYNC_CHECK=1: synchronise after every op and report the first one that faults."""

@@ -307,6 +307,25 @@ int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, in
                    float* objectness, hv_stream_t stream);
 
 
+
+/* ------------------------------------------------------------------------------------
+ * Detection post-processing: YOLODetectionHead.post_process +
+ * non_max_suppression (yolo_head.py:571-731) for a whole batch in two launches.
+ * Per (image, scale): class_score > conf_thr, greedy NMS (keep IoU < iou_thr, best first,
+ * at most max_det, up to 8192 candidates per image and scale); then per image the same NMS
+ * over the concatenated per-scale survivors.  Outputs [batch, max_det] (+ count[batch]).
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_nms_scale {
+  const float* boxes;          /* [batch, cells, 4] xyxy (decoder output [B, A, H, W, 4]) */
+  const float* class_scores;   /* [batch, cells] */
+  const int64_t* class_indices;/* [batch, cells] */
+  long cells;                  /* A * H * W */
+} hv_nms_scale;
+size_t hv_nms_work_bytes(int batch, int nscales, int max_det);
+int hv_nms(const hv_nms_scale* dev_scales, int nscales, int batch, float conf_thr, float iou_thr,
+           int max_det, float* boxes, float* scores, int64_t* labels, int* count, void* work,
+           hv_stream_t stream);
+
 /* ====================================================================================
  * Training step: backward kernels, BatchNorm batch statistics,
  * dropout, YOLOLoss, clipping and AdamW.  Same conventions as above (caller-owned

@@ -49,3 +49,22 @@ def mhc_cotangent(D: int, e: int) -> torch.Tensor:
 
 def model_input(B: int, S: int) -> torch.Tensor:
     return torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+
+
+def nms_case(seed: int, B: int = 2, grids=((8, 8), (4, 4), (2, 2)), A: int = 3, frac_above: float = 0.3):
+    """Random decoded outputs for the post-processing fixture: clustered xyxy boxes (so NMS
+    suppresses), class scores u^(1/(1-frac_above)) for u ~ U(0,1) (larger frac_above -> fewer
+    scores above 0.5), random labels."""
+    g = gen_seed(seed, B, 77)
+    out = {}
+    for s, (h, w) in enumerate(grids):
+        n = A * h * w
+        ctr = torch.rand(B, 4, 2, generator=g)                      # 4 clusters per image
+        pick = torch.randint(0, 4, (B, n), generator=g)
+        c = torch.gather(ctr, 1, pick.unsqueeze(-1).expand(B, n, 2)) + 0.03 * torch.randn(B, n, 2, generator=g)
+        wh = 0.05 + 0.2 * torch.rand(B, n, 2, generator=g)
+        boxes = torch.cat([c - wh / 2, c + wh / 2], -1).view(B, A, h, w, 4)
+        sc = torch.rand(B, A, h, w, generator=g) ** (1.0 / max(1e-3, 1 - frac_above))
+        lab = torch.randint(0, 80, (B, A, h, w), generator=g)
+        out[f"scale_{s}"] = {"boxes": boxes.float(), "class_scores": sc.float(), "class_indices": lab}
+    return out

@@ -340,9 +340,27 @@ def gen_train(hv):
     model.float()
 
 
+# ------------------------------------------------------------------ G6 post-processing
+def gen_nms(yh):
+    """YOLODetectionHead.post_process (yolo_head.py:571-731) on random decoded outputs."""
+    print("G6 nms")
+    from oracle.cases import nms_case
+    torch.manual_seed(0)
+    head = yh.YOLODetectionHead([16, 16, 16], num_classes=80)
+    for seed, conf, iou, mx in ((1, 0.5, 0.5, 100), (2, 0.3, 0.4, 100), (3, 0.5, 0.5, 7), (4, 0.99, 0.5, 100)):
+        dec = nms_case(seed)
+        res = head.post_process(dec, confidence_threshold=conf, iou_threshold=iou, max_detections=mx)
+        rec = {"conf": conf, "iou": iou, "max_det": mx}
+        for b, r in enumerate(res):
+            rec[f"boxes{b}"] = r["boxes"].reshape(-1, 4)
+            rec[f"scores{b}"] = r["scores"].reshape(-1)
+            rec[f"labels{b}"] = r["labels"].reshape(-1)
+        save(f"nms_{seed}", **rec)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train")
+    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train,nms")
     ap.add_argument("--models", default="")
     a = ap.parse_args()
     torch.set_num_threads(8)
@@ -360,6 +378,8 @@ def main():
         gen_layout(hv)
     if "train" in parts:
         gen_train(hv)
+    if "nms" in parts:
+        gen_nms(yh)
 
 
 

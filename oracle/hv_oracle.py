@@ -387,3 +387,61 @@ def system_forward(sd: Dict[str, Tensor], x: Tensor, cfg: OracleConfig = BASE) -
 
 def cast_state_dict(sd: Dict[str, Tensor], dtype=torch.float32) -> Dict[str, Tensor]:
     return {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in sd.items()}
+
+
+# ----------------------------------------------------------------------------------------
+# §8f-1: detection post-processing (yolo_head.py:571-731)
+# ----------------------------------------------------------------------------------------
+def _iou(b1: Tensor, b2: Tensor) -> Tensor:
+    """compute_iou (yolo_head.py:733-756)."""
+    ix1 = torch.max(b1[..., 0], b2[..., 0])
+    iy1 = torch.max(b1[..., 1], b2[..., 1])
+    ix2 = torch.min(b1[..., 2], b2[..., 2])
+    iy2 = torch.min(b1[..., 3], b2[..., 3])
+    inter = (ix2 - ix1).clamp(min=0) * (iy2 - iy1).clamp(min=0)
+    a1 = (b1[..., 2] - b1[..., 0]) * (b1[..., 3] - b1[..., 1])
+    a2 = (b2[..., 2] - b2[..., 0]) * (b2[..., 3] - b2[..., 1])
+    return inter / (a1 + a2 - inter + 1e-6)
+
+
+def nms(boxes: Tensor, scores: Tensor, iou_thr: float, max_det: int) -> List[int]:
+    """non_max_suppression (yolo_head.py:678-731): greedy, best first, keep IoU < thr."""
+    order = torch.sort(scores, descending=True, stable=True).indices
+    keep: List[int] = []
+    while order.numel() > 0:
+        i = int(order[0])
+        keep.append(i)
+        if len(keep) >= max_det:
+            break
+        rest = order[1:]
+        if rest.numel() == 0:
+            break
+        order = rest[_iou(boxes[i].unsqueeze(0), boxes[rest]) < iou_thr]
+    return keep
+
+
+def post_process(decoded: Dict, conf_thr: float = 0.5, iou_thr: float = 0.5, max_det: int = 100):
+    """YOLODetectionHead.post_process (yolo_head.py:571-676): per scale threshold + NMS,
+    then NMS over the concatenation of the per-scale survivors."""
+    per_scale = []
+    B = None
+    for key in sorted(decoded):
+        out = decoded[key]
+        scores = out["class_scores"]
+        B = scores.shape[0]
+        bf, sf, cf = out["boxes"].reshape(B, -1, 4), scores.reshape(B, -1), out["class_indices"].reshape(B, -1)
+        dets = []
+        for b in range(B):
+            m = sf[b] > conf_thr
+            bb, ss, cc = bf[b][m], sf[b][m], cf[b][m]
+            k = nms(bb, ss, iou_thr, max_det) if bb.numel() else []
+            dets.append((bb[k], ss[k], cc[k]))
+        per_scale.append(dets)
+    res = []
+    for b in range(B):
+        ab = torch.cat([d[b][0].reshape(-1, 4) for d in per_scale])
+        asc = torch.cat([d[b][1] for d in per_scale])
+        al = torch.cat([d[b][2] for d in per_scale])
+        k = nms(ab, asc, iou_thr, max_det) if ab.numel() else []
+        res.append({"boxes": ab[k], "scores": asc[k], "labels": al[k]})
+    return res

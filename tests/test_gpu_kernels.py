@@ -272,3 +272,32 @@ def test_decode_matches_reference_fixture(gpu_device):
     np.testing.assert_allclose(dec["boxes"].cpu().numpy(), g["boxes"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(dec["scores"].cpu().numpy(), g["scores"], rtol=1e-5, atol=1e-7)
     np.testing.assert_array_equal(dec["class_indices"].cpu().numpy(), g["class_indices"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_gpu_post_process_matches_reference_fixture(gpu_device, seed):
+    """§8f-1: hv_nms (two launches per batch) vs the reference's post_process (tests/golden/nms_*)."""
+    from hv_amd.detect import YOLODetectionHead
+    g = golden(f"nms_{seed}")
+    dec = {k: {n: t.to(gpu_device) for n, t in v.items()} for k, v in cases.nms_case(seed).items()}
+    head = YOLODetectionHead([16, 16, 16], num_classes=80)
+    res = head.post_process(dec, float(g["conf"]), float(g["iou"]), int(g["max_det"]))
+    for b, r in enumerate(res):
+        np.testing.assert_array_equal(r["labels"].cpu().numpy(), g[f"labels{b}"])
+        np.testing.assert_array_equal(r["scores"].cpu().numpy(), g[f"scores{b}"])
+        np.testing.assert_array_equal(r["boxes"].reshape(-1, 4).cpu().numpy(), g[f"boxes{b}"])
+
+
+def test_gpu_nms_large_matches_oracle(gpu_device):
+    """640x640-sized grids (19200 + 4800 + 1200 cells, many candidates) vs the oracle."""
+    from oracle import hv_oracle as O
+    from hv_amd import ops
+    dec = cases.nms_case(9, B=2, grids=((80, 80), (40, 40), (20, 20)), frac_above=0.9)  # ~7% above 0.5
+    ref = O.post_process(dec, 0.5, 0.5, 100)
+    dd = {k: {n: t.to(gpu_device) for n, t in v.items()} for k, v in dec.items()}
+    boxes, scores, labels, count = ops.nms_batched(dd, 0.5, 0.5, 100)
+    for b in range(2):
+        n = int(count[b])
+        assert n == len(ref[b]["scores"])
+        np.testing.assert_array_equal(scores[b, :n].cpu().numpy(), ref[b]["scores"].numpy())
+        np.testing.assert_array_equal(labels[b, :n].cpu().numpy(), ref[b]["labels"].numpy())

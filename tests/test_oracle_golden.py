@@ -193,3 +193,14 @@ def test_train_step_oracle_matches_reference():
         if key.startswith("g:") and key.endswith("_f64"):
             n = key[2:-4]
             np.testing.assert_allclose(sd[n].grad.numpy(), g[key], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_post_process_oracle_matches_reference(seed):
+    """§8f-1: the oracle's post_process/NMS vs the reference's (tests/golden/nms_*)."""
+    g = golden(f"nms_{seed}")
+    res = O.post_process(cases.nms_case(seed), float(g["conf"]), float(g["iou"]), int(g["max_det"]))
+    for b, r in enumerate(res):
+        np.testing.assert_array_equal(r["labels"].numpy(), g[f"labels{b}"])
+        np.testing.assert_allclose(r["scores"].numpy(), g[f"scores{b}"], rtol=0, atol=0)
+        np.testing.assert_allclose(r["boxes"].reshape(-1, 4).numpy(), g[f"boxes{b}"], rtol=0, atol=0)
