@@ -130,6 +130,7 @@ _SIGS = {
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),
+    "hv_preprocess": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp], i32),
     "hv_nms": ([vp, i32, i32, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
     # ---- training step
     "hv_wgrad_work_floats": ([i32, i32, i32, i32], C.c_size_t),

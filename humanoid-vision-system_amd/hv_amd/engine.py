@@ -25,7 +25,9 @@ from typing import Any, Callable, Dict, List, Optional, Union
 
 import numpy as np
 import torch
-import torch.nn.functional as F
+import torch.nn.functional as F  # noqa: F401
+
+from . import ops
 
 logger = logging.getLogger(__name__)
 
@@ -59,16 +61,19 @@ class InferenceConfig:
     collect_stability: bool = False
 
 
-def preprocess_image(img: np.ndarray, height: int, width: int, device) -> torch.Tensor:
-    """uint8 HWC BGR -> normalised fp32 CHW (preprocessing.py:181-232 semantics: BGR->RGB,
-    bilinear resize, /255, ImageNet mean/std).  Resize runs on the device."""
-    t = torch.from_numpy(np.ascontiguousarray(img[..., ::-1])).to(device)
-    t = t.permute(2, 0, 1).unsqueeze(0).float() / 255.0
-    if t.shape[-2:] != (height, width):
-        t = F.interpolate(t, size=(height, width), mode="bilinear", align_corners=False)
-    mean = torch.tensor(IMAGENET_MEAN, device=device).view(1, 3, 1, 1)
-    std = torch.tensor(IMAGENET_STD, device=device).view(1, 3, 1, 1)
-    return ((t - mean) / std)[0]
+def preprocess_image(img: np.ndarray, height: int, width: int, device, dtype=torch.float32) -> torch.Tensor:
+    """uint8 HWC BGR frame -> normalised CHW (preprocessing.py:181-232 semantics: BGR->RGB,
+    bilinear resize, /255, ImageNet mean/std) in one HIP launch (hv_preprocess)."""
+    return preprocess_frames([img], height, width, device, dtype)[0]
+
+
+def preprocess_frames(imgs: List[np.ndarray], height: int, width: int, device, dtype=torch.float32) -> torch.Tensor:
+    """Batch of same-size uint8 HWC BGR frames -> [n, 3, height, width]: one host->device copy
+    of the raw bytes, one preprocessing launch."""
+    if imgs[0].dtype != np.uint8 or imgs[0].ndim != 3 or imgs[0].shape[2] != 3:
+        raise ValueError("expected uint8 HWC 3-channel frames")
+    raw = torch.from_numpy(np.ascontiguousarray(np.stack(imgs))).to(device, non_blocking=True)
+    return ops.preprocess(raw, height, width, bgr=True, dtype=dtype)
 
 
 class InferenceEngine:
@@ -132,6 +137,8 @@ class InferenceEngine:
         return image.to(self.device)
 
     def preprocess_batch(self, images: List[np.ndarray]) -> torch.Tensor:
+        if all(isinstance(i, np.ndarray) for i in images) and len({i.shape for i in images}) == 1:
+            return preprocess_frames(images, self.config.input_height, self.config.input_width, self.device)
         return torch.stack([self._to_tensor(i) for i in images])
 
     # ------------------------------------------------------------------ inference

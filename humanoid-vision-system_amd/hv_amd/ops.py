@@ -533,6 +533,27 @@ def nms_batched(decoded, conf_thr: float, iou_thr: float, max_det: int):
     return boxes, scores, labels, count
 
 
+# ---------------------------------------------------------------------------- preprocessing
+IMAGENET_MEAN_STD = (0.485, 0.456, 0.406, 0.229, 0.224, 0.225)
+
+
+def preprocess(frames: Tensor, height: int, width: int, *, bgr: bool = True, dtype: torch.dtype = torch.float32,
+               nhwc: bool = False, mean_std=IMAGENET_MEAN_STD) -> Tensor:
+    """uint8 [n, h, w, 3] device frames -> normalised [n, 3, height, width] (NCHW tensor, or the
+    NCHW-shaped view of NHWC storage when nhwc=True -- zero-copy for the model's input)."""
+    _cuda(frames)
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise ValueError("preprocess expects uint8 [n, h, w, 3] frames")
+    frames = frames.contiguous()
+    n, h, w, _ = frames.shape
+    code = {torch.float32: L.HV_F32, torch.bfloat16: L.HV_BF16, torch.float16: 2}[dtype]
+    out = torch.empty((n, height, width, 3) if nhwc else (n, 3, height, width), device=frames.device, dtype=dtype)
+    ms = (C.c_float * 6)(*mean_std)
+    check(L.lib().hv_preprocess(frames.data_ptr(), n, h, w, int(bgr), height, width, ms, code, int(nhwc),
+                                out.data_ptr(), stream_ptr()), "hv_preprocess")
+    return out.permute(0, 3, 1, 2) if nhwc else out
+
+
 # ---------------------------------------------------------------------------- debug tracing
 def _install_sync_check():
     """HV_SYNC_CHECK=1: synchronise after every op and report the first one that faults."""

@@ -27,7 +27,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hv_stream_t; /* == hipStream_t */
 
-enum { HV_F32 = 0, HV_BF16 = 1 };
+enum { HV_F32 = 0, HV_BF16 = 1, HV_F16 = 2 /* preprocess output only */ };
 enum { HV_ACT_NONE = 0, HV_ACT_RELU = 1, HV_ACT_SILU = 2, HV_ACT_GELU = 3,
        HV_ACT_LEAKY = 4 /* slope 0.1 */, HV_ACT_SIGMOID = 5 };
 enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
@@ -325,6 +325,17 @@ size_t hv_nms_work_bytes(int batch, int nscales, int max_det);
 int hv_nms(const hv_nms_scale* dev_scales, int nscales, int batch, float conf_thr, float iou_thr,
            int max_det, float* boxes, float* scores, int64_t* labels, int* count, void* work,
            hv_stream_t stream);
+
+
+/* ------------------------------------------------------------------------------------
+ * Image preprocessing (ImagePreprocessor.process, inference/preprocessing.py:
+ * 181-276): uint8 HWC frames [n, h, w, 3] (BGR when swap_rb) -> bilinear resize
+ * (F.interpolate align_corners=False) -> /255 -> (v - mean) / std, written as NHWC
+ * (nhwc = 1, the model's token layout) or NCHW, in fp32 / bf16 / fp16.  One launch per batch.
+ * ------------------------------------------------------------------------------------ */
+int hv_preprocess(const uint8_t* img, int n, int h, int w, int swap_rb, int out_h, int out_w,
+                  const float* mean_std /* host [6] */, int out_dtype, int nhwc, void* out,
+                  hv_stream_t stream);
 
 /* ====================================================================================
  * Training step: backward kernels, BatchNorm batch statistics,

@@ -301,3 +301,21 @@ def test_gpu_nms_large_matches_oracle(gpu_device):
         assert n == len(ref[b]["scores"])
         np.testing.assert_array_equal(scores[b, :n].cpu().numpy(), ref[b]["scores"].numpy())
         np.testing.assert_array_equal(labels[b, :n].cpu().numpy(), ref[b]["labels"].numpy())
+
+
+@pytest.mark.parametrize("h,w,oh,ow", [(480, 640, 640, 640), (720, 1280, 640, 640), (64, 64, 64, 64), (300, 200, 416, 416)])
+def test_gpu_preprocess_matches_torch(gpu_device, h, w, oh, ow):
+    """§8f-2: uint8 BGR frames -> resize (bilinear, align_corners=False) -> /255 -> ImageNet norm."""
+    from hv_amd import ops
+    g = torch.Generator().manual_seed(h * w)
+    frames = torch.randint(0, 256, (2, h, w, 3), generator=g, dtype=torch.uint8)
+    t = frames.flip(-1).permute(0, 3, 1, 2).float() / 255.0
+    t = F.interpolate(t, size=(oh, ow), mode="bilinear", align_corners=False)
+    ref = (t - torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) / torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    out = ops.preprocess(frames.to(gpu_device), oh, ow)
+    assert (out.cpu() - ref).abs().max().item() < 2e-5
+    nh = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.bfloat16, nhwc=True)
+    assert nh.permute(0, 2, 3, 1).is_contiguous()
+    assert (nh.float().cpu() - ref).abs().max().item() < 2e-2
+    h16 = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.float16)
+    assert (h16.float().cpu() - ref).abs().max().item() < 5e-3
