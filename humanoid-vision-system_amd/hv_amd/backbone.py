@@ -68,6 +68,9 @@ class ConvMHCLayer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "ConvMHCLayer")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            return to_nchw_view(TM.conv_mhc_layer(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self)))
         with ctx_scope(self) as ctx:
             return to_nchw_view(self.forward_nhwc(to_nhwc(x, ctx.dtype)))
 
@@ -99,6 +102,9 @@ class ResidualMHCLayer(nn.Module):
 
     def forward(self, x):
         require_cuda(x, "ResidualMHCLayer")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            return to_nchw_view(TM.residual_layer(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self)))
         with ctx_scope(self) as ctx:
             return to_nchw_view(self.forward_nhwc(to_nhwc(x, ctx.dtype)))
 
@@ -164,9 +170,11 @@ class HybridVisionBackbone(nn.Module):
     def forward(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
         require_cuda(x, "HybridVisionBackbone")
         if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("hv_amd: backbone training backward is not implemented yet")
-        with ctx_scope(self) as ctx:
-            out = self.forward_nhwc(to_nhwc(x, ctx.dtype))
+            from . import train_model as TM
+            out = TM.backbone(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self))
+        else:
+            with ctx_scope(self) as ctx:
+                out = self.forward_nhwc(to_nhwc(x, ctx.dtype))
         res = {k: to_nchw_view(v) for k, v in out.items() if k != "raw_features"}
         res["raw_features"] = {k: to_nchw_view(v) for k, v in out["raw_features"].items()}
         return res

@@ -71,6 +71,12 @@ class FeaturePyramidNetwork(nn.Module):
         return out
 
     def forward(self, features: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            dt = resolve_dtype(self.mhc_fusions[0])
+            nh = {k: TM.nhwc_in(v, dt) for k, v in features.items() if k.startswith("scale_")}
+            return {k: to_nchw_view(v) for k, v in TM.fpn(self, nh, TM.module_H(self)).items()}
         with ctx_scope(self) as ctx:
             nh = {k: to_nhwc(v, ctx.dtype) for k, v in features.items() if k.startswith("scale_")}
             return {k: to_nchw_view(v) for k, v in self.forward_nhwc(nh).items()}
@@ -135,6 +141,12 @@ class YOLOPredictionHead(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "YOLOPredictionHead")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            lg = TM.head_logits(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self))
+            n, h, w, _ = lg.shape
+            return TM._PredViewFn.apply(lg, self.num_anchors)
         with ctx_scope(self) as ctx:
             lg = self.logits_nhwc(to_nhwc(x, ctx.dtype))
             n, h, w, _ = lg.shape
@@ -168,7 +180,10 @@ class YOLOLoss(nn.Module):
         self.num_scales = len(self.anchors)
 
     def forward(self, predictions, targets):
-        raise NotImplementedError("hv_amd: YOLO training loss is a later-round row (SURVEY §8a T / §8f-3)")
+        """yolo_head.py:374-465 via the fused loss kernel (hv_yolo_loss): component sums are
+        device tensors (no .item() per scale), total_loss is differentiable."""
+        from .train_model import yolo_loss_api
+        return yolo_loss_api(self, predictions, targets)
 
 
 class YOLODetectionHead(nn.Module):
@@ -199,6 +214,18 @@ class YOLODetectionHead(nn.Module):
         return preds, decoded
 
     def forward(self, features: Dict[str, torch.Tensor], targets=None, compute_loss: bool = False):
+        if self.training and torch.is_grad_enabled():
+            preds, decoded = {}, {}
+            for s, key in enumerate(("scale_small", "scale_medium", "scale_large")):
+                if key not in features:
+                    continue
+                p = self.pred_heads[s](features[key])
+                preds[f"scale_{s}"] = p
+                decoded[f"scale_{s}"] = self.decoder(p.detach(), self.anchor_generator(s), None)
+            out = {"predictions": preds, "decoded": decoded}
+            if compute_loss and targets is not None:
+                out["loss"] = self.loss_fn(preds, targets)
+            return out
         with ctx_scope(self) as ctx:
             nh = {k: to_nhwc(v, ctx.dtype) for k, v in features.items()}
             preds, decoded = self.forward_nhwc(nh)

@@ -233,6 +233,35 @@ class ManifoldHyperConnection(nn.Module):
         y = self.forward_tokens(x2)
         return y.view(shape).to(in_dtype if in_dtype in (torch.float32, torch.bfloat16) else dt)
 
+    monitor_every = 1      # training-mode stability monitor period (reference: every forward)
+
+    @torch.no_grad()
+    def monitor_stability(self, H_res: torch.Tensor, x_in: torch.Tensor, x_out: torch.Tensor) -> None:
+        """_monitor_stability (manifold_layers.py:282-316), device-side: eigenvalues of the
+        symmetric part of H_res, the signal-growth ratio into the circular history, row/column
+        sum errors -- kept as device tensors (no .item() in the training forward; the host reads
+        happen in get_stability_metrics)."""
+        h = H_res.detach().float()
+        try:
+            self.eigenvalues.copy_(torch.linalg.eigvalsh((h + h.T) / 2))
+        except RuntimeError:
+            pass
+        ratio = x_out.detach().float().norm(dim=-1).mean() / (x_in.detach().float().norm(dim=-1).mean() + 1e-8)
+        self.signal_ratio_history[self.signal_ratio_idx % 1000] = ratio
+        self.signal_ratio_idx += 1
+        self._monitor_dev = {"signal_ratio": ratio, "row_sum_error": (h.sum(dim=1).mean() - 1.0).abs(),
+                             "col_sum_error": (h.sum(dim=0).mean() - 1.0).abs()}
+
+    @property
+    def monitoring_metrics(self) -> Dict[str, float]:
+        d = getattr(self, "_monitor_dev", None)
+        if d is None:
+            raise AttributeError("monitoring_metrics")
+        ev = self.eigenvalues
+        out = {"max_eigenvalue": ev.max().item(), "min_eigenvalue": ev.min().item()}
+        out.update({k: float(v) for k, v in d.items()})
+        return out
+
     def get_stability_metrics(self) -> Dict[str, Any]:
         """manifold_layers.py:318-341 (host reads happen here, never in forward)."""
         ev = self.eigenvalues
@@ -243,7 +272,7 @@ class ManifoldHyperConnection(nn.Module):
             h = self.signal_ratio_history[: min(self.signal_ratio_idx, 1000)]
             metrics.update({"signal_ratio_mean": h.mean().item(), "signal_ratio_std": h.std().item(),
                             "signal_ratio_min": h.min().item(), "signal_ratio_max": h.max().item()})
-        if hasattr(self, "monitoring_metrics"):
+        if getattr(self, "_monitor_dev", None) is not None:
             metrics.update(self.monitoring_metrics)
         return metrics
 
@@ -284,6 +313,12 @@ class MultiHeadManifoldAttention(nn.Module):
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
         require_cuda(query, "MultiHeadManifoldAttention")
+        if self.training and torch.is_grad_enabled() and key is query and value is query \
+                and key_padding_mask is None and not need_weights:
+            from . import train_model as TM
+            n, L, D = query.shape
+            x = query.reshape(n * L, D).to(resolve_dtype(self.q_proj)).contiguous()
+            return TM.attention(self, x, n, TM.module_H(self)).view(n, L, D).to(query.dtype), None
         if key is not query or value is not query or key_padding_mask is not None or need_weights:
             raise NotImplementedError("hv_amd attention implements the self-attention call of "
                                       "TransformerEncoderBlock (vit_encoder_decoder.py:191)")
@@ -303,4 +338,8 @@ class RMSNorm(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "RMSNorm")
+        if torch.is_grad_enabled() and (x.requires_grad or self.scale.requires_grad):
+            from .train_fn import RMSNormFn
+            shp = x.shape
+            return RMSNormFn.apply(x.reshape(-1, shp[-1]), self.scale, self.eps).view(shp)
         return ops.rmsnorm(x.contiguous(), ops.f32(self.scale), self.eps)

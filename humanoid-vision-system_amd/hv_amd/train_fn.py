@@ -244,9 +244,16 @@ class MhcFn(torch.autograd.Function):
 
 def mhc(m, x: Tensor, H_res: Tensor) -> Tensor:
     seeds = tuple(next_seed() if pp > 0 else 0 for pp in (m.mlp[2].p, m.mlp[5].p, m.dropout.p))
-    return MhcFn.apply(x, H_res, m.H_pre_raw, m.H_post_raw, m.norm_pre.weight, m.norm_pre.bias,
-                       m.mlp[0].weight, m.mlp[0].bias, m.mlp[3].weight, m.mlp[3].bias,
-                       m.norm_post.weight, m.norm_post.bias, m, seeds)
+    y = MhcFn.apply(x, H_res, m.H_pre_raw, m.H_post_raw, m.norm_pre.weight, m.norm_pre.bias,
+                    m.mlp[0].weight, m.mlp[0].bias, m.mlp[3].weight, m.mlp[3].bias,
+                    m.norm_post.weight, m.norm_post.bias, m, seeds)
+    if m.training:                                   # a4: manifold_layers.py:275-276 (throttled)
+        cnt = getattr(m, "_mon_count", 0)
+        m._mon_count = cnt + 1
+        every = getattr(m, "monitor_every", 1)
+        if every > 0 and cnt % every == 0:
+            m.monitor_stability(H_res, x, y)
+    return y
 
 
 # =============================================================================== SE gate

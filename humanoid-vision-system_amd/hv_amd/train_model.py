@@ -32,6 +32,26 @@ def _hres_table(model) -> Dict[int, torch.Tensor]:
     return {id(m): h for m, h in zip(mods, outs)}
 
 
+def module_H(module) -> Dict[int, torch.Tensor]:
+    """Grouped differentiable Sinkhorn projections of every mHC inside `module` (module-level
+    training calls; the system forward builds one table for all 76 sites)."""
+    from .manifold import ManifoldHyperConnection
+    mods = [m for m in module.modules() if isinstance(m, ManifoldHyperConnection)]
+    if not mods:
+        return {}
+    raws = [m.H_res_raw for m in mods]
+    group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
+                              raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
+                              hists=[m.sinkhorn.convergence_history for m in mods])
+    outs = TF.SinkhornGroupFn.apply(group, *raws)
+    return {id(m): h for m, h in zip(mods, outs)}
+
+
+def nhwc_in(x: torch.Tensor, dtype) -> torch.Tensor:
+    """Differentiable NCHW -> contiguous NHWC in the compute dtype (module-entry glue)."""
+    return x.permute(0, 2, 3, 1).contiguous().to(dtype)
+
+
 def _tok(m, x: torch.Tensor, H) -> torch.Tensor:
     n, h, w, c = x.shape
     return TF.mhc(m, x.reshape(-1, c), H[id(m)]).view(n, h, w, c)
@@ -331,3 +351,16 @@ def final_features(model, fused, H):
                               None)
         return TF.LinearFn.apply(h, model.output_projection[4].weight, model.output_projection[4].bias, "none", 0.0,
                                  0, torch.float32)
+
+
+def yolo_loss_api(loss_fn, predictions: Dict[str, torch.Tensor], targets) -> Dict[str, Any]:
+    """YOLOLoss.forward on reference-layout predictions [B, A, H, W, 5+C] (training API)."""
+    logits = {}
+    A = None
+    for s in range(loss_fn.num_scales):
+        p = predictions.get(f"scale_{s}")
+        if p is None:
+            continue
+        B, A, h, w, P = p.shape
+        logits[s] = p.permute(0, 2, 3, 1, 4).reshape(B, h, w, A * P).contiguous()
+    return yolo_loss(loss_fn, logits, targets, A)

@@ -175,6 +175,30 @@ class FusedAdamW:
         check(lib.hv_adamw(self._table.data_ptr(), len(self.named), self._blocks, coefs, self.lr, b1, b2, self.eps,
                            self.wd, self.step_count, stream_ptr()), "hv_adamw")
 
+    # ---- torch.optim-compatible state (checkpoints load into / from torch.optim.AdamW)
+    def state_dict(self) -> Dict:
+        state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": self.exp_avg[i],
+                     "exp_avg_sq": self.exp_avg_sq[i]} for i in range(len(self.named))}
+        return {"state": state,
+                "param_groups": [{"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
+                                  "weight_decay": self.wd, "amsgrad": False, "maximize": False,
+                                  "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                                  "params": list(range(len(self.named)))}]}
+
+    def load_state_dict(self, sd: Dict) -> None:
+        g = sd["param_groups"][0]
+        self.lr, self.betas, self.eps, self.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+        steps = []
+        for i, (name, p) in enumerate(self.named):
+            st = sd["state"].get(i, sd["state"].get(str(i)))
+            if st is None:
+                continue
+            self.exp_avg[i].copy_(st["exp_avg"])
+            self.exp_avg_sq[i].copy_(st["exp_avg_sq"])
+            steps.append(int(float(st["step"])))
+        if steps:
+            self.step_count = max(steps)
+
     def total_norm(self) -> Tensor:
         """sqrt(sum of squared group norms) (mhc_trainer.py:383), a device scalar."""
         return self.norms.pow(2).sum().sqrt()
@@ -185,8 +209,14 @@ class HVTrainer:
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_grad_norm: float = 1.0, mhc_max_norm: float = 0.5, bucket_mb: int = 64,
-                 broadcast_buffers: bool = True, group=None):
+                 broadcast_buffers: bool = True, group=None, monitor_every: int = 50):
         self.model = model
+        # _monitor_stability (eigvalsh of every H_res, signal ratios) is metrics-only: run it
+        # every `monitor_every` steps instead of every forward (0 disables it)
+        from .manifold import ManifoldHyperConnection
+        for m in model.modules():
+            if isinstance(m, ManifoldHyperConnection):
+                m.monitor_every = monitor_every
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         self.grads = GradBuckets(named, bucket_mb << 20, group)
         self.opt = FusedAdamW(named, lr, weight_decay, betas, eps, (mhc_max_norm, max_grad_norm))
@@ -221,3 +251,26 @@ class HVTrainer:
         self.grads.finish()
         self.opt.step(clip=True)
         return loss
+
+
+def save_checkpoint(path: str, model, trainer: Optional["HVTrainer"] = None, epoch: int = 0, global_step: int = 0,
+                    config: Optional[Dict] = None, history: Optional[Dict] = None,
+                    best_val_loss: float = float("inf"), experiment_name: str = "hv_amd") -> None:
+    """Checkpoint in the reference trainer's format (mhc_trainer.py:595-627): the same keys,
+    model_state_dict in the reference parameter/buffer layout, optimizer_state_dict in
+    torch.optim.AdamW layout (scheduler/scaler states empty: the build uses neither)."""
+    import time
+    ck = {"epoch": epoch, "global_step": global_step, "model_state_dict": model.state_dict(),
+          "optimizer_state_dict": trainer.opt.state_dict() if trainer is not None else {},
+          "scheduler_state_dict": {}, "scaler_state_dict": {}, "config": config or {}, "history": history or {},
+          "best_val_loss": best_val_loss, "experiment_name": experiment_name, "timestamp": time.time()}
+    torch.save(ck, path)
+
+
+def load_checkpoint(path: str, model, trainer: Optional["HVTrainer"] = None, map_location=None) -> Dict:
+    """mhc_trainer.py:629-656: loads model (and optimizer) state; tensors only (weights_only)."""
+    ck = torch.load(path, map_location=map_location, weights_only=True)
+    model.load_state_dict(ck["model_state_dict"])
+    if trainer is not None and ck.get("optimizer_state_dict"):
+        trainer.opt.load_state_dict(ck["optimizer_state_dict"])
+    return ck

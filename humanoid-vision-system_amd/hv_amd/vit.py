@@ -91,6 +91,12 @@ class TransformerEncoderBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "TransformerEncoderBlock")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            n, L, D = x.shape
+            t = x.reshape(n * L, D).to(resolve_dtype(self.residual_mhc1)).contiguous()
+            return TM.encoder_block(self, t, n, TM.module_H(self)).view(n, L, D).to(x.dtype)
         with ctx_scope(self) as ctx:
             n, L, D = x.shape
             t = x.reshape(n * L, D).to(ctx.dtype).contiguous()
@@ -130,6 +136,10 @@ class VisionTransformerEncoder(nn.Module):
         require_cuda(x, "VisionTransformerEncoder")
         if return_features:
             raise NotImplementedError("return_features is not on the HybridVision path")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            return TM.vit_encoder(self, TM.nhwc_in(x, resolve_dtype(self.patch_embed.mhc_enhance)), TM.module_H(self))
         with ctx_scope(self) as ctx:
             return self.forward_nhwc(to_nhwc(x, ctx.dtype))
 
@@ -174,5 +184,10 @@ class HybridVisionEncoder(nn.Module):
 
     def forward(self, cnn_features: torch.Tensor) -> torch.Tensor:
         require_cuda(cnn_features, "HybridVisionEncoder")
+        if self.training and torch.is_grad_enabled():
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            x = TM.nhwc_in(cnn_features, resolve_dtype(self.fusion_mhc))
+            return to_nchw_view(TM.hybrid_encoder(self, x, TM.module_H(self)))
         with ctx_scope(self) as ctx:
             return to_nchw_view(self.forward_nhwc(to_nhwc(cnn_features, ctx.dtype)))

@@ -530,3 +530,28 @@ def test_trainer_step_reduces_loss(gpu_device):
     losses = [tr.step(x, tg)["total_loss"].item() for _ in range(6)]
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+def test_module_level_training_api(gpu_device):
+    """The drop-in modules train on their own (reference test style, test_models.py:130-187):
+    finite outputs, gradients reach every parameter that influences the output, and the
+    training-mode stability monitor fills the reference buffers."""
+    from hv_amd import ConvMHCLayer, ManifoldHyperConnection, TransformerEncoderBlock
+    torch.manual_seed(0)
+    m = ManifoldHyperConnection(64, expansion_rate=4).to(gpu_device).train()
+    x = torch.randn(2, 10, 64, device=gpu_device, requires_grad=True)
+    y = m(x)
+    y.float().pow(2).mean().backward()
+    assert torch.isfinite(x.grad).all()
+    gn = torch.nn.utils.clip_grad_norm_(m.parameters(), 1e9)
+    assert torch.isfinite(gn) and gn < 100
+    met = m.get_stability_metrics()
+    assert "signal_ratio" in met and met["max_eigenvalue"] <= 1.0 + 1e-3
+    c = ConvMHCLayer(32, 32, 3, 1).to(gpu_device).train()
+    xi = torch.randn(2, 32, 16, 16, device=gpu_device, requires_grad=True)
+    c(xi).float().sum().backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in c.parameters())
+    blk = TransformerEncoderBlock(256, 8).to(gpu_device).train()
+    t = torch.randn(2, 17, 256, device=gpu_device, requires_grad=True)
+    blk(t).float().sum().backward()
+    assert torch.isfinite(t.grad).all()
