@@ -334,6 +334,10 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
 
+static int g_big_tile = 0;   // 256x256 LDS-DMA kernel: 0 off (default: not faster yet), 1 by shape, 2 always
+int hv_gemm_big_tile_mode() { return g_big_tile; }
+extern "C" void hv_gemm_set_big_tile(int mode) { g_big_tile = mode; }
+
 static int g_force_regstage = 0;
 static int hv_gemm_force_regstage() { return g_force_regstage; }
 // 1: route every GEMM through the register-staged kernel (A/B testing of the two paths)

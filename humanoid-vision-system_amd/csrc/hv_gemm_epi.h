@@ -77,11 +77,11 @@ __device__ __forceinline__ void epi_train(const hv_gemm_desc& d, const f32x4& ac
   }
 }
 
-template <int BM, int BN, bool LN_EPI, bool TRAIN = false>
-__device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4 (&acc)[BM / 32][BN / 32],
+// WN waves along N (WM = waves / WN along M); every wave owns an (RM*16) x (RN*16) sub-tile.
+template <int BM, int BN, bool LN_EPI, bool TRAIN = false, int WN = 2, int RM = BM / 32, int RN = BN / 32>
+__device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN],
                                               int m0, int n0) {
-  constexpr int RM = BM / 32, RN = BN / 32;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 1, wc = wid & 1;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / WN, wc = wid % WN;
   const int fr = lane & 15, fg = lane >> 4;
   const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
   const bool gelu_fast = c_bf && !d.residual;
@@ -93,7 +93,7 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
   for (int b = 0; b < RN; ++b)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * (BN / 2) + b * 16 + fg * 4 + j;
+      const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4 + j;
       const bool ok = col < d.N;
       sc[b][j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
       bi[b][j] = (d.bias && ok) ? d.bias[col] : 0.f;
@@ -103,7 +103,7 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
 
 #pragma unroll
   for (int a = 0; a < RM; ++a) {
-    const int row = m0 + wr * (BM / 2) + a * 16 + fr;
+    const int row = m0 + wr * (RM * 16) + a * 16 + fr;
     if (row >= d.M) continue;
     float mean = 0.f, rstd = 1.f;
     if constexpr (LN_EPI) {
@@ -113,7 +113,7 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
     const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
 #pragma unroll
     for (int b = 0; b < RN; ++b) {
-      const int col = n0 + wc * (BN / 2) + b * 16 + fg * 4;
+      const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4;
       if (col >= d.N) continue;
       float v[4];
       if constexpr (!TRAIN) {

@@ -115,6 +115,8 @@ typedef struct hv_gemm_desc {
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* path selection for A/B tests: 1 = register-staged kernel only, 0 = default (LDS-DMA when eligible) */
 void hv_gemm_set_path(int regstage_only);
+/* 256x256-tile LDS-DMA kernel selection: 0 off (default), 1 by shape, 2 whenever eligible */
+void hv_gemm_set_big_tile(int mode);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
