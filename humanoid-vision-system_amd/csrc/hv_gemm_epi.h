@@ -16,9 +16,9 @@
 // Training epilogue modes (hv_gemm_desc.epi_mode 1/2, see hv_kernels.h).  A lane holds 4
 // consecutive columns: the pre-activation is stored / loaded as one 8-byte (bf16) or 16-byte
 // (fp32) vector when the row allows it.
-__device__ __forceinline__ void epi_train(const hv_gemm_desc& d, const f32x4& acc, float (&v)[4], int row, int col,
-                                          const float (&sc)[4], const float (&bi)[4], const float (&cs)[4],
-                                          float mean, float rstd, bool ln_epi) {
+__device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 acc, int row, int col, const f32x4 sc,
+                                           const f32x4 bi, const f32x4 cs, float mean, float rstd, bool ln_epi) {
+  f32x4 v;
   const bool aux_bf = d.aux_dtype == HV_BF16;
   const bool vec = col + 4 <= d.N && (d.ld_aux & 3) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
   const long ai = (long)row * d.ld_aux + col;
@@ -75,6 +75,7 @@ __device__ __forceinline__ void epi_train(const hv_gemm_desc& d, const f32x4& ac
     for (int j = 0; j < 4; ++j)
       v[j] = acc[j] * d.alpha * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
   }
+  return v;
 }
 
 // WN waves along N (WM = waves / WN along M); every wave owns an (RM*16) x (RN*16) sub-tile.
@@ -125,7 +126,10 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
           v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
         }
       } else {
-        epi_train(d, acc[a][b], v, row, col, sc[b], bi[b], cs[b], mean, rstd, LN_EPI);
+        const f32x4 t = epi_train(d, acc[a][b], row, col, f32x4{sc[b][0], sc[b][1], sc[b][2], sc[b][3]},
+                                  f32x4{bi[b][0], bi[b][1], bi[b][2], bi[b][3]},
+                                  f32x4{cs[b][0], cs[b][1], cs[b][2], cs[b][3]}, mean, rstd, LN_EPI);
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
       }
       if (vec && col + 4 <= d.N) {
         if (d.residual) {

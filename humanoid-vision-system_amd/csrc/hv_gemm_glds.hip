@@ -332,6 +332,6 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
                       (hv_gemm_big_tile_mode() == 1 && d.N >= 256 && t256 >= 192)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
-  if (d.M <= 64 || t128 < 256 || d.epi_mode) return launch<64, 128>(d, s);   // 128x128 + training epilogue spills
+  if (d.M <= 64 || t128 < 256 || d.epi_mode) return launch<64, 128>(d, s);   // 128x128 + training epilogue: acc demoted to scratch, 2x slower
   return launch<128, 128>(d, s);
 }

@@ -160,7 +160,10 @@ def _mhc_coefficients(m, H_res: Tensor, W1: Tensor, b1: Tensor, dt):
     gc, u, wct = ops.mhc_prep(m.H_pre_raw, m.H_post_raw, H_res, m.norm_pre.weight, m.norm_pre.bias,
                               gc_transposed=False)
     w1 = f32(W1)
-    A1 = ops.gemm(gc, w1)                          # [D, 2Hd] = Gc W1^T (fp32 MFMA)
+    if dt == torch.bfloat16:                       # [D, 2Hd] = Gc W1^T on the bf16 MFMA (fp32 result)
+        A1 = ops.gemm(ops.cast(gc, dt), ops.cast(w1, dt), out_dtype=torch.float32)
+    else:
+        A1 = ops.gemm(gc, w1)
     c1 = ops.gemv(w1, u, b1)                       # [2Hd]
     return gc, u, wct, A1, c1
 
@@ -222,7 +225,8 @@ class MhcFn(torch.autograd.Function):
                                       param_grads=False)
         # ---- coefficient backward (parameter-sized fp32)
         w1 = f32(W1)
-        dW1 = ops.gemm(dA1t, T.transpose_cast(gc, torch.float32))      # [2Hd, Hd] = dA1t Gc
+        pdt = torch.bfloat16 if dt == torch.bfloat16 else torch.float32   # parameter-side GEMM operands
+        dW1 = ops.gemm(ops.cast(dA1t, pdt), T.transpose_cast(gc, pdt), out_dtype=torch.float32)  # dA1t Gc
         dW1 += torch.outer(dc1, u)
         db1 = dc1
         dGc = T.wgrad(dA1t, w1)                            # [D, Hd] = dA1t^T W1
