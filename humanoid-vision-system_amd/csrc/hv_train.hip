@@ -845,6 +845,57 @@ __global__ void __launch_bounds__(256) k_adamw(const hv_param_entry* tab, int co
   }
 }
 
+// ------------------------------------------------------------------ mHC coefficient backward
+// d/d(H_pre_raw, gamma_pre, beta_pre) from dGc (gradient of the centred folded gate) and du:
+// dG = dGc - colmean_i(dGc) (adjoint of the centring), dS = gamma_i dG + beta_i du_j,
+// dH_pre_raw = dS s(1-s), dgamma_i = sum_j dG_ij s_ij, dbeta_i = sum_j du_j s_ij.  Wave per row i.
+__global__ void __launch_bounds__(256) k_mhc_pre_bwd(const float* __restrict__ dgc, const float* __restrict__ colsum,
+                                                     const float* __restrict__ du, const float* __restrict__ hraw,
+                                                     const float* gamma, const float* beta, int D, int Hd,
+                                                     float* dhraw, float* dgamma, float* dbeta) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= D) return;
+  const float gi = gamma ? gamma[i] : 1.f, bi = beta ? beta[i] : 0.f, invD = 1.0f / D;
+  float sg = 0.f, sb = 0.f;
+  for (int j = lane; j < Hd; j += 64) {
+    const long o = (long)i * Hd + j;
+    const float sj = hv_sigmoid(hraw[o]);
+    const float dg = dgc[o] - colsum[j] * invD;
+    sg += dg * sj;
+    sb += du[j] * sj;
+    dhraw[o] = (gi * dg + bi * du[j]) * sj * (1.f - sj);
+  }
+  sg = wave_sum(sg);
+  sb = wave_sum(sb);
+  if (lane == 0) {
+    dgamma[i] = sg;
+    dbeta[i] = sb;
+  }
+}
+
+// rows r < D: dH_res = dWc_x - rowmean;  rows r >= D: dH_post_raw = (dWc_h - rowmean) 2 s(1-s)
+__global__ void __launch_bounds__(256) k_mhc_post_bwd(const float* __restrict__ dwx, const float* __restrict__ dwh,
+                                                      const float* __restrict__ hpost_raw, int D, int Hd, float* dhres,
+                                                      float* dhpost) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= D + Hd) return;
+  const bool res = r < D;
+  const float* src = res ? dwx + (long)r * D : dwh + (long)(r - D) * D;
+  float m = 0.f;
+  for (int j = lane; j < D; j += 64) m += src[j];
+  m = wave_sum(m) / D;
+  for (int j = lane; j < D; j += 64) {
+    const float v = src[j] - m;
+    if (res) {
+      dhres[(long)r * D + j] = v;
+    } else {
+      const long o = (long)(r - D) * D + j;
+      const float sp = hv_sigmoid(hpost_raw[o]);
+      dhpost[o] = v * 2.f * sp * (1.f - sp);
+    }
+  }
+}
+
 inline unsigned grid_for(long n) {
   long b = (n + 255) / 256;
   return (unsigned)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -1152,6 +1203,30 @@ extern "C" int hv_adamw(const hv_param_entry* tab, int count, int total_blocks, 
   const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
   k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, lr, beta1, beta2, eps, weight_decay, bc1,
                                                          bc2s);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" size_t hv_mhc_param_backward_work_floats(int D, int Hd) {
+  return colred_ok(Hd) ? colred_work(D, Hd, 1, 1) + Hd : (size_t)red_chunks(D) * Hd + Hd;
+}
+
+extern "C" int hv_mhc_param_backward(int D, int Hd, const float* dgc, const float* du, const float* h_pre_raw,
+                                     const float* gamma_pre, const float* beta_pre, const float* dwc_x,
+                                     const float* dwc_h, const float* h_post_raw, float* dh_pre_raw, float* dgamma,
+                                     float* dbeta, float* dh_res, float* dh_post_raw, float* work,
+                                     hv_stream_t stream) {
+  if (!dgc || !du || !h_pre_raw || !dwc_x || !dwc_h || !h_post_raw || !dh_pre_raw || !dgamma || !dbeta || !dh_res ||
+      !dh_post_raw || !work || D <= 0 || Hd <= 0)
+    return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t wpart = colred_ok(Hd) ? colred_work(D, Hd, 1, 1) : (size_t)red_chunks(D) * Hd;
+  float* colsum = work + wpart;
+  const int rc = hv_colsum(HV_F32, dgc, Hd, D, Hd, colsum, 0, work, stream);
+  if (rc) return rc;
+  k_mhc_pre_bwd<<<hv_cdiv(D, 4), 256, 0, s>>>(dgc, colsum, du, h_pre_raw, gamma_pre, beta_pre, D, Hd, dh_pre_raw,
+                                               dgamma, dbeta);
+  k_mhc_post_bwd<<<hv_cdiv(D + Hd, 4), 256, 0, s>>>(dwc_x, dwc_h, h_post_raw, D, Hd, dh_res, dh_post_raw);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -150,6 +150,8 @@ _SIGS = {
     "hv_rownorm_backward": ([i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, f32, C.c_uint, i32, vp, vp, vp, vp,
                              vp, vp], i32),
     "hv_act_backward": ([i32, vp, vp, i64, i32, f32, C.c_uint, vp, vp], i32),
+    "hv_mhc_param_backward_work_floats": ([i32, i32], C.c_size_t),
+    "hv_mhc_param_backward": ([i32, i32] + [vp] * 14 + [vp], i32),
     "hv_dropout": ([i32, vp, i64, f32, C.c_uint, vp, vp], i32),
     "hv_sinkhorn_bwd_work_floats": ([i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_backward": ([vp, i32, i32, i32, i32, i32, vp], i32),

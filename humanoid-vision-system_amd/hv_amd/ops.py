@@ -24,6 +24,16 @@ def _cuda(*ts):
             raise RuntimeError("hv_amd ops require CUDA(HIP) tensors; there is no CPU path")
 
 
+def upload_table(entries, device) -> Tensor:
+    """ctypes struct array -> device bytes, asynchronously (pinned staging + non_blocking copy
+    on the current stream): a table upload never synchronises the host with the GPU, so it can
+    sit inside a training forward/backward without draining the queue."""
+    host = torch.frombuffer(bytearray(bytes(entries)), dtype=torch.uint8)
+    if torch.device(device).type == "cuda":
+        host = host.pin_memory()
+    return host.to(device, non_blocking=True)
+
+
 def _contig(t: Tensor, name: str) -> Tensor:
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
@@ -277,8 +287,7 @@ class SinkhornGroup:
         if rp != self._raw_ptrs:
             for e, p in zip(self.entries, rp):
                 e.raw = p
-            host = torch.frombuffer(bytearray(bytes(self.entries)), dtype=torch.uint8)
-            self.table = host.to(self.device)
+            self.table = upload_table(self.entries, self.device)
             self._raw_ptrs = rp
         rs, rbs, cs = self.totals
         check(L.lib().hv_sinkhorn_group_forward(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
@@ -305,7 +314,7 @@ class SinkhornGroup:
             be.dout, be.draw, be.bwork = d.data_ptr(), dr.data_ptr(), bw.data_ptr()
             keep += [d, bw]
             draws.append(dr.view(raw.shape))
-        table = torch.frombuffer(bytearray(bytes(bent)), dtype=torch.uint8).to(self.device)
+        table = upload_table(bent, self.device)
         rs, rbs, cs = self.totals
         check(lib.hv_sinkhorn_group_backward(table.data_ptr(), n_e, rs, rbs, cs, max(self.iters), stream_ptr()),
               "hv_sinkhorn_group_backward")
@@ -521,7 +530,7 @@ def nms_batched(decoded, conf_thr: float, iou_thr: float, max_det: int):
         ents[i].boxes, ents[i].class_scores, ents[i].class_indices, ents[i].cells = \
             bx.data_ptr(), sc.data_ptr(), ci.data_ptr(), cells
         keep += [bx, sc, ci]
-    table = torch.frombuffer(bytearray(bytes(ents)), dtype=torch.uint8).to(dev)
+    table = upload_table(ents, dev)
     boxes = torch.empty((B, max_det, 4), device=dev, dtype=torch.float32)
     scores = torch.empty((B, max_det), device=dev, dtype=torch.float32)
     labels = torch.empty((B, max_det), device=dev, dtype=torch.int64)

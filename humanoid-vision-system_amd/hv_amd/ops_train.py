@@ -427,3 +427,24 @@ def yolo_loss(logits: Tensor, targets: Tensor, A: int, lambdas, grad_dtype: Opti
                                lcl, sums.data_ptr(), dtype_code(dl.dtype), dl.data_ptr(), work.data_ptr(),
                                stream_ptr()), "hv_yolo_loss")
     return sums, dl
+
+
+def mhc_param_backward(dgc: Tensor, du: Tensor, h_pre_raw, gamma_pre, beta_pre, dwc_x: Tensor, dwc_h: Tensor,
+                       h_post_raw):
+    """One site's coefficient backward (hv_mhc_param_backward): returns dH_pre_raw, dgamma_pre,
+    dbeta_pre, dH_res, dH_post_raw (fp32)."""
+    D, Hd = dgc.shape
+    dev = dgc.device
+    hp, g, b, hq = f32(h_pre_raw), f32(gamma_pre), f32(beta_pre), f32(h_post_raw)
+    dgc, du, dwc_x, dwc_h = (_contig(t, "grad") for t in (dgc, du.contiguous(), dwc_x, dwc_h))
+    dhp = torch.empty((D, Hd), device=dev, dtype=torch.float32)
+    dg = torch.empty(D, device=dev, dtype=torch.float32)
+    db = torch.empty(D, device=dev, dtype=torch.float32)
+    dhr = torch.empty((D, D), device=dev, dtype=torch.float32)
+    dhq = torch.empty((Hd, D), device=dev, dtype=torch.float32)
+    work = _work(L.lib().hv_mhc_param_backward_work_floats(D, Hd), dev)
+    check(L.lib().hv_mhc_param_backward(D, Hd, dgc.data_ptr(), du.data_ptr(), hp.data_ptr(), g.data_ptr(),
+                                        b.data_ptr(), dwc_x.data_ptr(), dwc_h.data_ptr(), hq.data_ptr(),
+                                        dhp.data_ptr(), dg.data_ptr(), db.data_ptr(), dhr.data_ptr(), dhq.data_ptr(),
+                                        work.data_ptr(), stream_ptr()), "hv_mhc_param_backward")
+    return dhp, dg, db, dhr, dhq

@@ -230,18 +230,9 @@ class MhcFn(torch.autograd.Function):
         dW1 += torch.outer(dc1, u)
         db1 = dc1
         dGc = T.wgrad(dA1t, w1)                            # [D, Hd] = dA1t^T W1
-        dG = dGc - dGc.mean(dim=0, keepdim=True)           # adjoint of the centring over inputs
-        du = torch.mv(w1.t(), dc1)                         # [Hd]
-        S = torch.sigmoid(f32(H_pre_raw))
-        gp, bp = f32(g_pre), f32(b_pre)
-        dg_pre = (dG * S).sum(dim=1)
-        db_pre = (S * du[None, :]).sum(dim=1)
-        dS = gp[:, None] * dG + bp[:, None] * du[None, :]
-        dH_pre_raw = dS * S * (1.0 - S)
-        dH_res = dwc_x - dwc_x.mean(dim=1, keepdim=True)
-        dH_post = dwc_h - dwc_h.mean(dim=1, keepdim=True)
-        Sp = torch.sigmoid(f32(H_post_raw))
-        dH_post_raw = dH_post * 2.0 * Sp * (1.0 - Sp)
+        du = torch.mv(w1.t(), dc1)                         # [Hd] = W1^T dc1
+        dH_pre_raw, dg_pre, db_pre, dH_res, dH_post_raw = T.mhc_param_backward(
+            dGc, du, H_pre_raw, g_pre, b_pre, dwc_x, dwc_h, H_post_raw)
         return (dx, dH_res, dH_pre_raw, dH_post_raw, dg_pre, db_pre, dW1, db1, dW2, db2, dg_post, db_post,
                 None, None)
 

@@ -154,7 +154,8 @@ class FusedAdamW:
             e.blk = blk
             blk += lib.hv_param_blocks(p.numel())
         self._blocks = blk
-        self._table = torch.frombuffer(bytearray(bytes(ents)), dtype=torch.uint8).to(self.device)
+        from .ops import upload_table
+        self._table = upload_table(ents, self.device)
         self._work = torch.empty(2 * blk, device=self.device, dtype=torch.float32)
 
     def step(self, clip: bool = True):

@@ -409,6 +409,15 @@ int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, cons
                         int cols, const float* mean, const float* rstd, const float* gamma,
                         float drop_p, unsigned int seed, int dx_dtype, void* dx, const void* dx_add,
                         float* dgamma, float* dbeta, float* work, hv_stream_t stream);
+/* Coefficient backward of one mHC site (autograd of constrained_matrices, manifold_layers.py:
+   205-221, through the fold of DESIGN.md §2): from dGc [D, Hd] (gradient of the centred gate),
+   du [Hd], dWc_x [D, D] and dWc_h [Hd, D] (gradients of the centred output coefficients):
+   dH_pre_raw, dgamma_pre, dbeta_pre, dH_res (-> Sinkhorn backward) and dH_post_raw. fp32. */
+size_t hv_mhc_param_backward_work_floats(int D, int Hd);
+int hv_mhc_param_backward(int D, int Hd, const float* dgc, const float* du, const float* h_pre_raw,
+                          const float* gamma_pre, const float* beta_pre, const float* dwc_x,
+                          const float* dwc_h, const float* h_post_raw, float* dh_pre_raw, float* dgamma,
+                          float* dbeta, float* dh_res, float* dh_post_raw, float* work, hv_stream_t stream);
 /* dpre[i] = dy[i] * keep(i) * act'(pre[i])  (elementwise; dy/pre/dpre share dtype) */
 int hv_act_backward(int dtype, const void* dy, const void* pre, long n, int act, float drop_p,
                     unsigned int seed, void* dpre, hv_stream_t stream);

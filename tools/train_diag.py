@@ -58,7 +58,7 @@ if what in ("time", "all"):
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 640
     torch.manual_seed(0)
     m = HybridVisionSystem({"image_size": S, "precision": "bf16", "verbose": False}).to(dev).train()
-    tr = HVTrainer(m)
+    tr = HVTrainer(m, monitor_every=0)   # metrics-only monitor off while timing kernels
     x = torch.randn(B, 3, S, S, device=dev)
     tg = [t.to(dev) for t in synthetic_targets(B, S, seed=3)]
     for i in range(2):
@@ -70,5 +70,12 @@ if what in ("time", "all"):
         loss = tr.step(x, tg)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n
+    # host-side cost of one step (launch + autograd bookkeeping) with the GPU kept busy
+    torch.cuda.synchronize()
+    h0 = time.perf_counter()
+    tr.step(x, tg)
+    host_ms = (time.perf_counter() - h0) * 1e3
+    torch.cuda.synchronize()
+    print(f"host time of one step (no sync inside) {host_ms:.1f} ms")
     print(f"train step B={B} S={S}: {dt * 1e3:.1f} ms  {B / dt:.2f} img/s  loss={loss['total_loss'].item():.3f}"
           f"  mem={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
