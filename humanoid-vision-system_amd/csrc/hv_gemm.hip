@@ -336,6 +336,9 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
 
 static int g_big_tile = 0;   // 256x256 LDS-DMA kernel: 0 off (default: not faster yet), 1 by shape, 2 always
 int hv_gemm_big_tile_mode() { return g_big_tile; }
+static int g_small_tile = 1; // 64x64 LDS-DMA tiles for small grids: 1 on (default), 0 off (A/B tests)
+int hv_gemm_small_tile_mode() { return g_small_tile; }
+extern "C" void hv_gemm_set_small_tile(int mode) { g_small_tile = mode; }
 extern "C" void hv_gemm_set_big_tile(int mode) { g_big_tile = mode; }
 
 static int g_force_regstage = 0;

@@ -318,6 +318,7 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 }  // namespace
 
 int hv_gemm_big_tile_mode();   // hv_gemm.hip
+int hv_gemm_small_tile_mode();  // hv_gemm.hip
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
@@ -332,6 +333,9 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
                       (hv_gemm_big_tile_mode() == 1 && d.N >= 256 && t256 >= 192)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
+  // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs
+  const long t64x128 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 128);
+  if (hv_gemm_small_tile_mode() && t64x128 < 320) return launch<64, 64>(d, s);
   if (d.M <= 64 || t128 < 256 || d.epi_mode) return launch<64, 128>(d, s);   // 128x128 + training epilogue: acc demoted to scratch, 2x slower
   return launch<128, 128>(d, s);
 }

@@ -692,12 +692,15 @@ __global__ void k_scatter_rows(const T* dy, long stride, int n, int c, T* dx) {
 }
 
 // ------------------------------------------------------------------ YOLO loss
-__global__ void __launch_bounds__(1024) k_yolo_count(const float* targets, long cells, int P, float* nobj) {
+// object count: block partial counts added atomically (integer-valued floats < 2^24: exact in
+// any order, so deterministic)
+__global__ void __launch_bounds__(256) k_yolo_count(const float* targets, long cells, int P, float* nobj) {
   __shared__ float scratch[16];
   float s = 0.f;
-  for (long i = threadIdx.x; i < cells; i += blockDim.x) s += targets[i * P + 4] > 0.5f ? 1.f : 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < cells; i += (long)gridDim.x * 256)
+    s += targets[i * P + 4] > 0.5f ? 1.f : 0.f;
   s = block_sum(s, scratch);
-  if (threadIdx.x == 0) nobj[0] = s;
+  if (threadIdx.x == 0 && s > 0.f) atomicAdd(nobj, s);
 }
 
 __device__ __forceinline__ float bce_logits(float x, float t) {
@@ -1167,7 +1170,8 @@ extern "C" int hv_yolo_loss(int dtype, const void* logits, const float* targets,
   float* nobj = work;
   float* part = work + 8;
   const unsigned nblk = hv_cdiv(cells, 256);
-  k_yolo_count<<<1, 1024, 0, s>>>(targets, cells, P, nobj);
+  HV_CHECK(hipMemsetAsync(nobj, 0, sizeof(float), s));
+  k_yolo_count<<<(unsigned)((cells + 255) / 256 < 1024 ? (cells + 255) / 256 : 1024), 256, 0, s>>>(targets, cells, P, nobj);
 #define YL_LAUNCH(T, TD) k_yolo_loss<T, TD><<<nblk, 256, 0, s>>>((const T*)logits, targets, n, h, w, A, P, l_coord, \
       l_obj, l_noobj, l_cls, nobj, (TD*)dlogits, part)
   if (dtype == HV_F32 && d_dtype == HV_F32) YL_LAUNCH(float, float);

@@ -117,6 +117,8 @@ int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 void hv_gemm_set_path(int regstage_only);
 /* 256x256-tile LDS-DMA kernel selection: 0 off (default), 1 by shape, 2 whenever eligible */
 void hv_gemm_set_big_tile(int mode);
+/* 64x64-tile LDS-DMA kernel for small grids: 1 on (default), 0 off */
+void hv_gemm_set_small_tile(int mode);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
