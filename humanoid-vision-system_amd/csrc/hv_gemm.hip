@@ -334,7 +334,7 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
 
-static int g_big_tile = 0;   // 256x256 LDS-DMA kernel: 0 off (default: not faster yet), 1 by shape, 2 always
+static int g_big_tile = 1;   // 256x256 ping-pong LDS-DMA kernel: 0 off, 1 by shape (default), 2 always
 int hv_gemm_big_tile_mode() { return g_big_tile; }
 static int g_small_tile = 1; // 64x64 LDS-DMA tiles for small grids: 1 on (default), 0 off (A/B tests)
 int hv_gemm_small_tile_mode() { return g_small_tile; }

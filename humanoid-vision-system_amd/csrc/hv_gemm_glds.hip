@@ -10,6 +10,7 @@
 // clamped (computed, never stored).
 #include "hv_common.h"
 #include "hv_gemm_epi.h"
+#include <type_traits>
 
 __device__ __attribute__((aligned(64))) uint4 hv_glds_zero_line[4];   // read by out-of-image taps
 
@@ -25,6 +26,17 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base)
   (void)src; (void)lds_base;
 #endif
 }
+
+// The same 16-byte LDS-DMA as inline asm (M0 = wave-uniform LDS byte address).  The compiler
+// does not track it, so it does not drain vmcnt before every ds_read that follows the issue
+// (it cannot tell the other buffer's DMA from this buffer's reads); the kernel that uses it
+// waits for its DMAs itself with explicit vmcnt.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_asm(const void* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
+#pragma clang diagnostic pop
 
 template <int BM, int BN, bool CONV, bool TRAIN>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
@@ -157,18 +169,54 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// 256x256 tile, 8 waves (2 along M x 4 along N, 128x64 per wave, 32 accumulators), BK = 64,
-// one 128-KiB LDS array with two K-tile buffers.  The LDS-DMA of tile k+1 is issued right after
-// the barrier that opens tile k and stays in flight across the whole compute of tile k: raw
-// s_barrier (no implicit vmcnt(0) drain) + an explicit vmcnt(0) only where tile k+1 is needed.
-// MFMA clusters at raised wave priority.  (MI355X guide §5: the 128x128 two-barrier structure
-// tops out near 900 TF; this is the ~1 block/CU pipelined structure.)
+// 256x256 tile, 8 waves in two groups (wr = wave / 4: 128 rows each; wc = wave % 4: 64 columns
+// each), BK = 64, one 128-KiB LDS array holding two K-tile buffers ([256 A rows | 256 B rows] x
+// 128 B, the same XOR-swizzled image as above).
+//
+// PING-PONG: every K-tile is four phases, one 64x32 quadrant of the wave's 128x64 output per
+// phase (16 MFMAs over K = 64); a phase is a LOAD section (ds_read of the quadrant's fragments,
+// LDS-DMA issue, counted vmcnt) and an MFMA section, each closed by a raw s_barrier.  Group 1
+// runs one barrier behind group 0, so on every SIMD (waves w and w+4 share one) one wave reads
+// LDS while the other keeps the matrix core busy.
+//
+//   phase 1 reads A top (rows g*128 + 0..63) + B left (cols wc*64 + 0..31)  -> quadrant (T, L)
+//   phase 2 reads B right                                                    -> (T, R)
+//   phase 3 reads A bottom                                                   -> (B, R)
+//   phase 4 reads nothing (fragments still in registers)                     -> (B, L)
+//
+// A K-tile's buffer is staged in three PARTS, each freed by a phase's reads: TL (A top + B left,
+// 4 DMAs per wave), R (B right, 2), B (A bottom, 2).  K-tile t+2 goes into K-tile t's buffer part
+// by part as soon as the part is free: TL in phase 2, R in phase 3, B in phase 4 (WAR: every
+// load section ends with lgkmcnt(0) before its barrier, so group 1's phase-p reads are complete
+// before group 0's phase-(p+1) load section).  Prefetch distance ~1.5-2 K-tiles.  RAW: before
+// the barrier that ends the load section preceding a part's first read, every wave waits with a
+// counted vmcnt for its own DMAs of that part (the younger DMAs stay in flight); readers of
+// group 0 are one barrier, of group 1 two barriers past every wave's wait.  DMAs are issued with
+// inline asm (glds16_asm) so the compiler does not drain vmcnt before the ds_reads.
 constexpr int B256_STAGE = 512 * ROW;       // (256 A + 256 B rows) x 128 B per K-tile buffer
 
+template <int AH, int BH>
+__device__ __forceinline__ void pp_quadrant(f32x4 (&acc)[8][4], const uint4 (&fa)[4][2], const uint4 (&fb)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[AH * 4 + a][BH * 2 + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, fb[b][s]), __builtin_bit_cast(bf16x8, fa[a][s]), acc[AH * 4 + a][BH * 2 + b],
+            0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+#define PP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define PP_SYNC_LDS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
 template <bool CONV>
-__global__ void __launch_bounds__(512) gemm_glds256_kernel(const hv_gemm_desc d) {
-  constexpr int BM = 256, BN = 256, AI = 4, BI = 4;   // glds instructions per wave per tile (8 rows each)
-  constexpr int RM = 8, RN = 4;                       // 16x16 sub-tiles per wave
+__global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int RM = 8, RN = 4;                       // 16x16 sub-tiles per wave (128 x 64)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * B256_STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -184,12 +232,22 @@ __global__ void __launch_bounds__(512) gemm_glds256_kernel(const hv_gemm_desc d)
   const int tm = bid / tilesN, tn = bid % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
 
+  // staging map: DMA i of this wave covers 8 consecutive tile rows; i = 0,1 the A-top / B-left
+  // part, i = 2,3 the A-bottom / B-right part (16 row groups per part, two per wave)
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
   const int lrow = lane >> 3, pchunk = lane & 7;
-  const unsigned short* arow[AI];
-  int aih[AI], aiw[AI];
+  int arow0[4], brow0[4];                              // first tile row / column of DMA i (uniform)
 #pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    int row = m0 + (wid * AI + i) * 8 + lrow;
+  for (int i = 0; i < 4; ++i) {
+    const int q = wu * 2 + (i & 1);
+    arow0[i] = (q >> 3) * 128 + (i >> 1) * 64 + (q & 7) * 8;
+    brow0[i] = (q >> 2) * 64 + (i >> 1) * 32 + (q & 3) * 8;
+  }
+  const unsigned short* arow[4];
+  int aih[4], aiw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int row = m0 + arow0[i] + lrow;
     row = row < d.M ? row : d.M - 1;
     if constexpr (CONV) {
       const int hw = d.conv_oh * d.conv_ow;
@@ -203,41 +261,63 @@ __global__ void __launch_bounds__(512) gemm_glds256_kernel(const hv_gemm_desc d)
       arow[i] = (const unsigned short*)d.A + (long)row * d.lda;
     }
   }
-  const unsigned short* brow[BI];
+  const unsigned short* brow[4];
 #pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    int n = n0 + (wid * BI + i) * 8 + lrow;
+  for (int i = 0; i < 4; ++i) {
+    int n = n0 + brow0[i] + lrow;
     n = n < d.N ? n : d.N - 1;
     brow[i] = (const unsigned short*)d.B + (long)n * d.ldb;
   }
   const int lchunk = pchunk ^ (lrow & 7);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
 
-  auto stage = [&](int buf, int kt) {
-    unsigned char* sa = smem + buf * B256_STAGE;
-    unsigned char* sb = sa + BM * ROW;
+  auto dma_a = [&](int buf, int kt, int i) {
     const int k = kt * 64 + lchunk * 8;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const void* src;
-      if constexpr (CONV) {
-        const int tap = k / d.conv_c, ci = k - tap * d.conv_c;
-        const int kh = tap / d.conv_k, kw = tap - kh * d.conv_k;
-        const int ih = aih[i] + kh, iw = aiw[i] + kw;
-        src = ((unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
-                  ? (const void*)(arow[i] + ((long)ih * d.conv_w + iw) * d.conv_c + ci)
-                  : (const void*)hv_glds_zero_line;
+    const void* src;
+    if constexpr (CONV) {
+      const int tap = k / d.conv_c, ci = k - tap * d.conv_c;
+      const int kh = tap / d.conv_k, kw = tap - kh * d.conv_k;
+      const int ih = aih[i] + kh, iw = aiw[i] + kw;
+      src = ((unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
+                ? (const void*)(arow[i] + ((long)ih * d.conv_w + iw) * d.conv_c + ci)
+                : (const void*)hv_glds_zero_line;
+    } else {
+      if (d.A2 != nullptr && k >= d.k1) {
+        const int row = min(m0 + arow0[i] + lrow, d.M - 1);
+        src = (const unsigned short*)d.A2 + (long)row * d.lda2 + (k - d.k1);
       } else {
-        if (d.A2 != nullptr && k >= d.k1) {
-          const int row = min(m0 + (wid * AI + i) * 8 + lrow, d.M - 1);
-          src = (const unsigned short*)d.A2 + (long)row * d.lda2 + (k - d.k1);
-        } else {
-          src = arow[i] + k;
-        }
+        src = arow[i] + k;
       }
-      glds16(src, sa + (wid * AI + i) * 1024);
     }
+    glds16_asm(src, lds0 + buf * B256_STAGE + arow0[i] * ROW);
+  };
+  auto dma_b = [&](int buf, int kt, int i) {
+    glds16_asm(brow[i] + kt * 64 + lchunk * 8, lds0 + buf * B256_STAGE + BM * ROW + brow0[i] * ROW);
+  };
+  auto part_tl = [&](int buf, int kt) { dma_a(buf, kt, 0); dma_a(buf, kt, 1); dma_b(buf, kt, 0); dma_b(buf, kt, 1); };
+  auto part_r = [&](int buf, int kt) { dma_b(buf, kt, 2); dma_b(buf, kt, 3); };
+  auto part_b = [&](int buf, int kt) { dma_a(buf, kt, 2); dma_a(buf, kt, 3); };
+
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment reads: A rows wr*128 + half*64 + a*16 + fr, B cols wc*64 + half*32 + b*16 + fr;
+  // k-slice s of the 64-deep tile = 16-B chunks {4s + fg}
+  auto read_a = [&](const unsigned char* sa, int half, uint4 (&fa)[4][2]) {
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(brow[i] + k, sb + (wid * BI + i) * 1024);
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = wr * 128 + half * 64 + a * 16 + fr, lc = s * 4 + fg;
+        fa[a][s] = *reinterpret_cast<const uint4*>(sa + r * ROW + ((lc ^ (r & 7)) << 4));
+      }
+  };
+  auto read_b = [&](const unsigned char* sb, int half, uint4 (&fb)[2][2]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = wc * 64 + half * 32 + b * 16 + fr, lc = s * 4 + fg;
+        fb[b][s] = *reinterpret_cast<const uint4*>(sb + r * ROW + ((lc ^ (r & 7)) << 4));
+      }
   };
 
   f32x4 acc[RM][RN];
@@ -247,52 +327,77 @@ __global__ void __launch_bounds__(512) gemm_glds256_kernel(const hv_gemm_desc d)
     for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = d.K / 64;
-  const int fr = lane & 15, fg = lane >> 4;
-  stage(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's part of tile kt landed
-    __builtin_amdgcn_s_barrier();                            // ... everyone's; buffer buf^1 is free
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);                 // in flight across this tile's compute
-    const unsigned char* sa = smem + buf * B256_STAGE;
-    const unsigned char* sb = sa + BM * ROW;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int lc = s * 4 + fg;
-      uint4 fb[RN];
-#pragma unroll
-      for (int b = 0; b < RN; ++b) {
-        const int r = wc * 64 + b * 16 + fr;
-        fb[b] = *reinterpret_cast<const uint4*>(sb + r * ROW + ((lc ^ (r & 7)) << 4));
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {                          // two row halves of the wave's 128 rows
-        uint4 fa[RM / 2];
-#pragma unroll
-        for (int a = 0; a < RM / 2; ++a) {
-          const int r = wr * 128 + (h * 4 + a) * 16 + fr;
-          fa[a] = *reinterpret_cast<const uint4*>(sa + r * ROW + ((lc ^ (r & 7)) << 4));
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int a = 0; a < RM / 2; ++a)
-#pragma unroll
-          for (int b = 0; b < RN; ++b)
-            acc[h * 4 + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, fb[b]), __builtin_bit_cast(bf16x8, fa[a]), acc[h * 4 + a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
+  // prologue: K-tiles 0 and 1 in part order; K-tile 0's TL part retired before the first read
+  part_tl(0, 0); part_r(0, 0); part_b(0, 0);
+  if (nk > 1) {
+    part_tl(1, 1); part_r(1, 1); part_b(1, 1);
+    PP_VMCNT(12);
+  } else {
+    PP_VMCNT(4);
   }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();            // group 1 runs one barrier behind
+
+  uint4 fa[4][2], fbl[2][2], fbr[2][2];
+  // K-tile kt from buffer BUF (compile-time, unrolled by two)
+  auto ktile = [&](auto bufc, int kt) {
+    constexpr int BUF = decltype(bufc)::value;
+    const unsigned char* sa = smem + BUF * B256_STAGE;
+    const unsigned char* sb = sa + BM * ROW;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 1: A top + B left; then K-tile kt's R part must have landed
+    read_a(sa, 0, fa);
+    read_b(sb, 0, fbl);
+    if (n1) PP_VMCNT(10); else PP_VMCNT(2);
+    PP_SYNC_LDS();
+    __builtin_amdgcn_s_barrier();
+    pp_quadrant<0, 0>(acc, fa, fbl);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: B right; K-tile kt+2's TL part into the freed TL region; then kt's B part landed
+    read_b(sb, 1, fbr);
+    if (n2) {
+      part_tl(BUF, kt + 2);
+      PP_VMCNT(12);
+    } else if (n1) {
+      PP_VMCNT(8);
+    } else {
+      PP_VMCNT(0);
+    }
+    PP_SYNC_LDS();
+    __builtin_amdgcn_s_barrier();
+    pp_quadrant<0, 1>(acc, fa, fbr);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: A bottom; K-tile kt+2's R part
+    read_a(sa, 1, fa);
+    if (n2) part_r(BUF, kt + 2);
+    PP_SYNC_LDS();
+    __builtin_amdgcn_s_barrier();
+    pp_quadrant<1, 1>(acc, fa, fbr);
+    __builtin_amdgcn_s_barrier();
+    // phase 4: K-tile kt+2's B part; then K-tile kt+1's TL part landed
+    if (n2) {
+      part_b(BUF, kt + 2);
+      PP_VMCNT(12);
+    } else if (n1) {
+      PP_VMCNT(4);
+    }
+    __builtin_amdgcn_s_barrier();
+    pp_quadrant<1, 0>(acc, fa, fbl);
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    ktile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nk) ktile(std::integral_constant<int, 1>{}, kt + 1);
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();            // equal barrier counts
   if (d.a_mean) gemm_epilogue<BM, BN, true, false, 4, RM, RN>(d, acc, m0, n0);
   else gemm_epilogue<BM, BN, false, false, 4, RM, RN>(d, acc, m0, n0);
 }
 
 int launch256(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
-  if (d.conv_k > 0) gemm_glds256_kernel<true><<<grid, 512, 0, s>>>(d);
-  else gemm_glds256_kernel<false><<<grid, 512, 0, s>>>(d);
+  if (d.conv_k > 0) gemm_pp256_kernel<true><<<grid, 512, 0, s>>>(d);
+  else gemm_pp256_kernel<false><<<grid, 512, 0, s>>>(d);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -329,8 +434,10 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   if (d.ldb % 8) return HV_EUNSUPPORTED;
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   const long t256 = (long)hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
+  // 256x256 ping-pong kernel: long contractions on grids that still fill most CUs (measured:
+  // K = 256 loses to the 128x128 tile -- prologue-bound; K = 512 ties; K >= 1024 wins 10-45 %)
   if (!d.epi_mode && (hv_gemm_big_tile_mode() == 2 ||
-                      (hv_gemm_big_tile_mode() == 1 && d.N >= 256 && t256 >= 192)))
+                      (hv_gemm_big_tile_mode() == 1 && d.K >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
   // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs

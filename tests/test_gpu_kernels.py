@@ -180,6 +180,65 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
     assert rel_err(fast, ref) < 1e-4
 
 
+PP256_CASES = [  # (kind, M, N, K): ragged M/N, 1-3 K-tiles (prologue/tail vmcnt branches), long K
+    ("plain", 4096, 512, 1024), ("plain", 1000, 520, 640), ("plain", 300, 260, 64), ("plain", 513, 300, 128),
+    ("plain", 700, 777, 192), ("gelu_res", 2048, 768, 2048), ("ln", 1500, 1024, 256), ("concat", 1024, 512, 768),
+    ("conv", 2 * 40 * 40, 256, 9 * 64), ("conv", 2 * 20 * 20, 300, 9 * 128)]
+
+
+@pytest.mark.parametrize("kind,M,N,K", PP256_CASES)
+def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
+    """The 256x256 ping-pong LDS-DMA kernel (hv_gemm_set_big_tile(2) forces it) against the
+    default tiles: same per-element k order, so bit-identical outputs; plus a CPU fp32 check."""
+    ops = _ops()
+    from hv_amd import _lib
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    bf = torch.bfloat16
+    if kind == "conv":
+        c = K // 9
+        hw = int(round((M // 2) ** 0.5))
+        x = torch.randn(2, hw, hw, c, generator=g).to(bf).to(gpu_device)
+        w = (torch.randn(N, K, generator=g) / K ** 0.5).to(bf).to(gpu_device)
+        run = lambda: ops.conv2d(x, w, 3, 1, 1, out_dtype=torch.float32)  # noqa: E731
+        ref = F.conv2d(x.float().cpu().permute(0, 3, 1, 2), w.float().cpu().view(N, 3, 3, c).permute(0, 3, 1, 2),
+                       None, 1, 1).permute(0, 2, 3, 1)
+    else:
+        a = torch.randn(M, K, generator=g).to(bf).to(gpu_device)
+        b = (torch.randn(N, K, generator=g) / K ** 0.5).to(bf).to(gpu_device)
+        bias = torch.randn(N, generator=g).to(gpu_device)
+        af, bfl = a.float().cpu(), b.float().cpu()
+        if kind == "plain":
+            run = lambda: ops.gemm(a, b, bias=bias, out_dtype=torch.float32)  # noqa: E731
+            ref = af @ bfl.T + bias.cpu()
+        elif kind == "gelu_res":
+            res = torch.randn(M, N, generator=g).to(bf).to(gpu_device)
+            run = lambda: ops.gemm(a, b, bias=bias, act="gelu", residual=res)  # noqa: E731
+            ref = F.gelu(af @ bfl.T + bias.cpu()) + res.float().cpu()
+        elif kind == "ln":
+            mean = af.mean(1)
+            rstd = 1.0 / torch.sqrt(af.var(1, unbiased=False) + 1e-5)
+            cs = bfl.sum(1)
+            run = lambda: ops.gemm(a, b, bias=bias, a_mean=mean.to(gpu_device), a_rstd=rstd.to(gpu_device),  # noqa: E731
+                                   b_colsum=cs.to(gpu_device), out_dtype=torch.float32)
+            ref = ((af - mean[:, None]) * rstd[:, None]) @ bfl.T + bias.cpu()
+        else:  # K-concatenated operand [a | a2]
+            k1 = 256
+            a1, a2 = a[:, :k1].contiguous(), a[:, k1:].contiguous()
+            run = lambda: ops.gemm(a1, b, a2=a2, out_dtype=torch.float32)  # noqa: E731
+            ref = af @ bfl.T
+    lib = _lib.lib()
+    try:
+        lib.hv_gemm_set_big_tile(0)
+        base = run()
+        lib.hv_gemm_set_big_tile(2)
+        pp = run()
+    finally:
+        lib.hv_gemm_set_big_tile(1)
+    torch.cuda.synchronize()
+    assert torch.equal(pp, base), f"max |diff| {(pp.float() - base.float()).abs().max().item()}"
+    assert rel_err(pp, ref) < (2e-2 if pp.dtype == bf else 1e-4)
+
+
 CONV_CASES = [(3, 32, 3, 2, 1, 33), (32, 32, 3, 1, 1, 20), (32, 64, 3, 2, 1, 17), (64, 32, 1, 1, 0, 9),
               (128, 96, 3, 1, 1, 7), (16, 8, 3, 1, 1, 5)]
 
