@@ -187,3 +187,145 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
     }
   epi_rows<0, LN_EPI, TRAIN, WN, RM, RN>(d, acc, k, m0, n0);
 }
+
+// ---------------------------------------------------------------------------------------------
+// LDS-staged epilogue (inference modes, epi_mode 0).  The fragment layout above writes 16 rows x
+// 32 bytes per store instruction, which holds the GEMM's output stream to ~1 TB/s; here each wave
+// first writes v = act(scale * acc' + bias) as fp32 into an LDS image of SLAB rows x BN columns
+// (16-B chunk c of row r at c ^ (r & 7): conflict-free float4 writes), then every thread of the
+// workgroup streams whole rows out: 8 consecutive columns per thread, residual read with one
+// 16-B load, one 16-B bf16 (or two fp32) store.  Same arithmetic, same rounding as gemm_epilogue
+// (bit-identical outputs).  The slab is the tile (SLAB = BM) or, for the 256x256 kernel, one wave
+// group's 128 rows at a time; `smem` must hold SLAB * BN * 4 bytes and be free (no DMA in flight,
+// no pending reads) -- the caller's last barrier guarantees that.
+// 16-B chunk c of LDS-image row r (CPR chunks per row) lives at c ^ (r & 7)
+template <int CPR>
+__device__ __forceinline__ float4* epi_lds_chunk(unsigned char* smem, int r, int c) {
+  return reinterpret_cast<float4*>(smem + ((long)r * CPR + (c ^ (r & 7))) * 16);
+}
+
+// Row tile A of the wave's accumulators -> LDS image rows lrow0 + A*16 + fr (fp32, activation
+// applied).  Template recursion over A keeps every acc index a constant.
+template <int A, bool LN_EPI, int RM, int RN, int CPR>
+__device__ __forceinline__ void epi_stage_rows(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN], const EpiCols<RN>& k,
+                                               int grow0, int lrow0, int lcol0, unsigned char* smem) {
+  if constexpr (A < RM) {
+    const int lane = threadIdx.x & 63, fr = lane & 15, fg = lane >> 4;
+    const bool gelu_fast = d.c_dtype == HV_BF16 && !d.residual;
+    const int row = grow0 + A * 16 + fr;
+    float mean = 0.f, rstd = 1.f;
+    if constexpr (LN_EPI) {
+      const int rr = row < d.M ? row : d.M - 1;
+      mean = d.a_mean[rr];
+      rstd = d.a_rstd[rr];
+    }
+#pragma unroll
+    for (int b = 0; b < RN; ++b) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = acc[A][b][j];
+        if constexpr (LN_EPI) x = rstd * (x - mean * k.cs[b][j]);
+        x = x * k.sc[b][j] + k.bi[b][j];
+        v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+      }
+      *epi_lds_chunk<CPR>(smem, lrow0 + A * 16 + fr, (lcol0 + b * 16) / 4 + fg) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    epi_stage_rows<A + 1, LN_EPI, RM, RN, CPR>(d, acc, k, grow0, lrow0, lcol0, smem);
+  }
+}
+
+// Coalesced write-out of an LDS image of SLAB rows (tile rows r0 ..) x BN columns.
+template <int BN, int NT, int SLAB>
+__device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
+  const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
+  const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
+                   (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
+  // ---- coalesced write-out: thread -> (row, 8 columns)
+  constexpr int TPR = BN / 8;                 // threads per row
+  constexpr int RPP = NT / TPR;               // rows per pass
+#pragma unroll
+  for (int p = 0; p < SLAB / RPP; ++p) {
+    const int lr = p * RPP + threadIdx.x / TPR;
+    const int c8 = (threadIdx.x % TPR) * 8;
+    const int row = r0 + lr, col = n0 + c8;
+    if (row >= d.M || col >= d.N) continue;
+    const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
+    if (vec && col + 8 <= d.N) {
+      if (d.residual) {
+        if (r_bf) {
+          const uint4 r = *reinterpret_cast<const uint4*>((const unsigned short*)d.residual + rrow * d.ldr + col);
+          const unsigned rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] += __uint_as_float(rw[q] << 16);
+            v[2 * q + 1] += __uint_as_float(rw[q] & 0xffff0000u);
+          }
+        } else {
+          const float4 r0 = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col);
+          const float4 r1 = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col + 4);
+          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+          v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        }
+      }
+      if (c_bf) {
+        *reinterpret_cast<uint4*>((unsigned short*)d.C + (long)row * d.ldc + col) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+      } else {
+        float* o = (float*)d.C + (long)row * d.ldc + col;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (col + j >= d.N) break;
+        float x = v[j];
+        if (d.residual)
+          x += r_bf ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
+                    : ((const float*)d.residual)[rrow * d.ldr + col + j];
+        const long o = (long)row * d.ldc + col + j;
+        if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
+        else ((float*)d.C)[o] = x;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, bool LN_EPI, int WN, int RM, int RN, int NT, int SLAB>
+__device__ __forceinline__ void gemm_epilogue_staged(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN], int m0, int n0,
+                                                     unsigned char* smem) {
+  static_assert(BN % 8 == 0 && SLAB % 16 == 0 && (BM == SLAB || BM == 2 * SLAB), "shape");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / WN, wc = wid % WN;
+  const int fg = lane >> 4;
+  EpiCols<RN> k;
+#pragma unroll
+  for (int b = 0; b < RN; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4 + j;
+      const bool ok = col < d.N;
+      k.sc[b][j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
+      k.bi[b][j] = (d.bias && ok) ? d.bias[col] : 0.f;
+      k.cs[b][j] = 0.f;
+      if constexpr (LN_EPI) k.cs[b][j] = ok ? d.b_colsum[col] : 0.f;
+    }
+  const int wrow0 = wr * (RM * 16);
+  if constexpr (BM == SLAB) {
+    epi_stage_rows<0, LN_EPI, RM, RN, BN / 4>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);
+    __syncthreads();
+    epi_writeout<BN, NT, SLAB>(d, m0, n0, smem);
+  } else {                                      // two slabs: the waves of rows [0, SLAB) first
+    if (wrow0 < SLAB) epi_stage_rows<0, LN_EPI, RM, RN, BN / 4>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);
+    __syncthreads();
+    epi_writeout<BN, NT, SLAB>(d, m0, n0, smem);
+    __syncthreads();
+    if (wrow0 >= SLAB)
+      epi_stage_rows<0, LN_EPI, RM, RN, BN / 4>(d, acc, k, m0 + wrow0, wrow0 - SLAB, wc * (RN * 16), smem);
+    __syncthreads();
+    epi_writeout<BN, NT, SLAB>(d, m0 + SLAB, n0, smem);
+  }
+}

@@ -38,7 +38,7 @@ __device__ __forceinline__ void glds16_asm(const void* src, unsigned lds_addr) {
 }
 #pragma clang diagnostic pop
 
-template <int BM, int BN, bool CONV, bool TRAIN>
+template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
   constexpr int AI = BM / 32;               // A wave-instructions (8 rows each) per wave
@@ -164,8 +164,13 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 
   // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
   //      LN_EPI: LayerNorm after the product)
-  if (d.a_mean) gemm_epilogue<BM, BN, true, TRAIN>(d, acc, m0, n0);
-  else gemm_epilogue<BM, BN, false, TRAIN>(d, acc, m0, n0);
+  if constexpr (STAGED && !TRAIN) {
+    if (d.a_mean) gemm_epilogue_staged<BM, BN, true, 2, RM, RN, 256, BM>(d, acc, m0, n0, smem);
+    else gemm_epilogue_staged<BM, BN, false, 2, RM, RN, 256, BM>(d, acc, m0, n0, smem);
+  } else {
+    if (d.a_mean) gemm_epilogue<BM, BN, true, TRAIN>(d, acc, m0, n0);
+    else gemm_epilogue<BM, BN, false, TRAIN>(d, acc, m0, n0);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -213,7 +218,7 @@ __device__ __forceinline__ void pp_quadrant(f32x4 (&acc)[8][4], const uint4 (&fa
 #define PP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define PP_SYNC_LDS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-template <bool CONV>
+template <bool CONV, bool STAGED>
 __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   constexpr int BM = 256, BN = 256;
   constexpr int RM = 8, RN = 4;                       // 16x16 sub-tiles per wave (128 x 64)
@@ -390,14 +395,23 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
     if (kt + 1 < nk) ktile(std::integral_constant<int, 1>{}, kt + 1);
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();            // equal barrier counts
-  if (d.a_mean) gemm_epilogue<BM, BN, true, false, 4, RM, RN>(d, acc, m0, n0);
-  else gemm_epilogue<BM, BN, false, false, 4, RM, RN>(d, acc, m0, n0);
+  if constexpr (STAGED) {
+    if (d.a_mean) gemm_epilogue_staged<BM, BN, true, 4, RM, RN, 512, 128>(d, acc, m0, n0, smem);
+    else gemm_epilogue_staged<BM, BN, false, 4, RM, RN, 512, 128>(d, acc, m0, n0, smem);
+  } else {
+    if (d.a_mean) gemm_epilogue<BM, BN, true, false, 4, RM, RN>(d, acc, m0, n0);
+    else gemm_epilogue<BM, BN, false, false, 4, RM, RN>(d, acc, m0, n0);
+  }
 }
+
+int g_staged_epi = 1;             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
 
 int launch256(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
-  if (d.conv_k > 0) gemm_pp256_kernel<true><<<grid, 512, 0, s>>>(d);
-  else gemm_pp256_kernel<false><<<grid, 512, 0, s>>>(d);
+  // fragment-layout epilogue here: the staged one measured 1.3x slower on this kernel (K >= 1024,
+  // where the output stream is a small part of the work)
+  if (d.conv_k > 0) gemm_pp256_kernel<true, false><<<grid, 512, 0, s>>>(d);
+  else gemm_pp256_kernel<false, false><<<grid, 512, 0, s>>>(d);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -406,12 +420,11 @@ template <int BM, int BN>
 int launch(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
   if (d.epi_mode) {
-    if constexpr (BM * BN > 128 * 64) {
-      return HV_EUNSUPPORTED;                   // never selected: the training epilogue uses 64x128
-    } else {
-      if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(d);
-      else gemm_glds_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(d);
-    }
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(d);
+  } else if (g_staged_epi) {
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, true><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, false, true><<<grid, 256, 0, s>>>(d);
   } else {
     if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>(d);
     else gemm_glds_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>(d);
@@ -424,6 +437,9 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_big_tile_mode();   // hv_gemm.hip
 int hv_gemm_small_tile_mode();  // hv_gemm.hip
+int g_train128 = 0;             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
+extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
+extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
@@ -443,6 +459,6 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs
   const long t64x128 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 128);
   if (hv_gemm_small_tile_mode() && t64x128 < 320) return launch<64, 64>(d, s);
-  if (d.M <= 64 || t128 < 256 || d.epi_mode) return launch<64, 128>(d, s);   // 128x128 + training epilogue: acc demoted to scratch, 2x slower
+  if (d.M <= 64 || t128 < 256 || (d.epi_mode && !g_train128)) return launch<64, 128>(d, s);
   return launch<128, 128>(d, s);
 }

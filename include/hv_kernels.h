@@ -115,10 +115,14 @@ typedef struct hv_gemm_desc {
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* path selection for A/B tests: 1 = register-staged kernel only, 0 = default (LDS-DMA when eligible) */
 void hv_gemm_set_path(int regstage_only);
-/* 256x256-tile LDS-DMA kernel selection: 0 off (default), 1 by shape, 2 whenever eligible */
+/* 256x256 ping-pong LDS-DMA kernel selection: 0 off, 1 by shape (default), 2 whenever eligible */
 void hv_gemm_set_big_tile(int mode);
 /* 64x64-tile LDS-DMA kernel for small grids: 1 on (default), 0 off */
 void hv_gemm_set_small_tile(int mode);
+/* 128x128 tiles for the training epilogues (epi_mode 1/2): 0 = 64x128 only (default), 1 on */
+void hv_gemm_set_train128(int on);
+/* LDS-staged coalesced epilogue for the LDS-DMA kernels (inference modes): 1 on (default), 0 off */
+void hv_gemm_set_staged_epilogue(int on);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

@@ -227,15 +227,21 @@ def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
             run = lambda: ops.gemm(a1, b, a2=a2, out_dtype=torch.float32)  # noqa: E731
             ref = af @ bfl.T
     lib = _lib.lib()
+    outs = {}
     try:
-        lib.hv_gemm_set_big_tile(0)
-        base = run()
-        lib.hv_gemm_set_big_tile(2)
-        pp = run()
+        for staged in (1, 0):                   # LDS-staged coalesced epilogue vs fragment-layout stores
+            lib.hv_gemm_set_staged_epilogue(staged)
+            lib.hv_gemm_set_big_tile(0)
+            outs["base", staged] = run()
+            lib.hv_gemm_set_big_tile(2)
+            outs["pp", staged] = run()
     finally:
         lib.hv_gemm_set_big_tile(1)
+        lib.hv_gemm_set_staged_epilogue(1)
     torch.cuda.synchronize()
-    assert torch.equal(pp, base), f"max |diff| {(pp.float() - base.float()).abs().max().item()}"
+    pp, base = outs["pp", 1], outs["base", 0]
+    for key, o in outs.items():
+        assert torch.equal(o, base), f"{key}: max |diff| {(o.float() - base.float()).abs().max().item()}"
     assert rel_err(pp, ref) < (2e-2 if pp.dtype == bf else 1e-4)
 
 

@@ -2,7 +2,7 @@
 the tiny config, and the base-config training step time (forward + YOLOLoss + backward +
 clip + AdamW) at a few batch sizes.
 
-usage: python tools/train_diag.py [grads|time|all] [batch] [size]
+usage: python tools/train_diag.py [grads|time|all] [batch] [size] [train128 0|1]
 """
 import os
 import sys
@@ -54,6 +54,9 @@ if what in ("grads", "all"):
     print("median rel", sorted(r[0] for r in rows)[len(rows) // 2])
 
 if what in ("time", "all"):
+    if len(sys.argv) > 4:                      # A/B knob: 128x128 training-epilogue tiles on/off
+        from hv_amd import _lib
+        _lib.lib().hv_gemm_set_train128(int(sys.argv[4]))
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 640
     torch.manual_seed(0)
