@@ -197,13 +197,16 @@ __global__ void k_maxpool2x2(const T* __restrict__ x, int n, int h, int w, int c
   Elem<T>::store(y, i, v);
 }
 
-// channel sums over pixel chunks: part[n, chunk, c]; block = (64 channels) x 4 pixel lanes
-constexpr int CM_CHUNK = 1024;
+// channel sums over pixel chunks: part[n, chunk, c].  A block covers CM_UNROLL row steps of
+// RPI = 256 / (c / VEC) rows; each thread issues its CM_UNROLL 16-byte row-vector loads before
+// summing them (independent loads in flight instead of one dependent load per step), so the
+// pass runs at the memory rate rather than one load latency per row.
+constexpr int CM_UNROLL = 8;
+__host__ __device__ constexpr int cm_rows_per_chunk(int c, int vec) { return (256 / (c / vec)) * CM_UNROLL; }
+
 template <typename T>
 __global__ void __launch_bounds__(256) k_chan_partial(const T* __restrict__ x, int hw, int c,
                                                       int nchunk, float* part) {
-  // Each thread streams 16-byte row vectors (VEC channels) down a column of rows; a block
-  // covers RPI = 256 / (c / VEC) rows per step, so every wave load is fully coalesced.
   // Requires c % VEC == 0 and c / VEC <= 256 (checked by the launcher).
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float red[256 * VEC];
@@ -214,11 +217,17 @@ __global__ void __launch_bounds__(256) k_chan_partial(const T* __restrict__ x, i
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
   if (r < rpi) {
-    const int p0 = chunk * CM_CHUNK, p1 = min(hw, p0 + CM_CHUNK);
+    const int p0 = chunk * rpi * CM_UNROLL + r;
     const T* base = x + (long)b * hw * c + g * VEC;
-    for (int p = p0 + r; p < p1; p += rpi) {
-      const uint4 v = *reinterpret_cast<const uint4*>(base + (long)p * c);
-      const T* e = reinterpret_cast<const T*>(&v);
+    uint4 v[CM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < CM_UNROLL; ++u) {
+      const int p = p0 + u * rpi;
+      v[u] = p < hw ? *reinterpret_cast<const uint4*>(base + (long)p * c) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < CM_UNROLL; ++u) {
+      const T* e = reinterpret_cast<const T*>(&v[u]);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += Elem<T>::load(e, j);
     }
@@ -234,13 +243,19 @@ __global__ void __launch_bounds__(256) k_chan_partial(const T* __restrict__ x, i
   }
 }
 
-__global__ void k_chan_final(const float* part, int n, int nchunk, int c, float inv, float* out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n * c) return;
-  const int b = i / c, ch = i % c;
+// out[b, ch] = inv * sum_k part[b, k, ch]: block = 64 channels x 4 lanes over the chunks (lane q
+// takes chunks q, q+4, ...), lanes combined in a fixed order (deterministic)
+__global__ void __launch_bounds__(256) k_chan_final(const float* part, int n, int nchunk, int c, float inv,
+                                                    float* out) {
+  __shared__ float red[256];
+  const int b = blockIdx.y, ch = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
   float s = 0.f;
-  for (int k = 0; k < nchunk; ++k) s += part[((long)b * nchunk + k) * c + ch];
-  out[i] = s * inv;
+  if (ch < c)
+    for (int k = q; k < nchunk; k += 4) s += part[((long)b * nchunk + k) * c + ch];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (q == 0 && ch < c)
+    out[(long)b * c + ch] = ((red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192])) * inv;
 }
 
 // SE gate MLP (vision_backbone.py:77-83): one block per image.
@@ -622,8 +637,12 @@ extern "C" int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int 
   return HV_OK;
 }
 
+// sized for the smaller fp32 chunk (vec 4) when that is a valid layout, else for bf16 (vec 8)
 extern "C" size_t hv_channel_mean_work_floats(int n, int hw, int c) {
-  return (size_t)n * ((hw + CM_CHUNK - 1) / CM_CHUNK) * c;
+  if (c <= 0 || hw <= 0 || n <= 0) return 0;
+  const int vec = (c % 4 == 0 && c / 4 <= 256) ? 4 : 8;
+  const int rows = cm_rows_per_chunk(c < vec ? vec : c, vec);
+  return (size_t)n * ((hw + rows - 1) / rows) * c;
 }
 
 extern "C" int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out,
@@ -631,11 +650,12 @@ extern "C" int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, f
   if (n <= 0 || hw <= 0 || c <= 0 || !work) return HV_EINVAL;
   const int vec = dtype == HV_BF16 ? 8 : 4;
   if (c % vec || c / vec > 256 || ((uintptr_t)x & 15)) return HV_EINVAL;
-  const int nchunk = (hw + CM_CHUNK - 1) / CM_CHUNK;
+  const int rows = cm_rows_per_chunk(c, vec);
+  const int nchunk = (hw + rows - 1) / rows;
   hipStream_t s = (hipStream_t)stream;
   HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(nchunk, n), 256, 0, s>>>(
                           (const T*)x, hw, c, nchunk, work)));
-  k_chan_final<<<hv_cdiv((long)n * c, 256), 256, 0, s>>>(work, n, nchunk, c, 1.0f / hw, out);
+  k_chan_final<<<dim3(hv_cdiv(c, 64), n), 256, 0, s>>>(work, n, nchunk, c, 1.0f / hw, out);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
