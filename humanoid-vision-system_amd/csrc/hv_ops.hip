@@ -47,6 +47,163 @@ __global__ void __launch_bounds__(256) k_layernorm(const TX* __restrict__ x, int
   }
 }
 
+// ---- vectorised row kernels: G lanes per row (power of two <= 64), each lane NP vectors of 8
+// elements (one 16-B bf16 load or two 16-B fp32 loads), the row held in registers between the
+// mean and variance passes.  Used when cols % 8 == 0 and the rows are 16-B aligned.
+template <typename T> struct Vec8;
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+template <> struct Vec8<unsigned short> {
+  static __device__ __forceinline__ void load(const unsigned short* p, float (&v)[8]) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const unsigned w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = __uint_as_float(w[q] << 16);
+      v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[8]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                              pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  }
+};
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// mean / rstd of the row held by this lane group (NP x 8 values per lane, `ok` masks the tail)
+template <int G, int NP>
+__device__ __forceinline__ void group_stats(const float (&x)[NP][8], const bool (&ok)[NP], int cols, float eps,
+                                            float& mu, float& rs) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+    if (ok[q])
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[q][j];
+  mu = group_sum<G>(s) / cols;
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+    if (ok[q])
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = x[q][j] - mu; v += d * d; }
+  rs = rsqrtf(group_sum<G>(v) / cols + eps);
+}
+
+template <typename T, int G, int NP>
+__global__ void __launch_bounds__(256) k_row_stats_v(const T* __restrict__ x, long ldx, int rows, int cols,
+                                                     float eps, float* mean, float* rstd) {
+  const int r = blockIdx.x * (256 / G) + threadIdx.x / G, l = threadIdx.x % G;
+  if (r >= rows) return;
+  const T* p = x + (long)r * ldx;
+  float v[NP][8];
+  bool ok[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int c0 = (q * G + l) * 8;
+    ok[q] = c0 < cols;
+    if (ok[q]) Vec8<T>::load(p + c0, v[q]);
+  }
+  float mu, rs;
+  group_stats<G, NP>(v, ok, cols, eps, mu, rs);
+  if (l == 0) { mean[r] = mu; rstd[r] = rs; }
+}
+
+template <typename TX, typename TY, int G, int NP>
+__global__ void __launch_bounds__(256) k_layernorm_v(const TX* __restrict__ x, int rows, int cols, float eps,
+                                                     const float* gamma, const float* beta, TY* y, const void* res,
+                                                     int res_dt) {
+  const int r = blockIdx.x * (256 / G) + threadIdx.x / G, l = threadIdx.x % G;
+  if (r >= rows) return;
+  const TX* p = x + (long)r * cols;
+  float v[NP][8];
+  bool ok[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int c0 = (q * G + l) * 8;
+    ok[q] = c0 < cols;
+    if (ok[q]) Vec8<TX>::load(p + c0, v[q]);
+  }
+  float mu, rs;
+  group_stats<G, NP>(v, ok, cols, eps, mu, rs);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    if (!ok[q]) continue;
+    const int c0 = (q * G + l) * 8;
+    float o[8], g[8], b[8], rv[8];
+    if (gamma) { Vec8<float>::load(gamma + c0, g); Vec8<float>::load(beta + c0, b); }
+    if (res) {
+      if (res_dt == HV_BF16) Vec8<unsigned short>::load((const unsigned short*)res + (long)r * cols + c0, rv);
+      else Vec8<float>::load((const float*)res + (long)r * cols + c0, rv);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (v[q][j] - mu) * rs;
+      if (gamma) o[j] = o[j] * g[j] + b[j];
+      if (res) o[j] += rv[j];
+    }
+    Vec8<TY>::store(y + (long)r * cols + c0, o);
+  }
+}
+
+// (G, NP) for a row of `cols` (cols % 8 == 0, cols <= 4096)
+static inline void row_shape(int cols, int& G, int& NP) {
+  const int nv = cols / 8;
+  G = 8;
+  while (G < nv && G < 64) G <<= 1;
+  NP = 1;
+  while (NP * G < nv) NP <<= 1;
+}
+
+#define HV_ROW_SHAPES(G, NP, CALL)                                                     \
+  switch (G * 16 + NP) {                                                               \
+    case 8 * 16 + 1: { constexpr int G_ = 8, NP_ = 1; CALL; } break;                   \
+    case 16 * 16 + 1: { constexpr int G_ = 16, NP_ = 1; CALL; } break;                 \
+    case 32 * 16 + 1: { constexpr int G_ = 32, NP_ = 1; CALL; } break;                 \
+    case 64 * 16 + 1: { constexpr int G_ = 64, NP_ = 1; CALL; } break;                 \
+    case 64 * 16 + 2: { constexpr int G_ = 64, NP_ = 2; CALL; } break;                 \
+    case 64 * 16 + 4: { constexpr int G_ = 64, NP_ = 4; CALL; } break;                 \
+    case 64 * 16 + 8: { constexpr int G_ = 64, NP_ = 8; CALL; } break;                 \
+    default: return HV_EUNSUPPORTED;                                                   \
+  }
+
+// out = x * gate[b, c] (+ identity), 8 channels per thread (c % 8 == 0, 16-B aligned)
+template <typename T>
+__global__ void k_scale_residual_v(const T* __restrict__ x, const float* gate, const T* identity, int hw, int c,
+                                   long total8, T* y) {
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i8 >= total8) return;
+  const long i = i8 * 8;
+  const int ch = i % c;
+  const long b = i / ((long)hw * c);
+  float v[8], g[8];
+  Vec8<T>::load(x + i, v);
+  Vec8<float>::load(gate + b * c + ch, g);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= g[j];
+  if (identity) {
+    float r[8];
+    Vec8<T>::load(identity + i, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += r[j];
+  }
+  Vec8<T>::store(y + i, v);
+}
+
 // RMSNorm (manifold_layers.py:449-456): x / sqrt(mean(x^2) + eps) * scale
 template <typename T>
 __global__ void __launch_bounds__(256) k_rmsnorm(const T* __restrict__ x, int rows, int cols,
@@ -558,8 +715,16 @@ __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logit
 extern "C" int hv_row_stats(int dtype, const void* x, long ldx, int rows, int cols, float eps,
                             float* mean, float* rstd, hv_stream_t stream) {
   if (rows <= 0 || cols <= 0) return HV_EINVAL;
-  HV_DISPATCH(dtype, (k_row_stats<T><<<hv_cdiv(rows, 4), 256, 0, (hipStream_t)stream>>>(
-                          (const T*)x, ldx, rows, cols, eps, mean, rstd)));
+  hipStream_t s = (hipStream_t)stream;
+  if (cols % 8 == 0 && cols <= 4096 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0) {
+    int G, NP;
+    row_shape(cols, G, NP);
+    HV_ROW_SHAPES(G, NP, HV_DISPATCH(dtype, (k_row_stats_v<T, G_, NP_><<<hv_cdiv(rows, 256 / G_), 256, 0, s>>>(
+                                                (const T*)x, ldx, rows, cols, eps, mean, rstd))));
+  } else {
+    HV_DISPATCH(dtype, (k_row_stats<T><<<hv_cdiv(rows, 4), 256, 0, s>>>((const T*)x, ldx, rows, cols, eps, mean,
+                                                                          rstd)));
+  }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -568,8 +733,25 @@ extern "C" int hv_layernorm(int x_dtype, const void* x, int rows, int cols, floa
                             const float* gamma, const float* beta, int y_dtype, void* y,
                             const void* res_out, int res_dtype, hv_stream_t stream) {
   if (rows <= 0 || cols <= 0) return HV_EINVAL;
-  const dim3 g(hv_cdiv(rows, 4));
   hipStream_t s = (hipStream_t)stream;
+  if (cols % 8 == 0 && cols <= 4096 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+      ((uintptr_t)res_out & 15) == 0 && ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0 &&
+      (x_dtype == HV_F32 || x_dtype == HV_BF16) && (y_dtype == HV_F32 || y_dtype == HV_BF16)) {
+    int G, NP;
+    row_shape(cols, G, NP);
+    const unsigned grid = hv_cdiv(rows, 256 / G);
+#define HV_LN_V(TX, TY)                                                                                  \
+  HV_ROW_SHAPES(G, NP, (k_layernorm_v<TX, TY, G_, NP_><<<grid, 256, 0, s>>>((const TX*)x, rows, cols, eps, \
+                                                                            gamma, beta, (TY*)y, res_out, res_dtype)))
+    if (x_dtype == HV_F32 && y_dtype == HV_F32) { HV_LN_V(float, float); }
+    else if (x_dtype == HV_F32) { HV_LN_V(float, bf); }
+    else if (y_dtype == HV_BF16) { HV_LN_V(bf, bf); }
+    else { HV_LN_V(bf, float); }
+#undef HV_LN_V
+    HV_CHECK_LAUNCH();
+    return HV_OK;
+  }
+  const dim3 g(hv_cdiv(rows, 4));
   if (x_dtype == HV_F32 && y_dtype == HV_F32)
     k_layernorm<float, float><<<g, 256, 0, s>>>((const float*)x, rows, cols, eps, gamma, beta, (float*)y, res_out, res_dtype);
   else if (x_dtype == HV_F32 && y_dtype == HV_BF16)
@@ -672,8 +854,13 @@ extern "C" int hv_scale_residual(int dtype, const void* x, const float* gate, co
                                  int n, int hw, int c, void* y, hv_stream_t stream) {
   const long total = (long)n * hw * c;
   if (total <= 0) return HV_EINVAL;
-  HV_DISPATCH(dtype, (k_scale_residual<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
-                          (const T*)x, gate, (const T*)identity, hw, c, total, (T*)y)));
+  if (c % 8 == 0 && (((uintptr_t)x | (uintptr_t)identity | (uintptr_t)y | (uintptr_t)gate) & 15) == 0) {
+    HV_DISPATCH(dtype, (k_scale_residual_v<T><<<hv_cdiv(total / 8, 256), 256, 0, (hipStream_t)stream>>>(
+                            (const T*)x, gate, (const T*)identity, hw, c, total / 8, (T*)y)));
+  } else {
+    HV_DISPATCH(dtype, (k_scale_residual<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
+                            (const T*)x, gate, (const T*)identity, hw, c, total, (T*)y)));
+  }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
