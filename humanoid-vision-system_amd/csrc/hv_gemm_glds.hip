@@ -38,13 +38,14 @@ __device__ __forceinline__ void glds16_asm(const void* src, unsigned lds_addr) {
 }
 #pragma clang diagnostic pop
 
-template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false>
+template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
+  static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
   constexpr int AI = BM / 32;               // A wave-instructions (8 rows each) per wave
   constexpr int BI = BN / 32;
   constexpr int RM = BM / 32, RN = BN / 32;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -92,9 +93,13 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   }
   const int lchunk = pchunk ^ (lrow & 7);   // logical chunk fetched by this lane (rows 8-aligned)
 
+  // DMA of K-tile kt into ring buffer buf (inline asm: the compiler does not track it, so it does
+  // not drain vmcnt before the ds_reads of the other buffers; the loop waits with counted vmcnt)
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
   auto stage = [&](int buf, int kt) {
-    unsigned char* sa = smem + buf * STAGE_BYTES;
-    unsigned char* sb = sa + BM * ROW;
+    const unsigned la = lds0 + buf * STAGE_BYTES + wu * AI * 1024;
+    const unsigned lb = lds0 + buf * STAGE_BYTES + BM * ROW + wu * BI * 1024;
     const int k = kt * 64 + lchunk * 8;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
@@ -114,10 +119,10 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
           src = arow[i] + k;
         }
       }
-      glds16(src, sa + (wid * AI + i) * 1024);
+      glds16_asm(src, la + i * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(brow[i] + k, sb + (wid * BI + i) * 1024);
+    for (int i = 0; i < BI; ++i) glds16_asm(brow[i] + k, lb + i * 1024);
   };
 
   f32x4 acc[RM][RN];
@@ -127,15 +132,31 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
     for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = d.K / 64;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  constexpr int DPT = AI + BI;              // DMA instructions per wave per K-tile
+  // ring of NS buffers, NS-1 K-tiles in flight.  Iteration kt: wait for this wave's DMAs of tile
+  // kt (the younger tiles stay in flight), barrier (every wave's tile kt landed, every wave's
+  // reads of tile kt-1 retired), refill the buffer of tile kt-1 with tile kt+NS-1, compute kt.
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) stage(t, t);
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
-    const unsigned char* sa = smem + buf * STAGE_BYTES;
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if constexpr (NS == 4) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kt + NS - 1);
+    const unsigned char* sa = smem + (kt % NS) * STAGE_BYTES;
     const unsigned char* sb = sa + BM * ROW;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -158,9 +179,10 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[b]),
                                                               __builtin_bit_cast(bf16x8, fa[a]), acc[a][b], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  // every wave's last reads retired before the (staged) epilogue reuses the LDS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
   //      LN_EPI: LayerNorm after the product)
@@ -416,21 +438,36 @@ int launch256(const hv_gemm_desc& d, hipStream_t s) {
   return HV_OK;
 }
 
+// ring depth per tile: the small tiles have short K-steps that cannot cover the DMA latency
+// with one tile in flight (64x64: 4 buffers = 64 KiB, 64x128 / 128x64: 3 = 72 KiB)
 template <int BM, int BN>
-int launch(const hv_gemm_desc& d, hipStream_t s) {
+constexpr int deep_stages() { return BM * BN <= 64 * 64 ? 4 : (BM * BN <= 128 * 64 ? 3 : 2); }
+int g_deep = 1;                   // deeper LDS-DMA rings for the small tiles (A/B knob)
+
+template <int BM, int BN, int NS>
+int launch_ns(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
   if (d.epi_mode) {
-    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(d);
-    else gemm_glds_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(d);
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, false, NS><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, true, false, NS><<<grid, 256, 0, s>>>(d);
   } else if (g_staged_epi) {
-    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, true><<<grid, 256, 0, s>>>(d);
-    else gemm_glds_kernel<BM, BN, false, false, true><<<grid, 256, 0, s>>>(d);
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, true, NS><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, false, true, NS><<<grid, 256, 0, s>>>(d);
   } else {
-    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>(d);
-    else gemm_glds_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>(d);
+    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, false, NS><<<grid, 256, 0, s>>>(d);
+    else gemm_glds_kernel<BM, BN, false, false, false, NS><<<grid, 256, 0, s>>>(d);
   }
   HV_CHECK_LAUNCH();
   return HV_OK;
+}
+
+template <int BM, int BN>
+int launch(const hv_gemm_desc& d, hipStream_t s) {
+  constexpr int NS = deep_stages<BM, BN>();
+  if constexpr (NS > 2) {
+    if (g_deep) return launch_ns<BM, BN, NS>(d, s);
+  }
+  return launch_ns<BM, BN, 2>(d, s);
 }
 
 }  // namespace
@@ -440,6 +477,7 @@ int hv_gemm_small_tile_mode();  // hv_gemm.hip
 int g_train128 = 0;             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
+extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {

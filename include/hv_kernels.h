@@ -123,6 +123,8 @@ void hv_gemm_set_small_tile(int mode);
 void hv_gemm_set_train128(int on);
 /* LDS-staged coalesced epilogue for the LDS-DMA kernels (inference modes): 1 on (default), 0 off */
 void hv_gemm_set_staged_epilogue(int on);
+/* deeper LDS-DMA rings (4 / 3 buffers) for the 64x64 / 64x128 / 128x64 tiles: 1 on (default), 0 = 2 */
+void hv_gemm_set_deep_ring(int on);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

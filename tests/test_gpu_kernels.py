@@ -231,15 +231,18 @@ def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
     try:
         for staged in (1, 0):                   # LDS-staged coalesced epilogue vs fragment-layout stores
             lib.hv_gemm_set_staged_epilogue(staged)
-            lib.hv_gemm_set_big_tile(0)
-            outs["base", staged] = run()
+            for deep in (1, 0):                 # 3/4-buffer LDS-DMA rings vs 2 buffers
+                lib.hv_gemm_set_deep_ring(deep)
+                lib.hv_gemm_set_big_tile(0)
+                outs["base", staged, deep] = run()
             lib.hv_gemm_set_big_tile(2)
             outs["pp", staged] = run()
     finally:
         lib.hv_gemm_set_big_tile(1)
         lib.hv_gemm_set_staged_epilogue(1)
+        lib.hv_gemm_set_deep_ring(1)
     torch.cuda.synchronize()
-    pp, base = outs["pp", 1], outs["base", 0]
+    pp, base = outs["pp", 1], outs["base", 0, 0]
     for key, o in outs.items():
         assert torch.equal(o, base), f"{key}: max |diff| {(o.float() - base.float()).abs().max().item()}"
     assert rel_err(pp, ref) < (2e-2 if pp.dtype == bf else 1e-4)

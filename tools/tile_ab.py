@@ -1,5 +1,5 @@
 """A/B of GEMM tile rules (HIP events): `small` = 64x64 small-grid tiles on/off; `big` = the
-256x256 ping-pong kernel off / forced."""
+256x256 ping-pong kernel off / forced; `deep` = 2-buffer vs deeper LDS-DMA rings."""
 import os
 import sys
 
@@ -25,11 +25,12 @@ def timeit(fn, iters=30, warm=5):
 
 
 which = sys.argv[1] if len(sys.argv) > 1 else "small"
-setter = lib.hv_gemm_set_small_tile if which == "small" else lib.hv_gemm_set_big_tile
-modes = (0, 1) if which == "small" else (0, 2)
+setter = {"small": lib.hv_gemm_set_small_tile, "big": lib.hv_gemm_set_big_tile,
+          "deep": lib.hv_gemm_set_deep_ring}[which]
+modes = (0, 2) if which == "big" else (0, 1)
 default = 1
 shapes = ([(6416, 256, 768), (6416, 1024, 256), (6416, 512, 1024), (6416, 256, 1024), (6400, 256, 2304),
-           (1600, 512, 1024), (6400, 1024, 512), (25600, 256, 1280)] if which == "small" else
+           (1600, 512, 1024), (6400, 1024, 512), (25600, 256, 1280)] if which in ("small", "deep") else
           [(25600, 1024, 2048), (6400, 2048, 4096), (102400, 512, 1024), (25600, 2048, 256), (102400, 1024, 256),
            (6400, 4096, 512), (25600, 512, 1536), (8192, 8192, 8192), (4096, 4096, 4096), (1000, 520, 640)])
 for M, N, K in shapes:
