@@ -488,10 +488,12 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   if (d.ldb % 8) return HV_EUNSUPPORTED;
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   const long t256 = (long)hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
-  // 256x256 ping-pong kernel: long contractions on grids that still fill most CUs (measured:
-  // K = 256 loses to the 128x128 tile -- prologue-bound; K = 512 ties; K >= 1024 wins 10-45 %)
+  // 256x256 ping-pong kernel: long contractions with wide outputs on grids that still fill most
+  // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
+  // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for
+  // the implicit-im2col convolutions (+3..29 %); K = 256 loses everywhere (prologue-bound)
   if (!d.epi_mode && (hv_gemm_big_tile_mode() == 2 ||
-                      (hv_gemm_big_tile_mode() == 1 && d.K >= 1024 && t256 >= 160)))
+                      (hv_gemm_big_tile_mode() == 1 && d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
   // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs
