@@ -201,14 +201,17 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // register double buffering: the next k-step's global loads are issued before this step's
+  // MFMAs, so their latency overlaps the compute instead of stalling every k-step
+  float4 na0 = *reinterpret_cast<const float4*>(Ar);
+  float4 na1 = *reinterpret_cast<const float4*>(Ar + 4);
+  float4 nb0 = make_float4(0.f, 0.f, 0.f, 0.f), nb1 = nb0;
+  if (bvalid) {
+    nb0 = *reinterpret_cast<const float4*>(Br);
+    nb1 = *reinterpret_cast<const float4*>(Br + 4);
+  }
   for (int k0 = 0; k0 < K; k0 += 32) {
-    const float4 a0 = *reinterpret_cast<const float4*>(Ar + k0);
-    const float4 a1 = *reinterpret_cast<const float4*>(Ar + k0 + 4);
-    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
-    if (bvalid) {
-      b0 = *reinterpret_cast<const float4*>(Br + k0);
-      b1 = *reinterpret_cast<const float4*>(Br + k0 + 4);
-    }
+    const float4 a0 = na0, a1 = na1, b0 = nb0, b1 = nb1;
     __syncthreads();
     if constexpr (BF) {
       const u16x8 pa = {f2bf(a0.x), f2bf(a0.y), f2bf(a0.z), f2bf(a0.w), f2bf(a1.x), f2bf(a1.y), f2bf(a1.z), f2bf(a1.w)};
@@ -222,6 +225,14 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
       *reinterpret_cast<float4*>(Bs + lr * RB + lq * 4 + 16) = b1;
     }
     __syncthreads();
+    if (k0 + 32 < K) {
+      na0 = *reinterpret_cast<const float4*>(Ar + k0 + 32);
+      na1 = *reinterpret_cast<const float4*>(Ar + k0 + 36);
+      if (bvalid) {
+        nb0 = *reinterpret_cast<const float4*>(Br + k0 + 32);
+        nb1 = *reinterpret_cast<const float4*>(Br + k0 + 36);
+      }
+    }
     const int fr = lane & 15, fg = lane >> 4;
     if constexpr (BF) {
       uint4 fa[2], fb[2];
