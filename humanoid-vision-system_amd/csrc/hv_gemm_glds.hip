@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
         const int tap = k / d.conv_c, ci = k - tap * d.conv_c;
         const int kh = tap / d.conv_k, kw = tap - kh * d.conv_k;
         const int ih = aih[i] + kh, iw = aiw[i] + kw;
-        src = ((unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
+        src = (k < d.K && (unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
                   ? (const void*)(arow[i] + ((long)ih * d.conv_w + iw) * d.conv_c + ci)
                   : (const void*)hv_glds_zero_line;
       } else {
@@ -122,7 +122,11 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
       glds16_asm(src, la + i * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16_asm(brow[i] + k, lb + i * 1024);
+    for (int i = 0; i < BI; ++i) {
+      const void* src = brow[i] + k;
+      if constexpr (CONV) src = k < d.K ? src : (const void*)hv_glds_zero_line;   // K tail of the padded conv
+      glds16_asm(src, lb + i * 1024);
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 #pragma unroll
     for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = d.K / 64;
+  const int nk = (d.K + 63) / 64;          // conv: K % 64 != 0 allowed, the tail reads zeros
   constexpr int DPT = AI + BI;              // DMA instructions per wave per K-tile
   // ring of NS buffers, NS-1 K-tiles in flight.  Iteration kt: wait for this wave's DMAs of tile
   // kt (the younger tiles stay in flight), barrier (every wave's tile kt landed, every wave's
@@ -480,10 +484,15 @@ int g_train128 = 0;             // 128x128 tiles for the training epilogues: mea
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
 extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
+int g_conv_ktail = 0;            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
+extern "C" void hv_gemm_set_conv_ktail(int on) { g_conv_ktail = on; }
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
-  if (d.dtype != HV_BF16 || d.K % 64 || d.conv_transposed) return HV_EUNSUPPORTED;
+  // K % 64 != 0 only for convolutions (channels a multiple of 8): the last K-tile's tail reads the
+  // zero line for both operands (e.g. 3x3 convs with 32 input channels, K = 288)
+  if (d.dtype != HV_BF16 || d.conv_transposed) return HV_EUNSUPPORTED;
+  if (d.K % 64 && !(g_conv_ktail && d.conv_k > 0 && d.K % 8 == 0)) return HV_EUNSUPPORTED;
   if (d.a_mean && (!d.b_colsum || d.A2 || d.conv_k > 0)) return HV_EUNSUPPORTED;
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
@@ -494,7 +503,7 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
   // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for
   // the implicit-im2col convolutions (+3..29 %); K = 256 loses everywhere (prologue-bound)
-  if (!d.epi_mode && (hv_gemm_big_tile_mode() == 2 ||
+  if (!d.epi_mode && d.K % 64 == 0 && (hv_gemm_big_tile_mode() == 2 ||
                       (hv_gemm_big_tile_mode() == 1 && d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);

@@ -125,6 +125,8 @@ void hv_gemm_set_train128(int on);
 void hv_gemm_set_staged_epilogue(int on);
 /* deeper LDS-DMA rings (4 / 3 buffers) for the 64x64 / 64x128 / 128x64 tiles: 1 on (default), 0 = 2 */
 void hv_gemm_set_deep_ring(int on);
+/* convolutions with K % 64 != 0 (channels % 8 == 0) on the LDS-DMA kernel: 0 off (default), 1 on */
+void hv_gemm_set_conv_ktail(int on);
 
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

@@ -248,6 +248,31 @@ def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
     assert rel_err(pp, ref) < (2e-2 if pp.dtype == bf else 1e-4)
 
 
+@pytest.mark.parametrize("cin,cout,s,hw", [(32, 64, 1, 40), (32, 32, 2, 33), (16, 8, 1, 9), (40, 24, 1, 15)])
+def test_conv_ktail_lds_dma_vs_register_path(gpu_device, cin, cout, s, hw):
+    """3x3 convs with K = 9*cin not a multiple of 64 on the LDS-DMA kernel (zero-line K tail)
+    against the register-staged kernel and torch."""
+    ops = _ops()
+    from hv_amd import _lib
+    g = torch.Generator().manual_seed(cin * 100 + cout + hw)
+    x = torch.randn(2, hw, hw, cin, generator=g).to(torch.bfloat16).to(gpu_device)
+    w = (torch.randn(cout, 9 * cin, generator=g) / (9 * cin) ** 0.5).to(torch.bfloat16).to(gpu_device)
+    bias = torch.randn(cout, generator=g).to(gpu_device)
+    run = lambda: ops.conv2d(x, w, 3, s, 1, bias=bias, act="silu", out_dtype=torch.float32)  # noqa: E731
+    lib = _lib.lib()
+    try:
+        lib.hv_gemm_set_conv_ktail(1)
+        fast = run()
+        lib.hv_gemm_set_conv_ktail(0)
+        slow = run()
+    finally:
+        lib.hv_gemm_set_conv_ktail(0)
+    ref = F.silu(F.conv2d(x.float().cpu().permute(0, 3, 1, 2), w.float().cpu().view(cout, 3, 3, cin).permute(0, 3, 1, 2),
+                          bias.cpu(), s, 1)).permute(0, 2, 3, 1)
+    assert rel_err(fast, slow) < 1e-5
+    assert rel_err(fast, ref) < 1e-4
+
+
 CONV_CASES = [(3, 32, 3, 2, 1, 33), (32, 32, 3, 1, 1, 20), (32, 64, 3, 2, 1, 17), (64, 32, 1, 1, 0, 9),
               (128, 96, 3, 1, 1, 7), (16, 8, 3, 1, 1, 5)]
 
