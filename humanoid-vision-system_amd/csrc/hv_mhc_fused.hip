@@ -38,9 +38,9 @@ __device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_b
 #endif
 }
 
-template <int D, int HD, int TB_>
+template <int D, int HD, int TB_, int NW_ = 8>
 struct Cfg {
-  static constexpr int NW = 8, NT = 512;
+  static constexpr int NW = NW_, NT = 64 * NW_;
   static constexpr int TB = TB_;                   // 16-token blocks per wave (acc2: HT*TB tiles)
   static constexpr int TPW = 16 * TB, BM = NW * TPW;
   static constexpr int KC = 32, NCH = 2 * HD / KC;
@@ -63,8 +63,8 @@ __device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); 
 template <int CPA>
 __device__ __forceinline__ int swzA(int r, int c) { return c ^ (r & (CPA - 1)); }
 
-template <int D, int HD, int TB_, int MINB>
-__global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
+template <int D, int HD, int TB_, int MINB, int NW_ = 8>
+__global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_kernel(
     const unsigned short* __restrict__ x, int T,
     const unsigned short* __restrict__ a1t,   // [2HD, D]
     const float* __restrict__ c1,             // [2HD]
@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
     const float* __restrict__ g_post, const float* __restrict__ b_post,
     const unsigned short* __restrict__ res,   // optional [T, D], added after LN_post
     unsigned short* __restrict__ out) {
-  using C = Cfg<D, HD, TB_>;
+  using C = Cfg<D, HD, TB_, NW_>;
   constexpr int TB = C::TB, KC = C::KC;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
     unsigned char* sa = smem + st * C::STAGE;
     unsigned char* sw = sa + C::A1B;
 #pragma unroll
-    for (int p0 = 0; p0 < KC * C::CPA; p0 += 512) {
+    for (int p0 = 0; p0 < KC * C::CPA; p0 += C::NT) {
       const int p = p0 + tid;
       if (p0 + (tid & ~63) < KC * C::CPA) {                   // wave-uniform
         const int r = p / C::CPA, pc = p % C::CPA;
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
       }
     }
 #pragma unroll
-    for (int p0 = 0; p0 < HD * 4; p0 += 512) {
+    for (int p0 = 0; p0 < HD * 4; p0 += C::NT) {
       const int p = p0 + tid;
       if (p0 + (tid & ~63) < HD * 4) {
         const int r = p >> 2, pc = p & 3;
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
   auto issue_wc = [&](int ks, int st) {
     unsigned char* sb = smem + st * C::WCB;
 #pragma unroll
-    for (int p0 = 0; p0 < D * 4; p0 += 512) {
+    for (int p0 = 0; p0 < D * 4; p0 += C::NT) {
       const int p = p0 + tid;
       if (p0 + (tid & ~63) < D * 4) {
         const int r = p >> 2, pc = p & 3;
@@ -302,10 +302,10 @@ __global__ void __launch_bounds__(512, MINB) mhc_fused_kernel(
   }
 }
 
-template <int D, int HD, int TB, int MINB>
+template <int D, int HD, int TB, int MINB, int NW = 8>
 int launch(const hv_mhc_fused_args* a, hipStream_t s) {
-  using C = Cfg<D, HD, TB>;
-  auto k = mhc_fused_kernel<D, HD, TB, MINB>;
+  using C = Cfg<D, HD, TB, NW>;
+  auto k = mhc_fused_kernel<D, HD, TB, MINB, NW>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -341,15 +341,23 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
                        (uintptr_t)a->b_post | (uintptr_t)a->residual;
   if (al & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  // measured (tools/mhc_variants.py): more tokens per wave wins while acc2 fits in registers
+  // measured (tools/mhc_variants.py): more tokens per wave wins while acc2 fits in registers;
+  // (tools/mhc_ab.py) 4-wave workgroups, two per CU, beat one 8-wave workgroup by 16-20% at
+  // every D (the two groups' chunk barriers no longer coincide, so one group's MFMAs cover the
+  // other's DMA wait + barrier).  Variant 1 = 2-wave groups, 2 = the 8-wave groups.
   if (a->D == 32) {
-    if (g_variant == 1) return launch<32, 128, 2, 1>(a, s);
-    return launch<32, 128, 4, 1>(a, s);
+    if (g_variant == 1) return launch<32, 128, 4, 4, 2>(a, s);
+    if (g_variant == 2) return launch<32, 128, 4, 1>(a, s);
+    return launch<32, 128, 4, 2, 4>(a, s);
   }
   if (a->D == 64) {
-    if (g_variant == 1) return launch<64, 256, 1, 1>(a, s);
-    return launch<64, 256, 2, 1>(a, s);
+    if (g_variant == 1) return launch<64, 256, 2, 4, 2>(a, s);
+    if (g_variant == 2) return launch<64, 256, 2, 1>(a, s);
+    return launch<64, 256, 2, 2, 4>(a, s);
   }
-  if (a->D == 128) return launch<128, 512, 1, 1>(a, s);
+  if (a->D == 128) {
+    if (g_variant == 2) return launch<128, 512, 1, 1>(a, s);
+    return launch<128, 512, 1, 2, 4>(a, s);
+  }
   return launch<256, 512, 1, 1>(a, s);
 }

@@ -210,3 +210,26 @@ def test_model_deterministic_and_frozen_cache(gpu_device):
     b = m(x)["predictions"]["scale_2"].clone()
     c = m(x)["predictions"]["scale_2"].clone()
     assert torch.equal(a, b) and torch.equal(b, c)
+
+
+@pytest.mark.parametrize("D,T", [(32, 1000), (64, 777), (128, 300)])
+def test_mhc_fused_workgroup_shapes_bitwise_equal(gpu_device, D, T):
+    """The 4-wave (default) and 8-wave workgroup shapes of hv_mhc_fused give identical bits:
+    every wave computes its own tokens end to end, only the barrier grouping differs."""
+    import ctypes
+    from hv_amd import ManifoldHyperConnection, _lib
+    from hv_amd.runtime import RunCtx, use_ctx
+    lib = _lib.lib()
+    lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
+    m = ManifoldHyperConnection(D, expansion_rate=4, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    x = torch.randn(T, D, generator=torch.Generator().manual_seed(T)).to(torch.bfloat16).to(gpu_device)
+    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
+        try:
+            lib.hv_mhc_fused_set_variant(2)
+            y8 = m.forward_tokens(x).cpu()
+        finally:
+            lib.hv_mhc_fused_set_variant(0)
+        y4 = m.forward_tokens(x).cpu()
+    assert torch.equal(y4, y8)

@@ -1,0 +1,52 @@
+"""A/B the fused mHC kernel variants against the unfused GEMM chain at in-model shapes (B=16)."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
+import torch  # noqa: E402
+from hv_amd import ManifoldHyperConnection, _lib  # noqa: E402
+from hv_amd import manifold as MF  # noqa: E402
+
+lib = _lib.lib()
+lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
+shapes = [(int(a), int(b)) for a, b in (s.split(":") for s in sys.argv[1:])] or \
+    [(32, 1638400), (64, 409600), (128, 102400), (128, 25600)]
+
+
+def timed(fn, n=5):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+for D, T in shapes:
+    m = ManifoldHyperConnection(D, expansion_rate=4).cuda().eval()
+    x = torch.randn(T, D, device="cuda").to(torch.bfloat16)
+    p = m.plan()
+    Hd = 4 * D
+    fl = 2.0 * T * (D * 2 * Hd + 2 * Hd * Hd + (Hd + D) * D)
+    cases = {"unfused": (False, 0), "fused_v0": (True, 0), "fused_v1": (True, 1), "fused_v2": (True, 2)}
+    res = {k: [] for k in cases}
+    with torch.no_grad():
+        MF.USE_FUSED = False
+        ref = MF.mhc_apply(x, p).float()
+        for rep in range(5):
+            for k, (fu, v) in cases.items():
+                MF.USE_FUSED = fu
+                lib.hv_mhc_fused_set_variant(v)
+                if rep == 0:
+                    y = MF.mhc_apply(x, p).float()
+                    print(f"D={D} T={T} {k}: rel err vs unfused {((y - ref).norm() / ref.norm()).item():.2e}", flush=True)
+                res[k].append(timed(lambda: MF.mhc_apply(x, p)))
+    MF.USE_FUSED = True
+    lib.hv_mhc_fused_set_variant(0)
+    for k, ts in res.items():
+        t = sorted(ts)[len(ts) // 2]
+        print(f"mhc D={D:4d} T={T:8d} {k:9s}: {t:.3f} ms {fl / t / 1e9:7.1f} TF/s", flush=True)
