@@ -359,5 +359,8 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
     if (g_variant == 2) return launch<128, 512, 1, 1>(a, s);
     return launch<128, 512, 1, 2, 4>(a, s);
   }
+  // D=256 (ViT, off by default): at T=6416 / 25600 the unfused chain wins (65 / 150 us vs
+  // 94 / 139 us fused, tools/mhc_ab.py); 8-wave groups here, variant 1 = 4-wave
+  if (g_variant == 1) return launch<256, 512, 1, 1, 4>(a, s);
   return launch<256, 512, 1, 1>(a, s);
 }

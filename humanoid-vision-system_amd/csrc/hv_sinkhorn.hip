@@ -50,6 +50,20 @@ __device__ __forceinline__ int find_entry(const hv_sinkhorn_entry* t, int count,
   return lo;
 }
 
+// Fixed-order sum of nrb row-block partials of one column (stride m): eight independent
+// accumulators keep eight loads in flight, so the largest matrix (n = 1792: 112 partials)
+// no longer serialises ~100 dependent L2/MALL round trips on the few waves that own it.
+__device__ __forceinline__ float sum_partials(const float* __restrict__ part, int nrb, long m) {
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int r = 0;
+  for (; r + 8 <= nrb; r += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] += part[(long)(r + k) * m];
+  }
+  for (int k = 0; r < nrb; ++r, ++k) s[k] += part[(long)r * m];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
 // K = softmax(raw / tau, -1) * m (manifold_layers.py:56-57); a_0 = b_0 = 1.
 __global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restrict__ tab,
                                                int count, int total_rows) {
@@ -151,8 +165,7 @@ __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restri
   const int bidx = c / e.m, j = c % e.m;
   const int nrb = (e.n + RB - 1) / RB;
   const float* part = w.part + (long)bidx * nrb * e.m + j;
-  float s = 0.f;
-  for (int r = 0; r < nrb; ++r) s += part[(long)r * e.m];
+  const float s = sum_partials(part, nrb, e.m);
   const long bm = (long)e.batch * e.m;
   const float b = w.b[(long)t * bm + c];
   const float cs = b * s;
@@ -175,8 +188,8 @@ __global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restr
   const float* bT = w.b + (long)e.iters * bm + (long)bidx * e.m;
   float* M = e.out + (long)row * e.m;
   for (int j = lane; j < e.m; j += 64) M[j] = ai * M[j] * bT[j];
-  if (row == 0 && e.history) {             // first row's wave reduces the history
-    for (int t = 0; t < e.iters; ++t) {
+  if (e.history) {                         // history[t] reduced by the wave of row t (row 0 used
+    for (int t = row; t < e.iters; t += (int)bn) {   // to do all of them: a ~160 us serial tail)
       const float* rt = w.r + (long)t * bn;
       float s = 0.f;
       for (long i = lane; i < bn; i += 64) s += rt[i];
@@ -315,7 +328,7 @@ __global__ void __launch_bounds__(256) skb_cols(const hv_sinkhorn_bwd_entry* __r
   const int nrb = (e.fwd.n + RB - 1) / RB;
   const float* part = w.part + (long)bidx * nrb * e.fwd.m + j;
   float s = 0.f;
-  for (int r = 0; r < nrb; ++r) s += part[(long)r * e.fwd.m];
+  s += sum_partials(part, nrb, e.fwd.m);
   const long bm = (long)e.fwd.batch * e.fwd.m;
   w.s[c] = fw.b[(long)(t + 1) * bm + c] * s;
 }

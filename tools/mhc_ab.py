@@ -11,8 +11,10 @@ from hv_amd import manifold as MF  # noqa: E402
 
 lib = _lib.lib()
 lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
-shapes = [(int(a), int(b)) for a, b in (s.split(":") for s in sys.argv[1:])] or \
+# argv: D:T[:expansion] ...
+shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[1:]] or \
     [(32, 1638400), (64, 409600), (128, 102400), (128, 25600)]
+lib.hv_mhc_fused_enable_wide(1)
 
 
 def timed(fn, n=5):
@@ -26,11 +28,12 @@ def timed(fn, n=5):
     return s.elapsed_time(e) / n
 
 
-for D, T in shapes:
-    m = ManifoldHyperConnection(D, expansion_rate=4).cuda().eval()
+for shp in shapes:
+    D, T, ex = shp if len(shp) == 3 else (*shp, 4)
+    m = ManifoldHyperConnection(D, expansion_rate=ex).cuda().eval()
     x = torch.randn(T, D, device="cuda").to(torch.bfloat16)
     p = m.plan()
-    Hd = 4 * D
+    Hd = ex * D
     fl = 2.0 * T * (D * 2 * Hd + 2 * Hd * Hd + (Hd + D) * D)
     cases = {"unfused": (False, 0), "fused_v0": (True, 0), "fused_v1": (True, 1), "fused_v2": (True, 2)}
     res = {k: [] for k in cases}
