@@ -17,7 +17,8 @@ ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
 _LIB = None
 _LOCK = threading.Lock()
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhvs.so")
+# HV_LIB_PATH: load another build of the same C ABI (A/B of two builds in one GPU call)
+LIB_PATH = os.environ.get("HV_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhvs.so")
 
 vp = C.c_void_p
 i32 = C.c_int

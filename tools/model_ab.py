@@ -2,7 +2,8 @@
 setting (kernel choice is fixed at capture), replays timed in interleaved rounds.
 
 usage: python tools/model_ab.py <knob> <v0> <v1> [batch]
-  knob: deep | staged | big | small | train128 | ktail (hv_gemm_set_*)
+  knob: deep | staged | big | small | train128 | ktail (hv_gemm_set_*),
+        mhc (hv_mhc_fused_set_variant), wide (hv_mhc_fused_enable_wide)
 """
 import os
 import sys
@@ -18,7 +19,8 @@ knob, v0, v1 = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 16
 setter = {"deep": lib.hv_gemm_set_deep_ring, "staged": lib.hv_gemm_set_staged_epilogue,
           "big": lib.hv_gemm_set_big_tile, "small": lib.hv_gemm_set_small_tile,
-          "train128": lib.hv_gemm_set_train128, "ktail": lib.hv_gemm_set_conv_ktail}[knob]
+          "train128": lib.hv_gemm_set_train128, "ktail": lib.hv_gemm_set_conv_ktail,
+          "mhc": lib.hv_mhc_fused_set_variant, "wide": lib.hv_mhc_fused_enable_wide}[knob]
 torch.manual_seed(0)
 m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False}).cuda().eval()
 x = torch.randn(B, 3, 640, 640, device="cuda")
