@@ -658,54 +658,103 @@ __global__ void k_gather_rows(const T* x, long stride_rows, int n, int c, T* y) 
 }
 
 // ---------------------------------------------------------------- YOLO decode
+// One wave per group of YG = 8 consecutive cells (b, a, y, x): the group's predictions
+// ([YG][P], contiguous) and scores ([YG][nc], contiguous) are swept by all 64 lanes with
+// flat indices, so every store instruction covers 256 contiguous bytes (one wave per cell
+// left a 21-lane second pass per 85-float row and serial box stores).  The scores are kept
+// in LDS; the argmax per cell is then done by an 8-lane group (first index wins ties, like a
+// sequential scan), and lanes 0..YG-1 decode one box each.
+constexpr int YG = 8;
+constexpr int YMAXP = 256;                 // 5 + nc <= 256
+
 template <typename T>
 __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logits, int n, int h, int w,
                                                      int A, int nc, const float* anchor_wh,
                                                      float* pred, float* boxes, float* scores,
                                                      float* cscore, int64_t* cidx, float* obj) {
-  // one wave per cell (b, a, y, x): lanes cover the 5+nc logits, coalesced loads/stores,
-  // argmax by a wave reduction (first index wins ties, like a sequential scan)
-  const long cell = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+  __shared__ float sc_s[4][YG * (YMAXP - 5)];
+  __shared__ float ob_s[4][YG];
+  __shared__ long so_s[4][YG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long total = (long)n * A * h * w;
-  if (cell >= total) return;
-  const int x = cell % w;
-  long t = cell / w;
-  const int y = t % h; t /= h;
-  const int a = t % A;
-  const int b = t / A;
+  const long c0 = ((long)blockIdx.x * 4 + wv) * YG;          // first cell of this wave
+  if (c0 >= total) return;                                     // wave-uniform; no block barrier below
+  const int ncell = (int)min((long)YG, total - c0);
   const int P = 5 + nc;
-  const T* src = logits + (((long)b * h + y) * w + x) * (long)(A * P) + (long)a * P;
-  float* pr = pred + cell * P;
-  const float o = 1.0f / (1.0f + expf(-Elem<T>::load(src, 4)));
-  float best = -1.f;
-  int bi = 0x7fffffff;
-  for (int k = lane; k < P; k += 64) {
-    const float v = Elem<T>::load(src, k);
-    pr[k] = v;
-    if (k >= 5) {
-      const float s = o * (1.0f / (1.0f + expf(-v)));
-      scores[cell * nc + (k - 5)] = s;
-      if (s > best) { best = s; bi = k - 5; }
+  // lane c < ncell computes the logits offset of cell c0 + c (64-bit div/mod once per cell,
+  // not per element) into LDS; the sweeps below read it from there
+  long soff = 0;
+  if (lane < ncell) {
+    const long cell = c0 + lane;
+    const int x = cell % w;
+    long t = cell / w;
+    const int y = t % h; t /= h;
+    const int a = t % A;
+    const int b = t / A;
+    soff = (((long)b * h + y) * w + x) * (long)(A * P) + (long)a * P;
+    ob_s[wv][lane] = 1.0f / (1.0f + expf(-Elem<T>::load(logits + soff, 4)));
+    so_s[wv][lane] = soff;
+  }
+  auto src_of = [&](int c) -> const T* { return logits + so_s[wv][c]; };
+  __builtin_amdgcn_wave_barrier();
+  // predictions: raw logits, flat over [ncell][P] (P > 64: the cell index advances by <= 1)
+  {
+    int c = lane / P, k = lane - c * P;
+    for (int i = lane; i < ncell * P; i += 64) {
+      pred[c0 * P + i] = Elem<T>::load(src_of(c), k);
+      k += 64;
+      while (k >= P) { k -= P; ++c; }
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const float ob = __shfl_xor(best, off, 64);
-    const int oi = __shfl_xor(bi, off, 64);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  // scores = sigmoid(obj) * sigmoid(cls), flat over [ncell][nc]
+  {
+    int c = lane / nc, k = lane - c * nc;
+    for (int i = lane; i < ncell * nc; i += 64) {
+      const float sv = ob_s[wv][c] * (1.0f / (1.0f + expf(-Elem<T>::load(src_of(c), 5 + k))));
+      scores[c0 * nc + i] = sv;
+      sc_s[wv][i] = sv;
+      k += 64;
+      while (k >= nc) { k -= nc; ++c; }
+    }
   }
-  if (lane == 0) {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // argmax per cell: lane group g (8 lanes) owns cell g
+  {
+    const int g = lane >> 3, j = lane & 7;
+    float best = -1.f;
+    int bi = 0x7fffffff;
+    if (g < ncell)
+      for (int k = j; k < nc; k += 8) {
+        const float v = sc_s[wv][g * nc + k];
+        if (v > best) { best = v; bi = k; }
+      }
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) {
+      const float ob = __shfl_xor(best, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (j == 0 && g < ncell) {
+      cscore[c0 + g] = best;
+      cidx[c0 + g] = bi;
+    }
+  }
+  if (lane < ncell) {
+    const long cell = c0 + lane;
+    const int x = cell % w;
+    long t = cell / w;
+    const int y = t % h; t /= h;
+    const int a = t % A;
+    const T* src = logits + soff;
     const float v0 = Elem<T>::load(src, 0), v1 = Elem<T>::load(src, 1);
     const float v2 = Elem<T>::load(src, 2), v3 = Elem<T>::load(src, 3);
     const float sx = 1.0f / (1.0f + expf(-v0)), sy = 1.0f / (1.0f + expf(-v1));
     const float bx = ((float)x + sx) / (float)w, by = ((float)y + sy) / (float)h;
     const float bw = anchor_wh[2 * a] * expf(v2), bh = anchor_wh[2 * a + 1] * expf(v3);
-    float* bo = boxes + cell * 4;
-    bo[0] = bx - bw / 2; bo[1] = by - bh / 2; bo[2] = bx + bw / 2; bo[3] = by + bh / 2;
-    obj[cell] = o;
-    cscore[cell] = best;
-    cidx[cell] = bi;
+    *reinterpret_cast<float4*>(boxes + cell * 4) = make_float4(bx - bw / 2, by - bh / 2, bx + bw / 2, by + bh / 2);
+    obj[cell] = ob_s[wv][lane];
   }
 }
 
@@ -957,7 +1006,8 @@ extern "C" int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w
                               float* objectness, hv_stream_t stream) {
   const long total = (long)n * A * h * w;
   if (total <= 0 || nc <= 0) return HV_EINVAL;
-  HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 4), 256, 0, (hipStream_t)stream>>>(
+  if (nc + 5 > YMAXP || ((uintptr_t)boxes & 15)) return HV_EUNSUPPORTED;
+  HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 4L * YG), 256, 0, (hipStream_t)stream>>>(
                           (const T*)logits, n, h, w, A, nc, anchor_wh, predictions, boxes, scores,
                           class_scores, class_indices, objectness)));
   HV_CHECK_LAUNCH();

@@ -412,3 +412,21 @@ def test_gpu_preprocess_matches_torch(gpu_device, h, w, oh, ow):
     assert (nh.float().cpu() - ref).abs().max().item() < 2e-2
     h16 = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.float16)
     assert (h16.float().cpu() - ref).abs().max().item() < 5e-3
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 1, 1), (3, 5, 11), (2, 20, 20)])
+def test_decode_argmax_first_index_on_ties(gpu_device, n, h, w):
+    """hv_yolo_decode's class index/score equal the first-index argmax / max of the scores it
+    returns, with heavy ties (logits on a coarse grid) and partial 8-cell wave groups."""
+    ops = _ops()
+    from oracle import hv_oracle as O
+    g = torch.Generator().manual_seed(n * 100 + h)
+    lg = (torch.randint(-3, 4, (n, h, w, 3 * 85), generator=g).float() * 0.5).to(gpu_device)
+    dec, pr = ops.yolo_decode(lg, 3, 80, O.anchor_wh(1).float().to(gpu_device))
+    sc = dec["scores"].float().cpu().reshape(-1, 80)
+    ci = dec["class_indices"].cpu().reshape(-1)
+    assert torch.equal(ci, torch.argmax(sc, dim=1))
+    cs = dec["class_scores"].float().cpu().reshape(-1) if "class_scores" in dec else None
+    if cs is not None:
+        assert torch.equal(cs, sc.max(dim=1).values)
+    assert torch.equal(pr.cpu().reshape(-1), lg.reshape(n, h, w, 3, 85).permute(0, 3, 1, 2, 4).cpu().reshape(-1))
