@@ -376,7 +376,7 @@ class HybridVisionSystem(nn.Module):
     def _make_ctx(self) -> RunCtx:
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
         key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key)
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=True)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":
@@ -427,6 +427,7 @@ class HybridVisionSystem(nn.Module):
             outputs["backbone_features"] = bbv
             outputs["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
             outputs["final_features"] = final
+        ctx.join_prep()                        # side-stream prep joined even if no mHC ran
         return outputs
 
     def _final_features(self, fused: Dict[str, torch.Tensor]) -> torch.Tensor:

@@ -136,7 +136,7 @@ def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = N
     return ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x2.dtype, residual=residual)
 
 
-def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None) -> None:
+def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None, overlap: bool = False) -> None:
     """Sinkhorn + coefficient prep for every mHC module in `mods` through one grouped
     PrepProgram (reused from `cache` while `key` -- the owner's parameter/buffer storage --
     and the precision are unchanged, so a captured graph replays the same buffers)."""
@@ -152,7 +152,7 @@ def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None) -> 
         if cache is not None:
             cache["key"], cache["program"] = (key, ctx.dtype, FOLD_MAX_D), prog
     ctx.program = prog
-    prog.run(ctx)
+    prog.run(ctx, overlap)
 
 
 # ================================================================== mHC layer
@@ -206,6 +206,7 @@ class ManifoldHyperConnection(nn.Module):
     def plan(self) -> MhcPlan:
         ctx = current()
         if ctx is not None:
+            ctx.join_prep()
             p = ctx.plans.get(id(self))
             if p is None:
                 prepare_plans([self], ctx)

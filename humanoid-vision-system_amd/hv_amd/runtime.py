@@ -26,6 +26,14 @@ class RunCtx:
     dtype: torch.dtype
     plans: Dict[int, object] = field(default_factory=dict)
     program: Optional[object] = None      # prep.PrepProgram that produced `plans` (grouped prep)
+    prep_event: Optional[object] = None   # side-stream prep not yet joined (PrepProgram.run overlap)
+
+    def join_prep(self) -> None:
+        """Make the current stream wait for the side-stream Sinkhorn + mHC prep (once)."""
+        ev = self.prep_event
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+            self.prep_event = None
 
 
 def current() -> Optional[RunCtx]:

@@ -52,7 +52,9 @@ def _worker(rank, world, port, bucket_bytes, q):
             x = torch.randn(12, 16)
             net(x).pow(2).sum().backward()
             gb.finish()
-            res[step] = {n: p.grad.clone() for n, p in net.named_parameters()}
+            # numpy copies travel by value: tensors would be passed as shared-memory fds that the
+            # parent can only open while this process is alive (a race with its exit)
+            res[step] = {n: p.grad.detach().clone().numpy() for n, p in net.named_parameters()}
         q.put((rank, res, len(gb.buckets)))
     finally:
         dist.destroy_process_group()
@@ -94,7 +96,7 @@ def test_bucketed_allreduce_averages_gradients(bucket_bytes):
             assert nb > 2          # several buckets exercised
         for step in (0, 1):
             for n, g in res[step].items():
-                torch.testing.assert_close(g, ref[step][n], rtol=1e-5, atol=1e-6)
+                torch.testing.assert_close(torch.from_numpy(g), ref[step][n], rtol=1e-5, atol=1e-6)
 
 
 def test_mhc_group_assignment():
