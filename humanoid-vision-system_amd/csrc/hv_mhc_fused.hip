@@ -344,15 +344,16 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   // measured (tools/mhc_variants.py): more tokens per wave wins while acc2 fits in registers;
   // (tools/mhc_ab.py) 4-wave workgroups, two per CU, beat one 8-wave workgroup by 16-20% at
   // every D (the two groups' chunk barriers no longer coincide, so one group's MFMAs cover the
-  // other's DMA wait + barrier).  Variant 2 = the 8-wave groups; variant 1 = 1.5x tokens per
-  // wave (TB 6 / 3): 35-60% slower (register pressure); 2-wave groups were 4x slower (spills).
+  // other's DMA wait + barrier).  Variant 2 = the 8-wave groups; variant 1 = three 4-wave
+  // groups per CU (register cap 170): 2x slower.  Also measured slower: 1.5x tokens per wave
+  // (TB 6 / 3, 35-60%) and 2-wave groups (4x) -- all register spills.
   if (a->D == 32) {
-    if (g_variant == 1) return launch<32, 128, 6, 2, 4>(a, s);
+    if (g_variant == 1) return launch<32, 128, 4, 3, 4>(a, s);
     if (g_variant == 2) return launch<32, 128, 4, 1>(a, s);
     return launch<32, 128, 4, 2, 4>(a, s);
   }
   if (a->D == 64) {
-    if (g_variant == 1) return launch<64, 256, 3, 2, 4>(a, s);
+    if (g_variant == 1) return launch<64, 256, 2, 3, 4>(a, s);
     if (g_variant == 2) return launch<64, 256, 2, 1>(a, s);
     return launch<64, 256, 2, 2, 4>(a, s);
   }
