@@ -3,6 +3,7 @@
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -15,6 +16,10 @@ from .layers import ctx_scope, linear_prep, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection, prepare_plans
 from .runtime import RunCtx, current, param_versions, require_cuda, use_ctx, PRECISIONS
 from .vit import HybridVisionEncoder
+
+# side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HV_PREP_OVERLAP=1); on one
+# box, interleaved runs measured it 0.1 ms/step SLOWER in graph and eager mode
+_PREP_OVERLAP = os.environ.get("HV_PREP_OVERLAP", "0") == "1"
 
 DEFAULT_ANCHORS = [[(10, 13), (16, 30), (33, 23)],
                    [(30, 61), (62, 45), (59, 119)],
@@ -376,7 +381,7 @@ class HybridVisionSystem(nn.Module):
     def _make_ctx(self) -> RunCtx:
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
         key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=True)
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=_PREP_OVERLAP)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":
