@@ -5,6 +5,10 @@
 #include <stddef.h>
 
 #include "../../include/hv_kernels.h"
+#include "../../include/hv_tuning.h"
+
+// host-side launch counter (hv_diag.hip); relaxed atomic increment
+void hv_diag_count(int family);
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

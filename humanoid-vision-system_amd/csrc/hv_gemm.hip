@@ -16,6 +16,8 @@
 // four v_mfma_f32_16x16x4_f32 (fp32: lane group g takes k = 4g..4g+3, the k-order inside a
 // 16-deep step is permuted identically for A and B, so the products are exact).
 // 256 threads = 4 waves in a 2x2 grid; block -> tile mapping is XCD-aware (bijective).
+#include <atomic>
+
 #include "hv_common.h"
 #include "hv_gemm_epi.h"
 
@@ -293,6 +295,7 @@ template <typename T, int BM, int BN, bool TRAIN>
 int launch_mode_t(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
   constexpr int EPC = Tr<T>::EPC;
+  hv_diag_count(HV_KF_GEMM_REGSTAGE);
   if (d.conv_k > 0 && d.conv_transposed) {
     gemm_kernel<T, BM, BN, AM_CONVT, TRAIN><<<grid, 256, 0, s>>>(d);
   } else if (d.conv_k > 0) {
@@ -334,15 +337,15 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
 
-static int g_big_tile = 1;   // 256x256 ping-pong LDS-DMA kernel: 0 off, 1 by shape (default), 2 always
-int hv_gemm_big_tile_mode() { return g_big_tile; }
-static int g_small_tile = 1; // 64x64 LDS-DMA tiles for small grids: 1 on (default), 0 off (A/B tests)
-int hv_gemm_small_tile_mode() { return g_small_tile; }
+static std::atomic<int> g_big_tile{1};   // 256x256 ping-pong LDS-DMA kernel: 0 off, 1 by shape (default), 2 always
+int hv_gemm_big_tile_mode() { return g_big_tile.load(std::memory_order_relaxed); }
+static std::atomic<int> g_small_tile{1}; // 64x64 LDS-DMA tiles for small grids: 1 on (default), 0 off (A/B tests)
+int hv_gemm_small_tile_mode() { return g_small_tile.load(std::memory_order_relaxed); }
 extern "C" void hv_gemm_set_small_tile(int mode) { g_small_tile = mode; }
 extern "C" void hv_gemm_set_big_tile(int mode) { g_big_tile = mode; }
 
-static int g_force_regstage = 0;
-static int hv_gemm_force_regstage() { return g_force_regstage; }
+static std::atomic<int> g_force_regstage{0};
+static int hv_gemm_force_regstage() { return g_force_regstage.load(std::memory_order_relaxed); }
 // 1: route every GEMM through the register-staged kernel (A/B testing of the two paths)
 extern "C" void hv_gemm_set_path(int regstage_only) { g_force_regstage = regstage_only; }
 

@@ -8,6 +8,8 @@
 // global_load_lds is lane-linear.  Two LDS stages: the DMA of tile t+1 is in flight while
 // the MFMAs of tile t run.  Out-of-image conv taps read a zero line; rows past M are
 // clamped (computed, never stored).
+#include <atomic>
+
 #include "hv_common.h"
 #include "hv_gemm_epi.h"
 #include <type_traits>
@@ -430,10 +432,11 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   }
 }
 
-int g_staged_epi = 1;             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
+std::atomic<int> g_staged_epi{1};             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
 
 int launch256(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
+  hv_diag_count(HV_KF_GEMM_PP256);
   // fragment-layout epilogue here: the staged one measured 1.3x slower on this kernel (K >= 1024,
   // where the output stream is a small part of the work)
   if (d.conv_k > 0) gemm_pp256_kernel<true, false><<<grid, 512, 0, s>>>(d);
@@ -446,11 +449,13 @@ int launch256(const hv_gemm_desc& d, hipStream_t s) {
 // with one tile in flight (64x64: 4 buffers = 64 KiB, 64x128 / 128x64: 3 = 72 KiB)
 template <int BM, int BN>
 constexpr int deep_stages() { return BM * BN <= 64 * 64 ? 4 : (BM * BN <= 128 * 64 ? 3 : 2); }
-int g_deep = 1;                   // deeper LDS-DMA rings for the small tiles (A/B knob)
+std::atomic<int> g_deep{1};                   // deeper LDS-DMA rings for the small tiles (A/B knob)
 
 template <int BM, int BN, int NS>
 int launch_ns(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, BM) * hv_cdiv(d.N, BN);
+  hv_diag_count(BM == 128 && BN == 128 ? HV_KF_GEMM_GLDS_128x128 : BM == 64 && BN == 128 ? HV_KF_GEMM_GLDS_64x128
+                : BM == 128 ? HV_KF_GEMM_GLDS_128x64 : HV_KF_GEMM_GLDS_64x64);
   if (d.epi_mode) {
     if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, false, NS><<<grid, 256, 0, s>>>(d);
     else gemm_glds_kernel<BM, BN, false, true, false, NS><<<grid, 256, 0, s>>>(d);
@@ -480,11 +485,11 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_big_tile_mode();   // hv_gemm.hip
 int hv_gemm_small_tile_mode();  // hv_gemm.hip
-int g_train128 = 0;             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
+std::atomic<int> g_train128{0};             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
 extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
-int g_conv_ktail = 0;            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
+std::atomic<int> g_conv_ktail{0};            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
 extern "C" void hv_gemm_set_conv_ktail(int on) { g_conv_ktail = on; }
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).

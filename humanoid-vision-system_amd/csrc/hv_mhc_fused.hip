@@ -21,6 +21,8 @@
 // columns of that chunk are DMA'd (global_load_lds, 16 B/lane, XOR-swizzled rows) into a
 // double-buffered LDS stage shared by the 8 waves -- one barrier per chunk -- and Wc^T is
 // streamed the same way for GEMM3.  GELU is hv_gelu_fast (|err| <= 2.6e-5, below bf16).
+#include <atomic>
+
 #include "hv_common.h"
 
 namespace {
@@ -311,6 +313,7 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
+  hv_diag_count(HV_KF_MHC_FUSED);
   k<<<hv_cdiv(a->T, C::BM), C::NT, C::LDS, s>>>(
       (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
       a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
@@ -319,8 +322,8 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
   return HV_OK;
 }
 
-int g_fused_wide = 0;
-int g_variant = 0;
+std::atomic<int> g_fused_wide{0};
+std::atomic<int> g_variant{0};
 
 }  // namespace
 

@@ -671,7 +671,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logits, int n, int h, int w,
                                                      int A, int nc, const float* anchor_wh,
                                                      float* pred, float* boxes, float* scores,
-                                                     float* cscore, int64_t* cidx, float* obj) {
+                                                     float* cscore, int64_t* cidx, float* obj, float* det) {
   __shared__ float sc_s[4][YG * (YMAXP - 5)];
   __shared__ float ob_s[4][YG];
   __shared__ long so_s[4][YG];
@@ -710,8 +710,10 @@ __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logit
   {
     int c = lane / nc, k = lane - c * nc;
     for (int i = lane; i < ncell * nc; i += 64) {
-      const float sv = ob_s[wv][c] * (1.0f / (1.0f + expf(-Elem<T>::load(src_of(c), 5 + k))));
+      const float cp = 1.0f / (1.0f + expf(-Elem<T>::load(src_of(c), 5 + k)));
+      const float sv = ob_s[wv][c] * cp;
       scores[c0 * nc + i] = sv;
+      if (det) det[(c0 + c) * P + 5 + k] = cp;
       sc_s[wv][i] = sv;
       k += 64;
       while (k >= nc) { k -= nc; ++c; }
@@ -755,6 +757,11 @@ __global__ void __launch_bounds__(256) k_yolo_decode(const T* __restrict__ logit
     const float bw = anchor_wh[2 * a] * expf(v2), bh = anchor_wh[2 * a + 1] * expf(v3);
     *reinterpret_cast<float4*>(boxes + cell * 4) = make_float4(bx - bw / 2, by - bh / 2, bx + bw / 2, by + bh / 2);
     obj[cell] = ob_s[wv][lane];
+    if (det) {
+      float* dr = det + cell * P;
+      dr[0] = bx - bw / 2; dr[1] = by - bh / 2; dr[2] = bx + bw / 2; dr[3] = by + bh / 2;
+      dr[4] = ob_s[wv][lane];
+    }
   }
 }
 
@@ -961,11 +968,143 @@ extern "C" int hv_vit_tokens(int dtype, const void* x, const float* cls, const f
   return HV_OK;
 }
 
+
+
+// ---- general attention (MultiHeadManifoldAttention.forward with cross-attention, a key padding
+// mask or need_weights; manifold_layers.py:386-434): one lane per query row, 32-key K/V tiles
+// staged in LDS as fp32, online softmax; optional second pass writes the probabilities.
+// A row whose keys are all masked gives NaN, as softmax over all -inf does in the reference.
+template <typename T, int HD>
+__global__ void __launch_bounds__(64) k_attention_general(const T* __restrict__ q, const T* __restrict__ k,
+                                                          const T* __restrict__ v,
+                                                          const unsigned char* __restrict__ mask, T* __restrict__ o,
+                                                          float* __restrict__ wts, int Lq, int Lk, int heads,
+                                                          float scale) {
+  constexpr int KT = 32;
+  __shared__ float ks[KT][HD + 1];
+  __shared__ float vs[KT][HD + 1];
+  __shared__ unsigned char ms[KT];
+  const int D = heads * HD;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const bool live = i < Lq;
+  float qr[HD], acc[HD];
+  const T* qp = q + ((long)b * Lq + (live ? i : 0)) * D + h * HD;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) {
+    qr[d] = Elem<T>::load(qp, d) * scale;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j0 = 0; j0 < Lk; j0 += KT) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < KT * HD; e += 64) {
+      const int jj = e / HD, d = e - jj * HD;
+      const int j = j0 + jj;
+      float kv = 0.f, vv = 0.f;
+      if (j < Lk) {
+        const long off = ((long)b * Lk + j) * D + h * HD + d;
+        kv = Elem<T>::load(k, off);
+        vv = Elem<T>::load(v, off);
+      }
+      ks[jj][d] = kv;
+      vs[jj][d] = vv;
+    }
+    if (threadIdx.x < KT) {
+      const int j = j0 + threadIdx.x;
+      ms[threadIdx.x] = j < Lk ? (mask ? mask[(long)b * Lk + j] : 0) : 1;
+    }
+    __syncthreads();
+    for (int jj = 0; jj < KT; ++jj) {
+      if (ms[jj]) continue;
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < HD; ++d) sc = fmaf(qr[d], ks[jj][d], sc);
+      const float mn = fmaxf(m, sc);
+      const float corr = __expf(m - mn), p = __expf(sc - mn);
+      l = l * corr + p;
+#pragma unroll
+      for (int d = 0; d < HD; ++d) acc[d] = fmaf(acc[d], corr, p * vs[jj][d]);
+      m = mn;
+    }
+  }
+  if (live) {
+    const float inv = l > 0.f ? 1.f / l : NAN;
+    T* op = o + ((long)b * Lq + i) * D + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) Elem<T>::store(op, d, acc[d] * inv);
+  }
+  if (!wts) return;
+  float* wp = wts + (((long)b * heads + h) * Lq + (live ? i : 0)) * Lk;
+  for (int j0 = 0; j0 < Lk; j0 += KT) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < KT * HD; e += 64) {
+      const int jj = e / HD, d = e - jj * HD;
+      const int j = j0 + jj;
+      ks[jj][d] = j < Lk ? Elem<T>::load(k, ((long)b * Lk + j) * D + h * HD + d) : 0.f;
+    }
+    if (threadIdx.x < KT) {
+      const int j = j0 + threadIdx.x;
+      ms[threadIdx.x] = j < Lk ? (mask ? mask[(long)b * Lk + j] : 0) : 1;
+    }
+    __syncthreads();
+    if (!live) continue;
+    for (int jj = 0; jj < KT && j0 + jj < Lk; ++jj) {
+      float p;
+      if (l == 0.f) {
+        p = NAN;
+      } else if (ms[jj]) {
+        p = 0.f;
+      } else {
+        float sc = 0.f;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) sc = fmaf(qr[d], ks[jj][d], sc);
+        p = __expf(sc - m) / l;
+      }
+      wp[j0 + jj] = p;
+    }
+  }
+}
+
+// ---- batched byte-range copies (hv_copy_segments): 16 KiB per block, segment found by binary
+// search over the block prefix table passed by value
+constexpr int kCopyMax = 64;
+constexpr long long kCopyChunk = 16384;
+struct CopyBatch {
+  int count;
+  const unsigned char* src[kCopyMax];
+  unsigned char* dst[kCopyMax];
+  long long bytes[kCopyMax];
+  long long block_start[kCopyMax + 1];
+};
+
+__global__ void __launch_bounds__(256) k_copy_segments(const CopyBatch cb) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = cb.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cb.block_start[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const unsigned char* src = cb.src[lo];
+  unsigned char* dst = cb.dst[lo];
+  const long long beg = (b - cb.block_start[lo]) * kCopyChunk;
+  const long long end = beg + kCopyChunk < cb.bytes[lo] ? beg + kCopyChunk : cb.bytes[lo];
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const long long vend = beg + ((end - beg) & ~15LL);
+    for (long long i = beg + threadIdx.x * 16LL; i < vend; i += 256 * 16)
+      *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    for (long long i = vend + threadIdx.x; i < end; i += 256) dst[i] = src[i];
+  } else {
+    for (long long i = beg + threadIdx.x; i < end; i += 256) dst[i] = src[i];
+  }
+}
+
 extern "C" int hv_attention(int dtype, const void* q, const void* k, const void* v, void* out,
                             int n, int L, int heads, int hd, float sm_scale, hv_stream_t stream) {
   if (n <= 0 || L <= 0 || heads <= 0) return HV_EINVAL;
   if (hd != 32) return HV_EUNSUPPORTED;
   const dim3 g(hv_cdiv(L, 128), heads, n);
+  hv_diag_count(HV_KF_ATTN_SCALAR);
   HV_DISPATCH(dtype, (k_attention<T, 32><<<g, 128, 0, (hipStream_t)stream>>>(
                           (const T*)q, (const T*)k, (const T*)v, (T*)out, L, heads, sm_scale)));
   HV_CHECK_LAUNCH();
@@ -982,6 +1121,7 @@ extern "C" int hv_attention_mfma(const void* q, const void* k, const void* v, vo
   if (hd != 32 || (((uintptr_t)q | (uintptr_t)k | (uintptr_t)vt_work | (uintptr_t)out) & 15)) return HV_EUNSUPPORTED;
   const int Lp = (L + 31) / 32 * 32;
   hipStream_t s = (hipStream_t)stream;
+  hv_diag_count(HV_KF_ATTN_MFMA);
   k_vt_pad<<<dim3(hv_cdiv(32L * Lp, 256), n * heads), 256, 0, s>>>((const unsigned short*)v, L, Lp, heads,
                                                                    (unsigned short*)vt_work);
   k_attention_mfma<<<dim3(hv_cdiv(L, 64), heads, n), 256, 0, s>>>(
@@ -1003,13 +1143,13 @@ extern "C" int hv_gather_rows(int dtype, const void* x, long stride_rows, int n,
 extern "C" int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, int nc,
                               const float* anchor_wh, float* predictions, float* boxes,
                               float* scores, float* class_scores, int64_t* class_indices,
-                              float* objectness, hv_stream_t stream) {
+                              float* objectness, float* detections, hv_stream_t stream) {
   const long total = (long)n * A * h * w;
   if (total <= 0 || nc <= 0) return HV_EINVAL;
   if (nc + 5 > YMAXP || ((uintptr_t)boxes & 15)) return HV_EUNSUPPORTED;
   HV_DISPATCH(dtype, (k_yolo_decode<T><<<hv_cdiv(total, 4L * YG), 256, 0, (hipStream_t)stream>>>(
                           (const T*)logits, n, h, w, A, nc, anchor_wh, predictions, boxes, scores,
-                          class_scores, class_indices, objectness)));
+                          class_scores, class_indices, objectness, detections)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -1071,6 +1211,51 @@ extern "C" int hv_gemv(const float* W, const float* x, const float* b, int N, in
                        hv_stream_t stream) {
   if (N <= 0 || K <= 0) return HV_EINVAL;
   k_gemv<<<hv_cdiv(N, 4), 256, 0, (hipStream_t)stream>>>(W, x, b, N, K, y);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_copy_segments(const hv_copy_segment* segs, int count, hv_stream_t stream) {
+  if (count < 0 || (count > 0 && !segs)) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  for (int base = 0; base < count; base += kCopyMax) {
+    CopyBatch cb;
+    cb.count = 0;
+    long long blocks = 0;
+    for (int i = base; i < count && i < base + kCopyMax; ++i) {
+      if (segs[i].bytes < 0 || (segs[i].bytes > 0 && (!segs[i].src || !segs[i].dst))) return HV_EINVAL;
+      if (segs[i].bytes == 0) continue;
+      cb.src[cb.count] = (const unsigned char*)segs[i].src;
+      cb.dst[cb.count] = (unsigned char*)segs[i].dst;
+      cb.bytes[cb.count] = segs[i].bytes;
+      cb.block_start[cb.count] = blocks;
+      blocks += (segs[i].bytes + kCopyChunk - 1) / kCopyChunk;
+      ++cb.count;
+    }
+    if (cb.count == 0) continue;
+    cb.block_start[cb.count] = blocks;
+    k_copy_segments<<<(unsigned)blocks, 256, 0, s>>>(cb);
+    HV_CHECK_LAUNCH();
+  }
+  return HV_OK;
+}
+
+extern "C" int hv_attention_general(int dtype, const void* q, const void* k, const void* v,
+                                    const unsigned char* key_padding_mask, void* out, float* weights, int n,
+                                    int Lq, int Lk, int heads, int hd, float sm_scale, hv_stream_t stream) {
+  if (n <= 0 || Lq <= 0 || Lk <= 0 || heads <= 0 || !q || !k || !v || !out) return HV_EINVAL;
+  const dim3 g(hv_cdiv(Lq, 64), heads, n);
+  hipStream_t s = (hipStream_t)stream;
+  hv_diag_count(HV_KF_ATTN_SCALAR);
+#define HV_ATTN_GEN(HDV)                                                                            \
+  HV_DISPATCH(dtype, (k_attention_general<T, HDV><<<g, 64, 0, s>>>((const T*)q, (const T*)k, (const T*)v, \
+                                                                 key_padding_mask, (T*)out, weights, Lq, Lk,  \
+                                                                 heads, sm_scale)))
+  if (hd == 16) HV_ATTN_GEN(16);
+  else if (hd == 32) HV_ATTN_GEN(32);
+  else if (hd == 64) HV_ATTN_GEN(64);
+  else return HV_EUNSUPPORTED;
+#undef HV_ATTN_GEN
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

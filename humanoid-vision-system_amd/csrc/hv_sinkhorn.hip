@@ -211,6 +211,7 @@ extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
 extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count, int total_rows,
                                          int total_row_blocks, int total_cols, int max_iters,
                                          hv_stream_t stream) {
+  hv_diag_count(HV_KF_SINKHORN_GROUP);
   if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);

@@ -50,6 +50,10 @@ class GemmDesc(C.Structure):
                 ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("pad1_", i32)]
 
 
+class CopySegment(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("bytes", C.c_longlong)]
+
+
 class WgradDesc(C.Structure):
     _fields_ = [("dtype", i32), ("P", i32), ("N1", i32), ("N2", i32),
                 ("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("C", vp), ("ldc", i64),
@@ -100,6 +104,9 @@ _SIGS = {
     "hv_mhc_fused_supported": ([i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
     "hv_mhc_fused_enable_wide": ([i32], None),
+    "hv_mhc_fused_set_variant": ([i32], None),
+    "hv_diag_launch_counts": ([vp], None),
+    "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),
     "hv_struct_sizes": ([vp], None),
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),
@@ -135,7 +142,9 @@ _SIGS = {
     "hv_attention_work_elems": ([i32, i32, i32, i32], C.c_size_t),
     "hv_attention_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
-    "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+    "hv_copy_segments": ([vp, i32, vp], i32),
+    "hv_attention_general": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp], i32),
+    "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),
     "hv_preprocess": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp], i32),
     "hv_nms": ([vp, i32, i32, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),

@@ -68,7 +68,7 @@ class ConvMHCLayer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "ConvMHCLayer")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             return to_nchw_view(TM.conv_mhc_layer(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self)))
         with ctx_scope(self) as ctx:
@@ -102,7 +102,7 @@ class ResidualMHCLayer(nn.Module):
 
     def forward(self, x):
         require_cuda(x, "ResidualMHCLayer")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             return to_nchw_view(TM.residual_layer(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self)))
         with ctx_scope(self) as ctx:
@@ -169,7 +169,7 @@ class HybridVisionBackbone(nn.Module):
 
     def forward(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
         require_cuda(x, "HybridVisionBackbone")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             out = TM.backbone(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self))
         else:

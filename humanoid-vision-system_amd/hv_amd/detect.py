@@ -14,12 +14,16 @@ from . import ops
 from .backbone import HybridVisionBackbone
 from .layers import ctx_scope, linear_prep, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection, prepare_plans
-from .runtime import RunCtx, current, param_versions, require_cuda, use_ctx, PRECISIONS
+from .runtime import RunCtx, VersionWatch, current, require_cuda, use_ctx, PRECISIONS
 from .vit import HybridVisionEncoder
 
 # side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HV_PREP_OVERLAP=1); on one
 # box, interleaved runs measured it 0.1 ms/step SLOWER in graph and eager mode
 _PREP_OVERLAP = os.environ.get("HV_PREP_OVERLAP", "0") == "1"
+
+# outputs['detections'] keys: the per-scale names DetectionPostprocessor (postprocessing.py:
+# 234-244, 270-281) and MHCYOLOLoss (loss_functions.py:86) look up
+DETECTION_KEYS = ("small_scale", "medium_scale", "large_scale")
 
 DEFAULT_ANCHORS = [[(10, 13), (16, 30), (33, 23)],
                    [(30, 61), (62, 45), (59, 119)],
@@ -76,7 +80,7 @@ class FeaturePyramidNetwork(nn.Module):
         return out
 
     def forward(self, features: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             from .runtime import resolve_dtype
             dt = resolve_dtype(self.mhc_fusions[0])
@@ -146,7 +150,7 @@ class YOLOPredictionHead(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "YOLOPredictionHead")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             from .runtime import resolve_dtype
             lg = TM.head_logits(self, TM.nhwc_in(x, resolve_dtype(self)), TM.module_H(self))
@@ -174,7 +178,7 @@ class YOLODecoder(nn.Module):
 
 
 class YOLOLoss(nn.Module):
-    """yolo_head.py:297-465 (kept for API completeness; the training path is not on HIP yet)."""
+    """yolo_head.py:297-465 on the fused HIP loss kernels (hv_yolo_loss forward + dlogits)."""
 
     def __init__(self, num_classes: int = 80, anchors=None, image_size: int = 416, lambda_coord: float = 5.0,
                  lambda_noobj: float = 0.5, lambda_obj: float = 1.0, lambda_cls: float = 1.0):
@@ -206,20 +210,25 @@ class YOLODetectionHead(nn.Module):
         self.loss_fn = YOLOLoss(num_classes=num_classes, anchors=anchors)
         self.grid_sizes = [(13, 13), (26, 26), (52, 52)]
 
-    def forward_nhwc(self, feats: Dict[str, torch.Tensor]):
+    def forward_nhwc(self, feats: Dict[str, torch.Tensor], detections: Optional[Dict[str, torch.Tensor]] = None):
+        """detections: if a dict is given, it is filled with the per-scale decoded detections
+        tensors (HybridVisionSystem's 'detections' output key)."""
         preds, decoded = {}, {}
         for s, key in enumerate(("scale_small", "scale_medium", "scale_large")):
             if key not in feats:
                 continue
             lg = self.pred_heads[s].logits_nhwc(feats[key])
             awh = self.anchor_generator.anchors[s].reshape(self.num_anchors, 4)[:, 2:4].contiguous()
-            dec, pred = ops.yolo_decode(lg, self.num_anchors, self.num_classes, awh)
+            dec, pred = ops.yolo_decode(lg, self.num_anchors, self.num_classes, awh,
+                                        detections=detections is not None)
+            if detections is not None:
+                detections[DETECTION_KEYS[s]] = dec.pop("detections")
             preds[f"scale_{s}"] = pred
             decoded[f"scale_{s}"] = dec
         return preds, decoded
 
     def forward(self, features: Dict[str, torch.Tensor], targets=None, compute_loss: bool = False):
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             preds, decoded = {}, {}
             for s, key in enumerate(("scale_small", "scale_medium", "scale_large")):
                 if key not in features:
@@ -284,30 +293,53 @@ class YOLODetectionHead(nn.Module):
 class GraphRunner:
     """One HybridVisionSystem forward captured as a HIP graph (torch.cuda.CUDAGraph over the
     HIP runtime).  Every kernel of the step -- grouped Sinkhorn, coefficient folds, the token
-    path, decode -- is recorded once and replayed with no host launch overhead."""
+    path, decode -- is recorded once and replayed with no host launch overhead.
+
+    Staleness: the graph bakes in parameter storage (and, with the model frozen, the prepared
+    coefficients).  Every call snapshots the parameters' / input buffers' storage pointers and
+    version counters (runtime.VersionWatch) AFTER enqueueing the replay -- the ~0.4 ms host
+    check overlaps the GPU step -- and when anything changed (an optimizer step,
+    load_state_dict, a `.data` swap) it re-captures and replays again before returning, so a
+    result never comes from stale weights.
+
+    Ownership: replay() returns the captured static outputs, overwritten by the next replay;
+    __call__(x, owned=True) returns fresh copies (one segmented-copy launch)."""
 
     def __init__(self, model: "HybridVisionSystem", example: torch.Tensor, task: str = "detection"):
         require_cuda(example, "GraphRunner")
         self.model = model
+        self.task = task
         self.static_in = example.detach().clone()
+        self.recaptures = 0
+        self._capture()
+
+    def _capture(self):
+        model = self.model
+        self.graph = None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):                   # allocate workspaces, upload tables, set attributes
-                model(self.static_in, task=task)
+                model(self.static_in, task=self.task)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.static_out = model(self.static_in, task=task)
+            self.static_out = model(self.static_in, task=self.task)
+        self.version = model._watch.snapshot()
 
     def replay(self) -> Dict[str, Any]:
         self.graph.replay()
+        if self.model._watch.snapshot() != self.version:
+            self.recaptures += 1
+            self._capture()
+            self.graph.replay()
         return self.static_out
 
-    def __call__(self, x: torch.Tensor) -> Dict[str, Any]:
+    def __call__(self, x: torch.Tensor, owned: bool = False) -> Dict[str, Any]:
         self.static_in.copy_(x)
-        return self.replay()
+        out = self.replay()
+        return ops.clone_tree(out) if owned else out
 
 
 # ====================================================================== system
@@ -363,6 +395,7 @@ class HybridVisionSystem(nn.Module):
         self._mhc_modules = [m for m in self.modules() if isinstance(m, ManifoldHyperConnection)]
         self._frozen: Optional[Tuple[Any, RunCtx]] = None
         self._sk_cache: Dict[str, Any] = {}
+        self._watch = VersionWatch(self)
 
     # ---- precision / caching controls
     def set_precision(self, precision: str) -> "HybridVisionSystem":
@@ -392,7 +425,7 @@ class HybridVisionSystem(nn.Module):
     def _ctx(self) -> RunCtx:
         if self._frozen is None:
             return self._make_ctx()
-        ver = param_versions(self)
+        ver = self._watch.snapshot()
         if self._frozen[0] != ver:
             self._frozen = (ver, self._make_ctx())
         return self._frozen[1]
@@ -401,7 +434,7 @@ class HybridVisionSystem(nn.Module):
     def forward(self, x: torch.Tensor, targets=None, text_query=None, task: str = "detection",
                 compute_loss: bool = False) -> Dict[str, Any]:
         require_cuda(x, "HybridVisionSystem")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             # training step: BN batch statistics, dropout, autograd over HIP kernels
             from .train_model import system_forward
             return system_forward(self, x, targets, task, compute_loss)
@@ -418,9 +451,11 @@ class HybridVisionSystem(nn.Module):
             if task == "detection":
                 det_in = {"scale_small": fused["fused_small"], "scale_medium": fused["fused_medium"],
                           "scale_large": fused["fused_large"]}
-                preds, decoded = self.detection_head.forward_nhwc(det_in)
+                dets: Dict[str, torch.Tensor] = {}
+                preds, decoded = self.detection_head.forward_nhwc(det_in, dets)
                 outputs["predictions"] = preds
                 outputs["decoded"] = decoded
+                outputs["detections"] = dets
                 if compute_loss and targets is not None:
                     outputs["loss"] = self.detection_head.loss_fn(preds, targets)
             final = self._final_features(fused)

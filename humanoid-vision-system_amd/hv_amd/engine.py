@@ -7,8 +7,13 @@ reset_stats, AsyncInferenceEngine.infer_async / infer_sync -- with these differe
   * the model forward runs on the HIP kernels of hv_amd (bf16 activations, fp32
     coefficients) instead of torch.cuda.amp fp16 autocast; use_half_precision selects bf16;
   * streaming (batch 1) can replay a hipGraph of the whole forward with the coefficients
-    frozen (config.use_graphs), and stability metrics are read lazily (no per-frame host
-    syncs over 76 modules unless collect_stability is set);
+    frozen (config.use_graphs); the replay is re-captured when any parameter changes and
+    infer() returns owned copies of its outputs (GraphRunner);
+  * every infer() result carries 'stability_metrics' like the reference, as a lazy mapping:
+    the 76 modules' host reads happen on first access, not per frame (collect_stability=True
+    also materialises and records them for get_stability_report);
+  * forward outputs also carry 'detections' (post-processed boxes / scores / labels per
+    image), the key scripts/inference.py:121 reads;
   * the reference preprocessor's stale-cache defect is not reproduced.
 """
 from __future__ import annotations
@@ -21,6 +26,7 @@ import time
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
+from collections.abc import Mapping
 from typing import Any, Callable, Dict, List, Optional, Union
 
 import numpy as np
@@ -74,6 +80,30 @@ def preprocess_frames(imgs: List[np.ndarray], height: int, width: int, device, d
         raise ValueError("expected uint8 HWC 3-channel frames")
     raw = torch.from_numpy(np.ascontiguousarray(np.stack(imgs))).to(device, non_blocking=True)
     return ops.preprocess(raw, height, width, bgr=True, dtype=dtype)
+
+
+class LazyStabilityMetrics(Mapping):
+    """model.get_stability_metrics() (hybrid_vision.py:441-457), evaluated on first access:
+    the reference syncs the host ~300 times per frame for it (engine.py:300-302); streaming
+    callers that never read it pay nothing."""
+
+    def __init__(self, model):
+        self._model = model
+        self._data: Optional[Dict[str, Any]] = None
+
+    def _get(self) -> Dict[str, Any]:
+        if self._data is None:
+            self._data = self._model.get_stability_metrics() if hasattr(self._model, "get_stability_metrics") else {}
+        return self._data
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
 
 
 class InferenceEngine:
@@ -151,7 +181,7 @@ class InferenceEngine:
             x = x.unsqueeze(0)
         with self._lock:
             if self._runner is not None and tuple(x.shape) == tuple(self._runner.static_in.shape):
-                outputs = self._runner(x)
+                outputs = self._runner(x, owned=True)
             else:
                 outputs = self.model(x, task="detection")
             if self.device.type == "cuda":
@@ -160,12 +190,11 @@ class InferenceEngine:
         self.inference_times.append(ms)
         if self.device.type == "cuda":
             self.memory_usage.append(torch.cuda.memory_allocated() / 1024 ** 2)
+        st = LazyStabilityMetrics(self.model)
         res = {"outputs": outputs, "inference_time_ms": ms, "batch_size": x.shape[0],
-               "input_shape": x.shape, "device": str(self.device)}
-        if self.config.collect_stability and hasattr(self.model, "get_stability_metrics"):
-            st = self.model.get_stability_metrics()
-            self.stability_metrics.append(st)
-            res["stability_metrics"] = st
+               "input_shape": x.shape, "device": str(self.device), "stability_metrics": st}
+        if self.config.collect_stability:
+            self.stability_metrics.append(dict(st))
         return res
 
     inference = infer   # call-site alias (scripts/inference.py:121)

@@ -19,7 +19,8 @@ def conv_prep(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], dtype: torch.dtype,
     cout = conv.out_channels
     dev = conv.weight.device
     if bn is not None and bn.training:
-        raise NotImplementedError("hv_amd: BatchNorm batch statistics (training mode) not implemented yet")
+        raise RuntimeError("conv_prep folds eval-mode BatchNorm; training-mode BN (batch statistics) runs "
+                           "through hv_amd.train_model -- call the module in train() mode instead")
     if ctx is not None and ctx.program is not None and ctx.program.dtype == dtype:
         ctx.program.add_conv(conv, bn)            # grouped from the next forward on
     if bn is not None:

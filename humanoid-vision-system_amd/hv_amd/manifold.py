@@ -218,7 +218,7 @@ class ManifoldHyperConnection(nn.Module):
 
     def forward_tokens(self, x2: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x2: [T, D] token-major in the compute dtype."""
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_fn as TF
             y = TF.mhc(self, x2, self.sinkhorn(self.H_res_raw))
             return y if residual is None else TF.AddFn.apply(y, residual, 1.0)
@@ -313,20 +313,34 @@ class MultiHeadManifoldAttention(nn.Module):
         return self.out_proj.forward_tokens(o.view(n * L, -1))
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
+        """manifold_layers.py:386-434: (out [n, Lq, D], attn_weights [n, heads, Lq, Lk] or None).
+        Self-attention without mask/weights runs the MFMA kernel; cross-attention, a key
+        padding mask (True = ignore) or need_weights run hv_attention_general."""
         require_cuda(query, "MultiHeadManifoldAttention")
-        if self.training and torch.is_grad_enabled() and key is query and value is query \
-                and key_padding_mask is None and not need_weights:
+        general = key is not query or value is not query or key_padding_mask is not None or need_weights
+        if self.training and not general:
             from . import train_model as TM
             n, L, D = query.shape
             x = query.reshape(n * L, D).to(resolve_dtype(self.q_proj)).contiguous()
             return TM.attention(self, x, n, TM.module_H(self)).view(n, L, D).to(query.dtype), None
-        if key is not query or value is not query or key_padding_mask is not None or need_weights:
-            raise NotImplementedError("hv_amd attention implements the self-attention call of "
-                                      "TransformerEncoderBlock (vit_encoder_decoder.py:191)")
-        n, L, D = query.shape
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("hv_amd trains the self-attention call of TransformerEncoderBlock "
+                                      "(vit_encoder_decoder.py:191); masked / cross / need_weights attention "
+                                      "runs in eval mode or under torch.no_grad")
+        n, Lq, D = query.shape
         dt = resolve_dtype(self.q_proj)
-        x = query.reshape(n * L, D).to(dt).contiguous()
-        return self.forward_tokens(x, n).view(n, L, D).to(query.dtype), None
+        with torch.no_grad():
+            if not general:
+                x = query.reshape(n * Lq, D).to(dt).contiguous()
+                return self.forward_tokens(x, n).view(n, Lq, D).to(query.dtype), None
+            Lk = key.shape[1]
+            tok = lambda t: t.reshape(-1, D).to(dt).contiguous()   # noqa: E731
+            q = self.q_proj.forward_tokens(tok(query)).view(n, Lq, D)
+            k = self.k_proj.forward_tokens(tok(key)).view(n, Lk, D)
+            v = self.v_proj.forward_tokens(tok(value)).view(n, Lk, D)
+            o, w = ops.attention_general(q, k, v, self.num_heads, key_padding_mask, need_weights)
+            out = self.out_proj.forward_tokens(o.view(n * Lq, D)).view(n, Lq, D).to(query.dtype)
+        return out, w
 
 
 class RMSNorm(nn.Module):

@@ -471,6 +471,28 @@ def attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
     return o
 
 
+def attention_general(q: Tensor, k: Tensor, v: Tensor, heads: int, key_padding_mask: Optional[Tensor] = None,
+                      need_weights: bool = False):
+    """softmax(q k^T / sqrt(hd), masked) v for q [n, Lq, D], k / v [n, Lk, D] -> (out [n, Lq, D],
+    weights [n, heads, Lq, Lk] fp32 or None).  key_padding_mask: bool [n, Lk], True = ignore."""
+    n, Lq, D = q.shape
+    Lk = k.shape[1]
+    if k.shape != (n, Lk, D) or v.shape != k.shape or k.dtype != q.dtype or v.dtype != q.dtype:
+        raise ValueError("attention_general: q/k/v shapes or dtypes disagree")
+    hd = D // heads
+    mask = None
+    if key_padding_mask is not None:
+        if tuple(key_padding_mask.shape) != (n, Lk):
+            raise ValueError(f"key_padding_mask must be [{n}, {Lk}]")
+        mask = key_padding_mask.to(device=q.device, dtype=torch.uint8).contiguous()
+    o = torch.empty_like(q)
+    w = torch.empty((n, heads, Lq, Lk), device=q.device, dtype=torch.float32) if need_weights else None
+    check(L.lib().hv_attention_general(dtype_code(q.dtype), _contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
+                                       _contig(v, "v").data_ptr(), ptr(mask), o.data_ptr(), ptr(w), n, Lq, Lk,
+                                       heads, hd, hd ** -0.5, stream_ptr()), "hv_attention_general")
+    return o, w
+
+
 def gather_rows(x: Tensor, stride_rows: int) -> Tensor:
     """Row 0 of every group of `stride_rows` rows: x [n*stride_rows, c] -> [n, c]."""
     c = x.shape[-1]
@@ -484,8 +506,10 @@ def gather_rows(x: Tensor, stride_rows: int) -> Tensor:
     return y
 
 
-def yolo_decode(logits: Tensor, A: int, nc: int, anchor_wh: Tensor):
-    """logits NHWC [n, h, w, A*(5+nc)] -> reference YOLODecoder outputs (shim S5 layout)."""
+def yolo_decode(logits: Tensor, A: int, nc: int, anchor_wh: Tensor, detections: bool = False):
+    """logits NHWC [n, h, w, A*(5+nc)] -> reference YOLODecoder outputs (shim S5 layout); with
+    detections=True the dict also holds 'detections' [n, A, h, w, 5+nc] = (xyxy box,
+    objectness, class probabilities), written by the same launch."""
     n, h, w, _ = logits.shape
     dev = logits.device
     P = 5 + nc
@@ -495,14 +519,82 @@ def yolo_decode(logits: Tensor, A: int, nc: int, anchor_wh: Tensor):
     cs = torch.empty((n, A, h, w), device=dev, dtype=torch.float32)
     ci = torch.empty((n, A, h, w), device=dev, dtype=torch.int64)
     obj = torch.empty((n, A, h, w, 1), device=dev, dtype=torch.float32)
+    det = torch.empty((n, A, h, w, P), device=dev, dtype=torch.float32) if detections else None
     awh = f32(anchor_wh)
     if awh.numel() != 2 * A or logits.shape[-1] != A * P:
         raise ValueError("yolo_decode: anchor / channel count mismatch")
     check(L.lib().hv_yolo_decode(dtype_code(logits.dtype), _contig(logits, "logits").data_ptr(), n, h, w, A, nc,
                                  awh.data_ptr(), pred.data_ptr(), boxes.data_ptr(), scores.data_ptr(),
-                                 cs.data_ptr(), ci.data_ptr(), obj.data_ptr(), stream_ptr()), "hv_yolo_decode")
-    return {"boxes": boxes, "scores": scores, "class_scores": cs, "class_indices": ci,
-            "objectness": obj, "raw_predictions": pred}, pred
+                                 cs.data_ptr(), ci.data_ptr(), obj.data_ptr(), ptr(det), stream_ptr()),
+          "hv_yolo_decode")
+    out = {"boxes": boxes, "scores": scores, "class_scores": cs, "class_indices": ci,
+           "objectness": obj, "raw_predictions": pred}
+    if det is not None:
+        out["detections"] = det
+    return out, pred
+
+
+def _dense(t: Tensor) -> bool:
+    """Non-overlapping and dense (a permutation of a contiguous layout, e.g. the NCHW views
+    of NHWC storage): its bytes are one range starting at data_ptr()."""
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+def clone_tree(tree):
+    """Owned copies of every device tensor in a (nested dict / list / tuple) output tree:
+    one arena allocation + one hv_copy_segments launch per 64 tensors, same shapes, strides
+    and dtypes (a graph replay's static outputs, handed to callers that keep them)."""
+    leaves = []
+
+    def collect(o):
+        if isinstance(o, Tensor):
+            leaves.append(o)
+        elif isinstance(o, dict):
+            for v in o.values():
+                collect(v)
+        elif isinstance(o, (list, tuple)):
+            for v in o:
+                collect(v)
+    collect(tree)
+    uniq = {}
+    for t in leaves:
+        if t.is_cuda and id(t) not in uniq:
+            uniq[id(t)] = t if _dense(t) else t.contiguous()
+    if not uniq:
+        return tree
+    offs, total = {}, 0
+    for k, t in uniq.items():
+        offs[k] = total
+        total += (t.numel() * t.element_size() + 255) // 256 * 256
+    dev = next(iter(uniq.values())).device
+    arena = torch.empty(max(total, 1), device=dev, dtype=torch.uint8)
+    segs = (L.CopySegment * len(uniq))()
+    new = {}
+    for i, (k, t) in enumerate(uniq.items()):
+        nb = t.numel() * t.element_size()
+        flat = arena[offs[k]:offs[k] + nb].view(t.dtype)
+        d = torch.as_strided(flat, t.shape, t.stride())
+        new[k] = d
+        segs[i].src, segs[i].dst, segs[i].bytes = t.data_ptr(), d.data_ptr(), nb
+    check(L.lib().hv_copy_segments(segs, len(uniq), stream_ptr()), "hv_copy_segments")
+
+    def rebuild(o):
+        if isinstance(o, Tensor):
+            return new.get(id(o), o)
+        if isinstance(o, dict):
+            return {k: rebuild(v) for k, v in o.items()}
+        if isinstance(o, list):
+            return [rebuild(v) for v in o]
+        if isinstance(o, tuple):
+            return tuple(rebuild(v) for v in o)
+        return o
+    return rebuild(tree)
 
 
 # ---------------------------------------------------------------------------- post-processing
@@ -561,6 +653,20 @@ def preprocess(frames: Tensor, height: int, width: int, *, bgr: bool = True, dty
     check(L.lib().hv_preprocess(frames.data_ptr(), n, h, w, int(bgr), height, width, ms, code, int(nhwc),
                                 out.data_ptr(), stream_ptr()), "hv_preprocess")
     return out.permute(0, 3, 1, 2) if nhwc else out
+
+
+# ---------------------------------------------------------------------------- diagnostics
+KERNEL_FAMILIES = ("gemm_pp256", "glds_128x128", "glds_64x128", "glds_128x64", "glds_64x64", "gemm_regstage",
+                   "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group")
+
+
+def launch_counts(reset: bool = False) -> dict:
+    """Host-side launch counts per kernel family since the last reset (include/hv_tuning.h)."""
+    arr = (C.c_longlong * 16)()
+    L.lib().hv_diag_launch_counts(arr)
+    if reset:
+        L.lib().hv_diag_reset_counts()
+    return {n: int(arr[i]) for i, n in enumerate(KERNEL_FAMILIES)}
 
 
 # ---------------------------------------------------------------------------- debug tracing

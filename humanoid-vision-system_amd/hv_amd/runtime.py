@@ -69,3 +69,42 @@ def require_cuda(x: torch.Tensor, what: str) -> None:
 
 def param_versions(module: torch.nn.Module):
     return tuple((p.data_ptr(), p._version) for p in module.parameters())
+
+
+# Any parameter / buffer / submodule (re)registration anywhere bumps this generation, so a
+# VersionWatch re-walks its module tree only when the tree may have changed (the walk costs
+# ~2.6 ms on the base model; the per-call snapshot ~0.4 ms).
+_REG_GEN = [0]
+
+
+def _bump_generation(*_args):
+    _REG_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_generation)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump_generation)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_generation)
+
+
+# buffers the forward itself writes (mHC monitors, Sinkhorn history): not inputs of the forward
+_OUTPUT_BUFFERS = ("convergence_history", "eigenvalues", "signal_ratio_history", "gradient_norms")
+
+
+class VersionWatch:
+    """Cheap change detector for everything a prepared / captured forward baked in: the
+    storage pointer and in-place version counter of every parameter and input buffer (BN
+    statistics, anchors, ...) of `module`.  In-place updates (optimizer steps, load_state_dict
+    copies), `.data` swaps and `.to()` moves all change the snapshot."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.module = module
+        self._gen = -1
+        self._ts = []
+
+    def snapshot(self):
+        if self._gen != _REG_GEN[0]:
+            self._ts = list(self.module.parameters()) + [
+                b for n, b in self.module.named_buffers() if not n.endswith(_OUTPUT_BUFFERS)]
+            self._gen = _REG_GEN[0]
+        ts = self._ts
+        return tuple([t._version for t in ts]), tuple([t.data_ptr() for t in ts])

@@ -145,13 +145,16 @@ class SinkhornGroupFn(torch.autograd.Function):
     def forward(ctx, group, *raws):
         outs = group.run(list(raws))
         ctx.group = group
+        ctx.set_materialize_grads(False)
         return tuple(o.squeeze(0) if r.dim() == 2 else o for o, r in zip(outs, raws))
 
     @staticmethod
     def backward(ctx, *douts):
         g = ctx.group
-        draws = g.backward([d if d is not None else None for d in douts])
-        return (None,) + tuple(draws)
+        draws = g.backward(list(douts))
+        # a projection no loss depends on gets no gradient at all (None, as the reference's
+        # per-module autograd leaves it): the optimizer then skips that H_res_raw
+        return (None,) + tuple(d if o is not None else None for d, o in zip(draws, douts))
 
 
 # =============================================================================== mHC

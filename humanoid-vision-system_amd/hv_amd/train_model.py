@@ -163,8 +163,9 @@ def encoder_block(blk, x, n, H):
     return TF.DropAddFn.apply(x, h, p, TF.next_seed() if p > 0 else 0)
 
 
-def vit_encoder(enc, x, H):
-    """VisionTransformerEncoder.forward (vit_encoder_decoder.py:277-315) -> CLS [n, D]."""
+def vit_encoder(enc, x, H, features=None, head: bool = True):
+    """VisionTransformerEncoder.forward (vit_encoder_decoder.py:277-315) -> CLS [n, D];
+    `features` (a list) receives the token tensors after the embedding and every block."""
     pe = enc.patch_embed
     t = TF.conv(x, pe.projection)
     n, h, w, d = t.shape
@@ -173,11 +174,15 @@ def vit_encoder(enc, x, H):
     z = TF.VitAssembleFn.apply(t, pe.cls_token, pos)
     L = h * w + 1
     t = TF.RMSNormFn.apply(z.view(n * L, d), pe.norm.scale, pe.norm.eps)
+    if features is not None:
+        features.append(t.view(n, L, d))
     for blk in enc.blocks:
         t = encoder_block(blk, t, n, H)
+        if features is not None:
+            features.append(t.view(n, L, d))
     cls = TF.GatherRowsFn.apply(t, L)
     cls = TF.RMSNormFn.apply(cls, enc.norm.scale, enc.norm.eps)
-    if isinstance(enc.head, nn.Linear):
+    if head and isinstance(enc.head, nn.Linear):
         cls = TF.linear(cls, enc.head)
     return cls
 
@@ -279,17 +284,19 @@ def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection"
     fused = fpn(model.feature_fusion, bb, H)
     head = model.detection_head
     if task == "detection":
-        preds, decoded, logits = {}, {}, {}
+        preds, decoded, logits, dets = {}, {}, {}, {}
         for s, key in enumerate(("fused_small", "fused_medium", "fused_large")):
             lg = head_logits(head.pred_heads[s], fused[key], H)
             logits[s] = lg
             awh = head.anchor_generator.anchors[s].reshape(head.num_anchors, 4)[:, 2:4].contiguous()
             with torch.no_grad():
-                dec, pred = ops.yolo_decode(lg.detach(), head.num_anchors, head.num_classes, awh)
+                dec, pred = ops.yolo_decode(lg.detach(), head.num_anchors, head.num_classes, awh, detections=True)
+            dets[("small_scale", "medium_scale", "large_scale")[s]] = dec.pop("detections")
             preds[f"scale_{s}"] = _PredViewFn.apply(lg, head.num_anchors) if lg.requires_grad else pred
             decoded[f"scale_{s}"] = dec
         out["predictions"] = preds
         out["decoded"] = decoded
+        out["detections"] = dets
         if compute_loss and targets is not None:
             out["loss"] = yolo_loss(head.loss_fn, logits, targets, head.num_anchors)
     out["final_features"] = final_features(model, fused, H)
@@ -333,24 +340,59 @@ def yolo_loss(loss_fn, logits: Dict[int, torch.Tensor], targets, A: int) -> Dict
 
 
 def final_features(model, fused, H):
-    """_extract_final_features (hybrid_vision.py:369-402): GAP x3 -> cat -> mHC -> MLP."""
-    pooled = [ops.channel_mean(fused[k].detach()) for k in ("fused_small", "fused_medium", "fused_large")]
-    # the reference keeps this branch in the graph; its output feeds no loss, so no
-    # gradient reaches it -- computed without autograd history
-    with torch.no_grad():
-        dt = fused["fused_small"].dtype
-        c = torch.cat(pooled, 1).to(dt).contiguous()
-        c = TF.MhcFn.apply(c, H[id(model.final_fusion)].detach(), *[t.detach() for t in (
-            model.final_fusion.H_pre_raw, model.final_fusion.H_post_raw, model.final_fusion.norm_pre.weight,
-            model.final_fusion.norm_pre.bias, model.final_fusion.mlp[0].weight, model.final_fusion.mlp[0].bias,
-            model.final_fusion.mlp[3].weight, model.final_fusion.mlp[3].bias, model.final_fusion.norm_post.weight,
-            model.final_fusion.norm_post.bias)], model.final_fusion,
-            tuple(TF.next_seed() if p > 0 else 0 for p in (model.final_fusion.mlp[2].p, model.final_fusion.mlp[5].p,
-                                                           model.final_fusion.dropout.p)))
-        h = TF.LinearFn.apply(c, model.output_projection[2].weight, model.output_projection[2].bias, "relu", 0.0, 0,
-                              None)
-        return TF.LinearFn.apply(h, model.output_projection[4].weight, model.output_projection[4].bias, "none", 0.0,
-                                 0, torch.float32)
+    """_extract_final_features (hybrid_vision.py:369-402): GAP x3 -> cat -> mHC -> MLP, kept
+    in the autograd graph as in the reference: a loss on final_features trains final_fusion
+    and output_projection (the detection loss does not reach them, so they get no gradient)."""
+    pooled = [_ChannelMeanFn.apply(fused[k]) for k in ("fused_small", "fused_medium", "fused_large")]
+    dt = fused["fused_small"].dtype
+    ff = model.final_fusion
+    c = _CatCastFn.apply(dt, *pooled)
+    c = TF.MhcFn.apply(c, H[id(ff)], ff.H_pre_raw, ff.H_post_raw, ff.norm_pre.weight, ff.norm_pre.bias,
+                       ff.mlp[0].weight, ff.mlp[0].bias, ff.mlp[3].weight, ff.mlp[3].bias, ff.norm_post.weight,
+                       ff.norm_post.bias, ff,
+                       tuple(TF.next_seed() if p > 0 else 0 for p in (ff.mlp[2].p, ff.mlp[5].p, ff.dropout.p)))
+    h = TF.LinearFn.apply(c, model.output_projection[2].weight, model.output_projection[2].bias, "relu", 0.0, 0,
+                          None)
+    return TF.LinearFn.apply(h, model.output_projection[4].weight, model.output_projection[4].bias, "none", 0.0,
+                             0, torch.float32)
+
+
+class _ChannelMeanFn(torch.autograd.Function):
+    """Global average pool of an NHWC map -> fp32 [n, c] (hv_channel_mean); backward spreads
+    g / (h*w) over the pixels."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.meta = (x.shape, x.dtype)
+        return ops.channel_mean(x.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        shape, dt = ctx.meta
+        n, c = shape[0], shape[-1]
+        hw = 1
+        for d in shape[1:-1]:
+            hw *= d
+        zero = torch.zeros(shape, device=g.device, dtype=dt)
+        return ops.add_rowvec(zero, (g / hw).contiguous())
+
+
+class _CatCastFn(torch.autograd.Function):
+    """cat(pooled, dim 1) in the compute dtype (the [n, 1792] final-fusion input)."""
+
+    @staticmethod
+    def forward(ctx, dt, *xs):
+        ctx.widths = [x.shape[1] for x in xs]
+        return torch.cat(xs, 1).to(dt).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.float()
+        outs, o = [], 0
+        for w in ctx.widths:
+            outs.append(g[:, o:o + w].contiguous())
+            o += w
+        return (None, *outs)
 
 
 def yolo_loss_api(loss_fn, predictions: Dict[str, torch.Tensor], targets) -> Dict[str, Any]:

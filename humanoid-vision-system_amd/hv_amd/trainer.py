@@ -74,16 +74,28 @@ class GradBuckets:
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self._pending: List = []
         self._ready = [0] * len(self.buckets)
-        self._hooks = []
+        # which parameters received a gradient this step: the optimizer skips the others like
+        # torch.optim skips grad=None (optimizer.py:144) -- the flat views are never None
+        self.received = [False] * len(self.params)
+        self._index = {id(p): i for i, p in enumerate(self.params)}
+        # the engine runs a leaf's hooks even when its producer returned None for it (e.g. the
+        # grouped Sinkhorn's unused final-fusion projection), so receipt is read from the
+        # gradient itself in a tensor hook; bucket readiness stays on the post-accumulate hook
+        self._hooks = [p.register_hook(self._flag_hook(i)) for i, p in enumerate(self.params)]
         if self.world > 1:
-            for p in self.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            self._hooks += [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def _span(self, i: int):
         b = self.buckets[i]
         lo = min(self.offsets[id(p)] for p in b)
         hi = max(self.offsets[id(p)] + p.numel() for p in b)
         return lo, hi
+
+    def _flag_hook(self, idx: int):
+        def hook(g):
+            if g is not None:
+                self.received[idx] = True
+        return hook
 
     def _on_grad(self, p: Tensor):
         i = self.bucket_of[id(p)]
@@ -100,6 +112,7 @@ class GradBuckets:
             if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
                 p.grad = self.flat[off:off + p.numel()].view_as(p)
         self.flat.zero_()
+        self.received = [False] * len(self.params)
         self._ready = [0] * len(self.buckets)
         self._pending = []
 
@@ -132,13 +145,14 @@ class FusedAdamW:
         self.exp_avg = [torch.zeros_like(p) for _, p in self.named]
         self.exp_avg_sq = [torch.zeros_like(p) for _, p in self.named]
         self.step_count = 0
+        self.param_steps = [0] * len(self.named)   # per-parameter steps (reference state['step'])
         self.norms = torch.zeros(len(self.max_norms), device=dev, dtype=torch.float32)
         self.coefs = torch.ones(len(self.max_norms), device=dev, dtype=torch.float32)
         self._table = None
         self._key = None
         self.device = dev
 
-    def _build(self):
+    def _build(self, active):
         lib = L.lib()
         ents = (L.ParamEntry * len(self.named))()
         blk = 0
@@ -147,7 +161,7 @@ class FusedAdamW:
                 raise TypeError(f"{name}: FusedAdamW needs contiguous fp32 parameters")
             e = ents[i]
             e.param = p.data_ptr()
-            e.grad = p.grad.data_ptr() if p.grad is not None else None
+            e.grad = p.grad.data_ptr() if p.grad is not None and active[i] else None
             e.exp_avg, e.exp_avg_sq = self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr()
             e.n = p.numel()
             e.group = mhc_group(name)
@@ -158,13 +172,18 @@ class FusedAdamW:
         self._table = upload_table(ents, self.device)
         self._work = torch.empty(2 * blk, device=self.device, dtype=torch.float32)
 
-    def step(self, clip: bool = True):
-        key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named)
+    def step(self, clip: bool = True, active: Optional[Sequence[bool]] = None):
+        """active[i] False = parameter i got no gradient this step: no clipping contribution,
+        no weight decay, no moment update (torch.optim's grad-is-None skip)."""
+        active = tuple(active) if active is not None else (True,) * len(self.named)
+        key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named) + active
         if key != self._key:
-            self._build()
+            self._build(active)
             self._key = key
         lib = L.lib()
         self.step_count += 1
+        for i, a in enumerate(active):
+            self.param_steps[i] += int(a)
         coefs = None
         if clip:
             mx = (C.c_float * len(self.max_norms))(*self.max_norms)
@@ -178,12 +197,19 @@ class FusedAdamW:
 
     # ---- torch.optim-compatible state (checkpoints load into / from torch.optim.AdamW)
     def state_dict(self) -> Dict:
-        state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": self.exp_avg[i],
-                     "exp_avg_sq": self.exp_avg_sq[i]} for i in range(len(self.named))}
+        """torch.optim layout; loads into torch.optim.AdamW and into the reference
+        ManifoldAwareOptimizer (optimizer.py:31-70: its param group also carries mhc_params and
+        manifold_update_freq, read by step() at :125).  Parameters that never received a
+        gradient have no state, as in torch."""
+        state = {i: {"step": torch.tensor(float(self.param_steps[i])), "exp_avg": self.exp_avg[i],
+                     "exp_avg_sq": self.exp_avg_sq[i]} for i in range(len(self.named)) if self.param_steps[i] > 0}
         return {"state": state,
                 "param_groups": [{"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
                                   "weight_decay": self.wd, "amsgrad": False, "maximize": False,
                                   "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                                  "mhc_params": {"mhc_lr_scale": 0.5, "project_iterations": 20,
+                                                 "strict_double_stochastic": True},
+                                  "manifold_update_freq": 100,
                                   "params": list(range(len(self.named)))}]}
 
     def load_state_dict(self, sd: Dict) -> None:
@@ -196,7 +222,8 @@ class FusedAdamW:
                 continue
             self.exp_avg[i].copy_(st["exp_avg"])
             self.exp_avg_sq[i].copy_(st["exp_avg_sq"])
-            steps.append(int(float(st["step"])))
+            self.param_steps[i] = int(float(st["step"]))
+            steps.append(self.param_steps[i])
         if steps:
             self.step_count = max(steps)
 
@@ -226,6 +253,33 @@ class HVTrainer:
         self.broadcast_buffers = broadcast_buffers and self.world > 1
         if self.world > 1:                         # DDP construction: replicas start identical
             self._broadcast(list(model.parameters()) + list(model.buffers()))
+        self._buf_flats = self._flatten_buffers() if self.broadcast_buffers else []
+
+    def _flatten_buffers(self):
+        """Rebind every buffer of the model as a view of one flat tensor per dtype, so the
+        per-step DDP buffer broadcast (broadcast_buffers=True) is one collective per dtype
+        with no packing or unpacking copies.  In-place updates (BN running statistics, mHC
+        monitors) write through the views; load_state_dict copies into them."""
+        by_dtype: Dict[torch.dtype, list] = {}
+        for mod in self.model.modules():
+            for name, b in mod._buffers.items():
+                if b is not None:
+                    by_dtype.setdefault(b.dtype, []).append((mod, name, b))
+        flats = []
+        for dt, entries in by_dtype.items():
+            total = sum(b.numel() for _, _, b in entries)
+            flat = torch.empty(total, device=entries[0][2].device, dtype=dt)
+            off = 0
+            with torch.no_grad():
+                for mod, name, b in entries:
+                    v = flat[off:off + b.numel()].view_as(b)
+                    v.copy_(b)
+                    mod._buffers[name] = v
+                    off += b.numel()
+            flats.append(flat)
+        from .runtime import _bump_generation
+        _bump_generation()                      # buffers were rebound: VersionWatch re-walks
+        return flats
 
     def _broadcast(self, tensors):
         float_ts = [t for t in tensors if t.is_floating_point()]
@@ -243,14 +297,14 @@ class HVTrainer:
 
     def step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
         self.model.train()
-        if self.broadcast_buffers:
-            self._broadcast([b for b in self.model.buffers() if b.is_floating_point()])
+        for flat in self._buf_flats:               # DDP broadcast_buffers: rank 0's buffers
+            dist.broadcast(flat, 0, group=self.group)
         self.grads.zero()
         out = self.model(images, targets=targets, compute_loss=True)
         loss = out["loss"]
         loss["total_loss"].backward()
         self.grads.finish()
-        self.opt.step(clip=True)
+        self.opt.step(clip=True, active=self.grads.received)
         return loss
 
 
@@ -259,11 +313,16 @@ def save_checkpoint(path: str, model, trainer: Optional["HVTrainer"] = None, epo
                     best_val_loss: float = float("inf"), experiment_name: str = "hv_amd") -> None:
     """Checkpoint in the reference trainer's format (mhc_trainer.py:595-627): the same keys,
     model_state_dict in the reference parameter/buffer layout, optimizer_state_dict in
-    torch.optim.AdamW layout (scheduler/scaler states empty: the build uses neither)."""
+    torch.optim.AdamW layout (+ the reference optimizer's group keys), an empty scheduler state
+    (LRScheduler.load_state_dict accepts it) and the state of an enabled GradScaler at its
+    initial scale (the build uses no loss scaling: bf16 needs none), which
+    GradScaler(enabled=True).load_state_dict accepts where an empty dict raises."""
     import time
     ck = {"epoch": epoch, "global_step": global_step, "model_state_dict": model.state_dict(),
           "optimizer_state_dict": trainer.opt.state_dict() if trainer is not None else {},
-          "scheduler_state_dict": {}, "scaler_state_dict": {}, "config": config or {}, "history": history or {},
+          "scheduler_state_dict": {},
+          "scaler_state_dict": {"scale": 65536.0, "growth_factor": 2.0, "backoff_factor": 0.5,
+                                "growth_interval": 2000, "_growth_tracker": 0}, "config": config or {}, "history": history or {},
           "best_val_loss": best_val_loss, "experiment_name": experiment_name, "timestamp": time.time()}
     torch.save(ck, path)
 

@@ -91,7 +91,7 @@ class TransformerEncoderBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "TransformerEncoderBlock")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             from .runtime import resolve_dtype
             n, L, D = x.shape
@@ -120,31 +120,48 @@ class VisionTransformerEncoder(nn.Module):
         self.norm = RMSNorm(embed_dim)
         self.head = nn.Linear(embed_dim, num_classes) if num_classes > 0 else nn.Identity()
 
-    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_nhwc(self, x: torch.Tensor, features=None, head: bool = True) -> torch.Tensor:
+        """x NHWC -> CLS [n, D] (through the head if `head`); `features` (a list) receives the
+        token tensors [n, L, D] after the patch embedding and after every block."""
         t = self.patch_embed.forward_nhwc(x)                 # [n, L, D]
         n, L, D = t.shape
+        if features is not None:
+            features.append(t)
         t = t.view(n * L, D)
         for blk in self.blocks:
             t = blk.forward_tokens(t, n)
+            if features is not None:
+                features.append(t.view(n, L, D))
         cls = ops.rmsnorm(ops.gather_rows(t, L), ops.f32(self.norm.scale))   # only CLS survives
-        if isinstance(self.head, nn.Linear):
+        if head and isinstance(self.head, nn.Linear):
             w, b = linear_prep(self.head, cls.dtype)
             cls = ops.gemm(cls, w, bias=b)
         return cls
 
     def forward(self, x: torch.Tensor, return_features: bool = False):
+        """vit_encoder_decoder.py:277-315: output, or (output, [patch tokens, block outputs...])."""
         require_cuda(x, "VisionTransformerEncoder")
-        if return_features:
-            raise NotImplementedError("return_features is not on the HybridVision path")
-        if self.training and torch.is_grad_enabled():
+        feats = [] if return_features else None
+        if self.training:
             from . import train_model as TM
             from .runtime import resolve_dtype
-            return TM.vit_encoder(self, TM.nhwc_in(x, resolve_dtype(self.patch_embed.mhc_enhance)), TM.module_H(self))
-        with ctx_scope(self) as ctx:
-            return self.forward_nhwc(to_nhwc(x, ctx.dtype))
+            out = TM.vit_encoder(self, TM.nhwc_in(x, resolve_dtype(self.patch_embed.mhc_enhance)), TM.module_H(self),
+                                 features=feats)
+        else:
+            with ctx_scope(self) as ctx:
+                out = self.forward_nhwc(to_nhwc(x, ctx.dtype), feats)
+        return (out, feats) if return_features else out
 
-    def extract_features(self, x):
-        return self.forward(x)
+    def extract_features(self, x: torch.Tensor) -> torch.Tensor:
+        """vit_encoder_decoder.py:317-333: the normalised CLS token, without the head."""
+        require_cuda(x, "VisionTransformerEncoder")
+        if self.training:
+            from . import train_model as TM
+            from .runtime import resolve_dtype
+            return TM.vit_encoder(self, TM.nhwc_in(x, resolve_dtype(self.patch_embed.mhc_enhance)), TM.module_H(self),
+                                  head=False)
+        with ctx_scope(self) as ctx:
+            return self.forward_nhwc(to_nhwc(x, ctx.dtype), head=False)
 
 
 class HybridVisionEncoder(nn.Module):
@@ -184,7 +201,7 @@ class HybridVisionEncoder(nn.Module):
 
     def forward(self, cnn_features: torch.Tensor) -> torch.Tensor:
         require_cuda(cnn_features, "HybridVisionEncoder")
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             from . import train_model as TM
             from .runtime import resolve_dtype
             x = TM.nhwc_in(cnn_features, resolve_dtype(self.fusion_mhc))

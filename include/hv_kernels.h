@@ -113,21 +113,6 @@ typedef struct hv_gemm_desc {
 } hv_gemm_desc;
 
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
-/* path selection for A/B tests: 1 = register-staged kernel only, 0 = default (LDS-DMA when eligible) */
-void hv_gemm_set_path(int regstage_only);
-/* 256x256 ping-pong LDS-DMA kernel selection: 0 off, 1 by shape (default), 2 whenever eligible */
-void hv_gemm_set_big_tile(int mode);
-/* 64x64-tile LDS-DMA kernel for small grids: 1 on (default), 0 off */
-void hv_gemm_set_small_tile(int mode);
-/* 128x128 tiles for the training epilogues (epi_mode 1/2): 0 = 64x128 only (default), 1 on */
-void hv_gemm_set_train128(int on);
-/* LDS-staged coalesced epilogue for the LDS-DMA kernels (inference modes): 1 on (default), 0 off */
-void hv_gemm_set_staged_epilogue(int on);
-/* deeper LDS-DMA rings (4 / 3 buffers) for the 64x64 / 64x128 / 128x64 tiles: 1 on (default), 0 = 2 */
-void hv_gemm_set_deep_ring(int on);
-/* convolutions with K % 64 != 0 (channels % 8 == 0) on the LDS-DMA kernel: 0 off (default), 1 on */
-void hv_gemm_set_conv_ktail(int on);
-
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
  * RMSNorm :449-456 eps 1e-8).
@@ -184,8 +169,6 @@ typedef struct hv_mhc_fused_args {
   void* out;            /* [T, D] */
 } hv_mhc_fused_args;
 int hv_mhc_fused_supported(int D, int Hd, int dtype);
-/* 1: also dispatch (256, 512) to the fused kernel (off by default: slower than unfused) */
-void hv_mhc_fused_enable_wide(int on);
 int hv_mhc_fused(const hv_mhc_fused_args* args, hv_stream_t stream);
 
 /* y[N] = W[N, K] x[K] + b  (fp32; folded mHC bias c1 = W1 u + b1) */
@@ -307,6 +290,24 @@ int hv_attention_mfma(const void* q, const void* k, const void* v, void* vt_work
 int hv_gather_rows(int dtype, const void* x, long stride_rows, int n, int c, void* y,
                    hv_stream_t stream);
 
+/* General MultiHeadManifoldAttention core (manifold_layers.py:404-427): q [n, Lq, heads*hd],
+   k / v [n, Lk, heads*hd] (cross-attention allowed), optional key_padding_mask [n, Lk] (1 =
+   masked, -inf before the softmax), optional weights [n, heads, Lq, Lk] fp32 (need_weights).
+   hd in {16, 32, 64}.  Rows with every key masked are NaN, as in the reference. */
+int hv_attention_general(int dtype, const void* q, const void* k, const void* v,
+                         const unsigned char* key_padding_mask, void* out, float* weights, int n,
+                         int Lq, int Lk, int heads, int hd, float sm_scale, hv_stream_t stream);
+
+/* Batched device-to-device copy of `count` byte ranges in one launch per 64 ranges (the
+   engine's owned copies of a graph replay's outputs: InferenceEngine.infer returns fresh
+   tensors per call, engine.py:251-317, while a replay rewrites the captured buffers). */
+typedef struct hv_copy_segment {
+  const void* src;
+  void* dst;
+  long long bytes;
+} hv_copy_segment;
+int hv_copy_segments(const hv_copy_segment* segs /* host array */, int count, hv_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * YOLO decode (yolo_head.py:196-201 permute + YOLODecoder.forward :220-294, shims S4/S5).
  * logits: NHWC [n, h, w, A*(5+nc)] (fp32|bf16).  Writes fp32 predictions [n, A, h, w, 5+nc],
@@ -316,7 +317,11 @@ int hv_gather_rows(int dtype, const void* x, long stride_rows, int n, int c, voi
 int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, int nc,
                    const float* anchor_wh /* [A, 2] */, float* predictions, float* boxes,
                    float* scores, float* class_scores, int64_t* class_indices,
-                   float* objectness, hv_stream_t stream);
+                   float* objectness,
+                   float* detections /* optional [n, A, h, w, 5+nc]: xyxy box, objectness,
+                                        sigmoid class probabilities (the per-scale layout
+                                        DetectionPostprocessor reads, postprocessing.py:234-244) */,
+                   hv_stream_t stream);
 
 
 

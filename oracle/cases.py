@@ -18,8 +18,20 @@ MODEL_CASES = [  # (tag, tiny, family, size, batch, subsample rows of scale_0)
     ("tiny_init_224_b2", True, "init", 224, 2, 1),
     ("base_wc_224_b2", False, "wc", 224, 2, 1),
     ("base_wc_512_b1", False, "wc", 512, 1, 4),
-    ("base_wc_640_b1", False, "wc", 640, 1, 4),
+    ("base_wc_640_b2", False, "wc", 640, 2, 4),     # image 0 == the former 640 B=1 input
+    ("base_wc_1024_b1", False, "wc", 1024, 1, 8),   # config D size (ViT over 1025 tokens)
 ]
+TRAIN_CASES = [  # (tag, tiny, size, batch, target seed)
+    ("tiny_64_b2", True, 64, 2, 3),
+    ("base_224_b2", False, 224, 2, 3),               # config C's model (base), row T
+]
+
+
+def grad_probe(name: str, numel: int) -> torch.Tensor:
+    """Fixed random direction per parameter: <grad, probe> / sqrt(numel) pins the gradient's
+    direction where only its norm would be too weak (base-model fixtures cannot store 353M
+    gradient entries)."""
+    return torch.randn(numel, generator=gen_seed(zlib.crc32(name.encode()), 5), dtype=torch.float64)
 
 
 def gen_seed(*key) -> torch.Generator:

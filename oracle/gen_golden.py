@@ -238,6 +238,20 @@ def gen_blocks(ml, vb, ve, yh):
     x = torch.randn(2, 50, 256, generator=gen_seed(256, 50))
     with torch.no_grad():
         save("encblock_256_n50", x=x, y=m(x))
+    # attention beyond the encoder's self-attention call: cross-attention (Lq != Lk), a key
+    # padding mask and need_weights (manifold_layers.py:386-434)
+    torch.manual_seed(0)
+    m = ml.MultiHeadManifoldAttention(256, num_heads=8).eval()
+    W.load_formula_weights(m, fam)
+    q = torch.randn(2, 7, 256, generator=gen_seed(256, 7, 1))
+    kv = torch.randn(2, 11, 256, generator=gen_seed(256, 11, 2))
+    mask = torch.zeros(2, 11, dtype=torch.bool)
+    mask[1, 8:] = True
+    mask[0, ::3] = True
+    with torch.no_grad():
+        out, w = m(q, kv, kv, key_padding_mask=mask, need_weights=True)
+        out_self, _ = m(q, q, q)
+    save("attn_cross_mask", q=q, kv=kv, mask=mask, out=out, weights=w, out_self=out_self)
     # decoder on random logits
     dec = yh.YOLODecoder()
     ag = yh.YOLOAnchorGenerator()
@@ -295,49 +309,61 @@ def gen_model(hv, only=None):
 
 
 # ------------------------------------------------------------------ G5 training step
-def gen_train(hv):
-    """Tiny model, training mode (BN batch statistics), every dropout p=0 so the step is
-    deterministic, YOLOLoss on synthetic targets (hv_amd/targets.py builder), backward in
-    fp32 and fp64.  Records loss components, predictions and per-parameter gradient norms
-    plus full gradients of a few small parameters."""
+def gen_train(hv, only=None):
+    """Training mode (BN batch statistics), every dropout p=0 so the step is deterministic,
+    YOLOLoss on synthetic targets (hv_amd/targets.py builder), backward in fp32 and fp64.
+    Records loss components, predictions, per-parameter gradient norms and gradient probes
+    (<grad, fixed random direction>, oracle/cases.py:grad_probe), plus full gradients of a few
+    small parameters.  Cases: oracle/cases.py TRAIN_CASES (tiny 64 B2; base 224 B2 = config C's
+    model)."""
     print("G5 train")
+    import json
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "humanoid-vision-system_amd"))
     from hv_amd.targets import synthetic_targets
-    B, S = 2, 64
-    _TINY["on"] = True
-    torch.manual_seed(0)
-    model = hv.HybridVisionSystem({"image_size": S})
-    _TINY["on"] = False
-    W.load_formula_weights(model, "wc")
-    for mod in model.modules():
-        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
-            mod.p = 0.0
-    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
-    tg = synthetic_targets(B, S, seed=3)
-    rec = {"B": B, "S": S}
-    for tag, dt in (("", torch.float32), ("_f64", torch.float64)):
-        m = model.to(dt).train()
-        m.zero_grad()
-        out = m(x.to(dt), targets=[t.to(dt) for t in tg], compute_loss=True)
-        loss = out["loss"]
-        loss["total_loss"].backward()
-        rec["total_loss" + tag] = loss["total_loss"].detach().float()
-        for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
-            rec[k + tag] = torch.tensor(float(loss[k]))
-        for sidx in range(3):
-            rec[f"pred{sidx}" + tag] = out["predictions"][f"scale_{sidx}"].detach().float()
-        names = [n for n, p in m.named_parameters()]
-        rec["grad_norm" + tag] = torch.tensor([p.grad.double().norm().item() if p.grad is not None else -1.0
-                                               for p in m.parameters()])
-        for n, p in m.named_parameters():
-            if p.grad is not None and p.numel() <= 4096 and ("norm_post" in n or "bn." in n or "H_res_raw" in n
-                                                              and p.numel() <= 1024 or "pred_conv.bias" in n):
-                rec["g:" + n + tag] = p.grad.detach().float()
-    import json
-    with open(os.path.join(OUT, "train_tiny_param_names.json"), "w") as f:
-        json.dump(names, f)
-    save("train_tiny_64_b2", **rec)
-    model.float()
+    from oracle.cases import TRAIN_CASES, grad_probe
+    for tag, tiny, S, B, tseed in TRAIN_CASES:
+        if only and tag not in only:
+            continue
+        t0 = time.time()
+        _TINY["on"] = tiny
+        torch.manual_seed(0)
+        model = hv.HybridVisionSystem({"image_size": S})
+        _TINY["on"] = False
+        W.load_formula_weights(model, "wc")
+        for mod in model.modules():
+            if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+                mod.p = 0.0
+        x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+        tg = synthetic_targets(B, S, seed=tseed)
+        rec = {"B": B, "S": S, "target_seed": tseed, "threads": torch.get_num_threads()}
+        for sfx, dt in (("", torch.float32), ("_f64", torch.float64)):
+            m = model.to(dt).train()
+            m.zero_grad(set_to_none=True)
+            out = m(x.to(dt), targets=[t.to(dt) for t in tg], compute_loss=True)
+            loss = out["loss"]
+            loss["total_loss"].backward()
+            rec["total_loss" + sfx] = loss["total_loss"].detach().float()
+            for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
+                rec[k + sfx] = torch.tensor(float(loss[k]))
+            for sidx in range(3):
+                rec[f"pred{sidx}" + sfx] = out["predictions"][f"scale_{sidx}"].detach().float()
+            names = [n for n, p in m.named_parameters()]
+            rec["grad_norm" + sfx] = torch.tensor([p.grad.double().norm().item() if p.grad is not None else -1.0
+                                                   for p in m.parameters()])
+            rec["grad_probe" + sfx] = torch.tensor(
+                [float(p.grad.double().flatten() @ grad_probe(n, p.numel())) / math.sqrt(p.numel())
+                 if p.grad is not None else 0.0 for n, p in m.named_parameters()])
+            for n, p in m.named_parameters():
+                if p.grad is not None and p.numel() <= 4096 and ("norm_post" in n or "bn." in n or "H_res_raw" in n
+                                                                  and p.numel() <= 1024 or "pred_conv.bias" in n):
+                    rec["g:" + n + sfx] = p.grad.detach().float()
+            del out, loss
+        kind = "tiny" if tiny else "base"
+        with open(os.path.join(OUT, f"train_{kind}_param_names.json"), "w") as f:
+            json.dump(names, f)
+        save(f"train_{tag}", **rec)
+        print(f"  {tag}: {time.time() - t0:.1f}s")
+        del model, m
 
 
 # ------------------------------------------------------------------ G6 post-processing
@@ -362,6 +388,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train,nms")
     ap.add_argument("--models", default="")
+    ap.add_argument("--trains", default="")
     a = ap.parse_args()
     torch.set_num_threads(8)
     ml, vb, ve, yh, hv = apply_shims()
@@ -377,7 +404,7 @@ def main():
     if "layout" in parts:
         gen_layout(hv)
     if "train" in parts:
-        gen_train(hv)
+        gen_train(hv, [m for m in a.trains.split(",") if m])
     if "nms" in parts:
         gen_nms(yh)
 

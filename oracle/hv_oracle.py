@@ -221,15 +221,26 @@ def interp_positions(pe: Tensor, n: int) -> Tensor:
 
 
 def attention(sd, p: str, x: Tensor, it: int, heads: int = 8) -> Tensor:
-    """MultiHeadManifoldAttention.forward (manifold_layers.py:386-434), eval, no mask."""
-    B, N, D = x.shape
+    """MultiHeadManifoldAttention.forward (manifold_layers.py:386-434), eval, self-attention."""
+    return attention_general(sd, p, x, x, x, it, heads)[0]
+
+
+def attention_general(sd, p: str, query: Tensor, key: Tensor, value: Tensor, it: int, heads: int = 8,
+                      key_padding_mask: Optional[Tensor] = None):
+    """MultiHeadManifoldAttention.forward (manifold_layers.py:386-434), eval: q/k/v mHC
+    projections (:400-402), scores * head_dim^-0.5 (:410), key_padding_mask filled with -inf
+    (:413-417), softmax (:420), PV, out_proj (:430).  Returns (out, attn_weights)."""
+    B, Lq, D = query.shape
     hd = D // heads
-    q = mhc(sd, p + "q_proj.", x, it).reshape(B, N, heads, hd).transpose(1, 2)
-    k = mhc(sd, p + "k_proj.", x, it).reshape(B, N, heads, hd).transpose(1, 2)
-    v = mhc(sd, p + "v_proj.", x, it).reshape(B, N, heads, hd).transpose(1, 2)
-    w = torch.softmax((q @ k.transpose(-2, -1)) * hd ** -0.5, dim=-1)
-    o = (w @ v).transpose(1, 2).reshape(B, N, D)
-    return mhc(sd, p + "out_proj.", o, it)
+    q = mhc(sd, p + "q_proj.", query, it).reshape(B, Lq, heads, hd).transpose(1, 2)
+    k = mhc(sd, p + "k_proj.", key, it).reshape(B, -1, heads, hd).transpose(1, 2)
+    v = mhc(sd, p + "v_proj.", value, it).reshape(B, -1, heads, hd).transpose(1, 2)
+    s = (q @ k.transpose(-2, -1)) * hd ** -0.5
+    if key_padding_mask is not None:
+        s = s.masked_fill(key_padding_mask.unsqueeze(1).unsqueeze(2), float("-inf"))
+    w = torch.softmax(s, dim=-1)
+    o = (w @ v).transpose(1, 2).reshape(B, Lq, D)
+    return mhc(sd, p + "out_proj.", o, it), w
 
 
 def encoder_block(sd, p: str, x: Tensor, it: int) -> Tensor:

@@ -1,5 +1,5 @@
 """CPU-side checks: the C-ABI library loads and exports every entry point declared in
-include/hv_kernels.h; the host module surface mirrors the reference (state_dict layout,
+include/hv_kernels.h (drop-in ABI) and include/hv_tuning.h (A/B knobs, launch counters); the host module surface mirrors the reference (state_dict layout,
 constructor call forms); the product path refuses to run without the HIP path."""
 import json
 import os
@@ -12,7 +12,7 @@ from conftest import GOLDEN, MODEL_CFG, ROOT
 
 
 def _declared():
-    src = open(os.path.join(ROOT, "include", "hv_kernels.h")).read()
+    src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("hv_kernels.h", "hv_tuning.h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:int|size_t|void)\s+(hv_\w+)\s*\(", src, flags=re.M)))
 

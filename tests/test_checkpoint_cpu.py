@@ -29,6 +29,7 @@ def test_optimizer_state_roundtrip_with_torch_adamw(tmp_path):
     for t in opt.exp_avg + opt.exp_avg_sq:
         t.copy_(torch.rand_like(t))
     opt.step_count = 7
+    opt.param_steps = [7, 7]
     ref = torch.optim.AdamW([p for _, p in named], lr=1.0)
     ref.load_state_dict(opt.state_dict())
     sd = ref.state_dict()
@@ -55,3 +56,34 @@ def test_checkpoint_file_roundtrip(tmp_path):
         assert torch.equal(a, b), k
     assert set(ck) >= {"epoch", "global_step", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict",
                        "scaler_state_dict", "config", "history", "best_val_loss", "experiment_name", "timestamp"}
+
+
+def test_checkpoint_loads_into_reference_trainer_state_types(tmp_path):
+    """The reference trainer's load_checkpoint (mhc_trainer.py:641-647) feeds the optimizer,
+    scheduler and scaler states to torch objects: the scaler state must be accepted by an
+    enabled GradScaler and the param group must carry the reference optimizer's own keys
+    (optimizer.py:55-70, read by its step() at :125)."""
+    from hv_amd.trainer import FusedAdamW, save_checkpoint
+    torch.manual_seed(0)
+    named = [("a.mhc.w", torch.randn(10, requires_grad=True)), ("b.conv.weight", torch.randn(3, 4, requires_grad=True))]
+    opt = FusedAdamW(named)
+    opt.param_steps = [3, 0]                         # b never received a gradient
+    sd = opt.state_dict()
+    assert list(sd["state"]) == [0]
+    g = sd["param_groups"][0]
+    assert g["manifold_update_freq"] == 100 and g["mhc_params"]["project_iterations"] == 20
+
+    class _T:
+        pass
+    tr = _T()
+    tr.opt = opt
+    m = torch.nn.Linear(2, 2)
+    path = str(tmp_path / "ck.pt")
+    save_checkpoint(path, m, tr)
+    ck = torch.load(path, weights_only=True)
+    sc = torch.amp.GradScaler("cpu", enabled=True)
+    sc.load_state_dict(ck["scaler_state_dict"])
+    assert sc.get_scale() == 65536.0
+    ref = torch.optim.AdamW([p for _, p in named], lr=1.0)
+    ref.load_state_dict(ck["optimizer_state_dict"])
+    assert ref.param_groups[0]["manifold_update_freq"] == 100

@@ -1,7 +1,10 @@
 """Data-parallel gradient path of the trainer on CPU with gloo, world_size 2:
-bucketed, hook-driven all-reduce must produce the rank-average of the per-rank gradients,
-unused-parameter buckets must still be reduced, and buffer broadcast must make replicas
-identical (DDP broadcast_buffers semantics)."""
+bucketed, hook-driven all-reduce must produce the rank-average of the per-rank gradients and
+unused-parameter buckets must still be reduced (GradBuckets); HVTrainer itself must make the
+replicas identical at construction (parameter + buffer broadcast), broadcast rank 0's
+buffers before every step (DDP broadcast_buffers, BN statistics per replica), average the
+gradients over a nested module tree, and hand the optimizer the per-parameter 'received a
+gradient' flags."""
 import os
 import socket
 import sys
@@ -107,3 +110,103 @@ def test_mhc_group_assignment():
     assert mhc_group("final_fusion.H_res_raw") == 0          # 'H_' in name
     assert mhc_group("backbone.stem.0.conv.weight") == 1
     assert mhc_group("detection_head.pred_heads.0.pred_conv.bias") == 1
+
+
+class TrainNet(torch.nn.Module):
+    """A nested module tree with BN buffers, an mHC-named branch and an unused parameter,
+    called the way HVTrainer calls HybridVisionSystem (images, targets=, compute_loss=)."""
+
+    def __init__(self):
+        super().__init__()
+        self.stem = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.BatchNorm2d(8),
+                                        torch.nn.SiLU())
+        self.block = torch.nn.ModuleDict({"mhc": torch.nn.Linear(8, 8), "bn": torch.nn.BatchNorm1d(8)})
+        self.unused = torch.nn.Linear(3, 3)
+
+    def forward(self, x, targets=None, compute_loss=False):
+        h = self.stem(x).mean(dim=(2, 3))
+        y = self.block["bn"](self.block["mhc"](h))
+        return {"loss": {"total_loss": (y - targets).pow(2).mean()}}
+
+
+def _trainer_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, PKG]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hv_amd.trainer import HVTrainer
+        torch.manual_seed(rank)                    # replicas start DIFFERENT
+        net = TrainNet()
+        with torch.no_grad():
+            for m in net.modules():
+                if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                    m.running_mean.fill_(float(rank + 1))
+        tr = HVTrainer(net, bucket_mb=1)
+        calls = []
+        tr.opt.step = lambda clip=True, active=None: calls.append(list(active))
+        init = {n: p.detach().clone().numpy() for n, p in net.named_parameters()}
+        bufs0 = {n: b.detach().clone().numpy() for n, b in net.named_buffers()}
+        res = []
+        for step in range(2):
+            if rank == 1:                          # diverge the replica's buffers: rank 0's win
+                with torch.no_grad():
+                    net.block["bn"].running_var.fill_(7.0)
+            torch.manual_seed(100 + 10 * rank + step)
+            x = torch.randn(4, 3, 6, 6)
+            tgt = torch.randn(4, 8)
+            tr.step(x, tgt)
+            res.append({"grads": {n: p.grad.detach().clone().numpy() for n, p in net.named_parameters()},
+                        "bufs": {n: b.detach().clone().numpy() for n, b in net.named_buffers()},
+                        "x": x.numpy(), "t": tgt.numpy()})
+        q.put((rank, init, bufs0, res, calls, [n for n, _ in tr.opt.named]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_hvtrainer_ddp_broadcast_and_average():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted([q.get(timeout=180) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, init0, buf0, res0, calls0, names), (_, init1, buf1, res1, calls1, _) = results
+    torch.manual_seed(0)
+    ref_init = {n: p.detach().numpy() for n, p in TrainNet().named_parameters()}
+    for n in ref_init:                                    # construction: rank 0's parameters
+        torch.testing.assert_close(torch.from_numpy(init0[n]), torch.from_numpy(ref_init[n]))
+        torch.testing.assert_close(torch.from_numpy(init1[n]), torch.from_numpy(ref_init[n]))
+    for n in buf0:                                        # construction: rank 0's buffers
+        torch.testing.assert_close(torch.from_numpy(buf1[n]), torch.from_numpy(buf0[n]))
+    # reference: one replica on rank 0's state, each rank's batch with rank 0's buffers
+    ref = TrainNet()
+    ref.load_state_dict({**{k: torch.from_numpy(v) for k, v in init0.items()},
+                         **{k: torch.from_numpy(v) for k, v in buf0.items()}})
+    ref.train()
+    for step in range(2):
+        start = {k: v.clone() for k, v in ref.state_dict().items()}
+        gsum, bufs = None, []
+        for r, res in ((0, res0), (1, res1)):
+            ref.load_state_dict(start)
+            ref.zero_grad()
+            out = ref(torch.from_numpy(res[step]["x"]), torch.from_numpy(res[step]["t"]))
+            out["loss"]["total_loss"].backward()
+            g = {n: (p.grad.clone() if p.grad is not None else torch.zeros_like(p)) for n, p in ref.named_parameters()}
+            gsum = g if gsum is None else {n: gsum[n] + g[n] for n in g}
+            bufs.append({k: v.clone() for k, v in ref.named_buffers()})
+        for r, res in ((0, res0), (1, res1)):
+            for n, gv in res[step]["grads"].items():
+                torch.testing.assert_close(torch.from_numpy(gv), gsum[n] / 2, rtol=1e-5, atol=1e-6)
+            for n, bv in res[step]["bufs"].items():        # per-replica BN update from rank 0's stats
+                torch.testing.assert_close(torch.from_numpy(bv), bufs[r][n], rtol=1e-5, atol=1e-6)
+        ref.load_state_dict({**start, **{k: v for k, v in bufs[0].items()}})
+    for calls in (calls0, calls1):                         # optimizer sees which params got no grad
+        assert len(calls) == 2
+        for act in calls:
+            assert dict(zip(names, act)) == {n: not n.startswith("unused.") for n in names}
