@@ -10,13 +10,23 @@ every step exactly as the reference recomputes it per forward.
 
 Multi-GPU: inference shards images with no data-path collective ("replicas", weak scaling):
 one process per GPU (torchrun), barrier + synchronize around the timed region, time = max
-over ranks, value = images processed by all ranks / that time.
+over ranks, value = images processed by all ranks / that time.  `--gpus N` without a torchrun
+environment re-launches this script under torch.distributed.run with N ranks (before any GPU
+call) and exits with its status.  The training legs (config C at 640, config D at 1024) run
+data-parallel over RCCL at N > 1.
+
+Side legs in the same JSON line: `latency` (B=1 device-resident replays), `streaming` (config E:
+1280x720 uint8 frames paced at 30 FPS through ingest -> graph -> NMS -> host), `large`
+(config D per-GPU shapes: 1024², B=8 inference and training), `training` (config C), and
+`cpu_baseline` (the oracle on the host cores, rank 0 at N=1).
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,7 +52,7 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores available (affinity / OMP)")
     ap.add_argument("--eager", dest="graph", action="store_false",
                     help="time host-launched steps instead of HIP-graph replays")
     ap.add_argument("--train", dest="train", action="store_true", default=None,
@@ -51,7 +61,45 @@ def parse():
     ap.add_argument("--no-train", dest="train", action="store_false")
     ap.add_argument("--train-batch", type=int, default=16)
     ap.add_argument("--train-steps", type=int, default=4)
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="skip the paced 30-FPS streaming leg (config E)")
+    ap.add_argument("--stream-frames", type=int, default=900)
+    ap.add_argument("--no-large", dest="large", action="store_false",
+                    help="skip the 1024² legs (config D)")
+    ap.add_argument("--large-batch", type=int, default=8)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: exercise the launcher, rendezvous and the one-line report (CPU tests)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start N ranks under torch.distributed.run (one
+    process per GPU, rendezvous on 127.0.0.1) as a child, before this process touches the GPU,
+    and return its exit status.  Rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def host_threads() -> int:
+    """Host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS when set
+    (the GPU box exposes the whole machine to os.cpu_count() but grants a 16-core share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 class GemmTimer:
@@ -121,27 +169,13 @@ def cpu_baseline(model_cpu_sd, size, threads):
                       f"same random-init weights, after 1 warmup"}
 
 
-def train_bench(a, dev, world, rank):
-    """Config C: base 640x640 bf16 training step -- train-mode forward, YOLOLoss on
-    synthetic COCO targets, backward (Sinkhorn autograd included), bucketed gradient all-reduce
-    over RCCL overlapped with the backward when N>1, per-group clipping, AdamW."""
-    from hv_amd import HybridVisionSystem
-    from hv_amd.targets import synthetic_targets
-    from hv_amd.trainer import HVTrainer
-    torch.manual_seed(0)
-    model = HybridVisionSystem({"image_size": a.size, "precision": a.precision, "verbose": False}).to(dev).train()
-    tr = HVTrainer(model)
-    B = a.train_batch
-    x = torch.randn(B, 3, a.size, a.size, device=dev)
-    tg = [t.to(dev) for t in synthetic_targets(B, a.size, seed=1000 + rank)]
-    for _ in range(2):
-        tr.step(x, tg)
+def _sync_time(world, dev, fn):
+    """Barrier + synchronize on both sides of fn(); returns the elapsed seconds, max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(a.train_steps):
-        loss = tr.step(x, tg)
+    fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -150,17 +184,110 @@ def train_bench(a, dev, world, rank):
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
+    return el
+
+
+def train_bench(a, dev, world, rank, size, batch, steps, gflop_step_img):
+    """Training step (config C at 640, config D at 1024): train-mode forward,
+    YOLOLoss on synthetic COCO targets, backward (Sinkhorn autograd included), bucketed
+    gradient all-reduce over RCCL overlapped with the backward when N>1, per-group clipping,
+    AdamW."""
+    from hv_amd import HybridVisionSystem
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer
+    torch.manual_seed(0)
+    model = HybridVisionSystem({"image_size": size, "precision": a.precision, "verbose": False}).to(dev).train()
+    tr = HVTrainer(model)
+    x = torch.randn(batch, 3, size, size, device=dev)
+    tg = [t.to(dev) for t in synthetic_targets(batch, size, seed=1000 + rank)]
+    for _ in range(2):
+        tr.step(x, tg)
+    box = {}
+
+    def run():
+        for _ in range(steps):
+            box["loss"] = tr.step(x, tg)
+    el = _sync_time(world, dev, run)
     out = {"metric": "train images/s (forward + YOLOLoss + backward + all-reduce + clip + AdamW)",
-           "value": round(world * B * a.train_steps / el, 3), "unit": "images/s",
-           "ms_per_step": round(el / a.train_steps * 1e3, 2), "per_gpu_batch": B, "steps": a.train_steps,
-           "workload": f"hybrid_vision base {a.size}x{a.size} training, bf16 activations, fp32 params, "
-                       f"{'DDP RCCL' if world > 1 else 'single GPU'}",
-           "loss": round(loss["total_loss"].item(), 3),
-           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
-           "model_tflops_reference_graph": round(2095.9 * world * B * a.train_steps / el / 1e3, 2)}
+           "value": round(world * batch * steps / el, 3), "unit": "images/s",
+           "ms_per_step": round(el / steps * 1e3, 2), "per_gpu_batch": batch, "steps": steps, "n_gpus": world,
+           "workload": f"hybrid_vision base {size}x{size} training, bf16 activations, fp32 params, "
+                       f"{'DDP over RCCL (bucketed all-reduce overlapped with backward)' if world > 1 else 'single GPU'}",
+           "loss": round(box["loss"]["total_loss"].item(), 3),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}
+    if gflop_step_img:
+        out["model_tflops_reference_graph"] = round(gflop_step_img * world * batch * steps / el / 1e3, 2)
     del tr, model
     torch.cuda.empty_cache()
     return out
+
+
+def streaming_bench(model, dev, frames_n):
+    """Config E: 1280x720 uint8 BGR camera frames arriving at a fixed 30 FPS for
+    `frames_n` frames; each goes host -> pinned staging -> device, Pillow-exact preprocessing,
+    the hipGraph forward (coefficients frozen), decode, NMS and the detections back to the host
+    (StreamingPipeline).  Latency = result on the host - the frame's scheduled arrival."""
+    import numpy as np
+    from hv_amd.engine import StreamingPipeline
+    pipe = StreamingPipeline(model, (720, 1280), (640, 640))
+    rng = np.random.default_rng(7)
+    yy, xx = np.meshgrid(np.linspace(0, 1, 720), np.linspace(0, 1, 1280), indexing="ij")
+    pool = []
+    for i in range(8):                      # synthetic camera frames: gradients + blocks + noise
+        base = 127 + 100 * np.sin(6.28 * (xx * (i + 1) + yy * 2))[..., None] * np.array([1.0, 0.7, 0.4])
+        blocks = 50 * ((np.floor(xx * 9 + i) + np.floor(yy * 5)) % 2)[..., None]
+        pool.append(np.clip(base + blocks + rng.normal(0, 15, (720, 1280, 3)), 0, 255).astype(np.uint8))
+    for i in range(30):
+        pipe(pool[i % 8])
+    period = 1.0 / 30
+    lat, ndet = [], 0
+    t_start = time.perf_counter() + 0.05
+    for i in range(frames_n):
+        t_arr = t_start + i * period
+        while True:
+            now = time.perf_counter()
+            if now >= t_arr:
+                break
+            if t_arr - now > 2e-3:
+                time.sleep(t_arr - now - 1e-3)
+        res = pipe(pool[i % 8])
+        lat.append((time.perf_counter() - t_arr) * 1e3)
+        ndet += len(res["scores"])
+    wall = time.perf_counter() - t_start
+    lat_s = sorted(lat)
+    pct = lambda q: round(lat_s[min(len(lat_s) - 1, int(q * len(lat_s)))], 3)  # noqa: E731
+    model.freeze(False)
+    return {"frames": frames_n, "target_fps": 30, "achieved_fps": round(frames_n / wall, 2),
+            "p50_ms": pct(0.50), "p95_ms": pct(0.95), "p99_ms": pct(0.99), "max_ms": round(lat_s[-1], 3),
+            "mean_ms": round(float(np.mean(lat)), 3), "over_budget_frames": int(sum(v > 1e3 * period for v in lat)),
+            "detections_per_frame": round(ndet / frames_n, 2), "recaptures": pipe.recaptures,
+            "pipeline": "1280x720 uint8 BGR host frame -> pinned -> HBM -> hv_preprocess_pil (Pillow-exact "
+                        "resize to 640x640, NHWC bf16) -> hipGraph forward (frozen coefficients) + decode -> "
+                        "hipGraph hv_nms (conf 0.25, IoU 0.45) -> detections on the host"}
+
+
+def dry_run(a, world, rank):
+    """--dry-run: the launcher / rendezvous / report path without GPU work (CPU tests)."""
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = max(time.perf_counter() - t0, 1e-9)
+    if world > 1:
+        t = torch.tensor([el])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank)
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "dry_run": True, "ranks": ranks, "scaling": "weak",
+                          "config": {"parallelism": f"replicas{world}"}}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -168,6 +295,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    if a.dry_run:
+        return dry_run(a, world, rank)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
@@ -192,71 +323,95 @@ def main():
             model(x)
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - te) / 3 * 1e3
-        step = model.capture(x).replay if a.graph else (lambda: model(x))
+        runner = model.capture(x) if a.graph else None
+        step = runner.replay if a.graph else (lambda: model(x))
         for _ in range(a.warmup):
             step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+
+        def run():
+            for _ in range(a.steps):
+                step()
+        elapsed = _sync_time(world, dev, run)
 
     # dominant-kernel roofline: the MFMA GEMM family, timed with HIP events in one more step
     with torch.no_grad(), GemmTimer(ops) as gt:
         model(x)
     n_l, avg_ms, avg_flop, gemm_tflops, avg_bytes = gt.summary()
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    tf = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+    if not os.path.exists(tf):
+        tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
     if a.size == 640 and a.batch == 16 and a.precision == "bf16" and os.path.exists(tf):
         with open(tf) as f:
             traffic = json.load(f).get("gemm", {}).get("bytes_per_launch")
+    del runner
 
     lat = None
     if rank == 0 and not a.no_latency:
-        # streaming config E: single 640x640 frame, hipGraph-captured forward; the frame is copied
-        # into the graph's input buffer inside the timed interval
+        # B=1 device-resident replays (no ingest); the frame is copied into the graph's input
+        # buffer inside the timed interval
         lat = {}
         frames = torch.randn(8, 1, 3, a.size, a.size, device=dev)
         for mode in ("recompute", "frozen"):
             model.freeze(mode == "frozen")
             with torch.no_grad():
-                runner = model.capture(frames[0])
+                r1 = model.capture(frames[0])
                 ts = []
                 for i in range(60):
                     torch.cuda.synchronize()
                     t1 = time.perf_counter()
-                    runner(frames[i % 8])
+                    r1(frames[i % 8])
                     torch.cuda.synchronize()
                     if i >= 10:
                         ts.append((time.perf_counter() - t1) * 1e3)
-            del runner
+            del r1
             ts.sort()
             lat[mode] = {"p50_ms": round(ts[len(ts) // 2], 3), "p95_ms": round(ts[int(len(ts) * 0.95) - 1], 3),
                          "p99_ms": round(ts[-1], 3)}
         model.freeze(False)
         lat["batch"] = 1
-        lat["note"] = ("hipGraph replay; 'recompute' re-runs Sinkhorn + coefficient prep per frame like the "
-                       "reference, 'frozen' reuses them until a parameter changes (eval streaming)")
+        lat["note"] = ("hipGraph replay of device-resident frames; 'recompute' re-runs Sinkhorn + coefficient prep per "
+                       "frame like the reference, 'frozen' reuses them until a parameter changes (eval streaming)")
+
+    stream = None
+    if rank == 0 and world == 1 and a.stream and a.size == 640:
+        stream = streaming_bench(model, dev, a.stream_frames)
+    torch.cuda.empty_cache()
+
+    large = None
+    if a.large and a.size == 640:
+        # config D per-GPU shapes (global batch 64 = 8 per GPU x 8): inference replicas + DDP training
+        xl = torch.randn(a.large_batch, 3, 1024, 1024, device=dev)
+        with torch.no_grad():
+            rl = model.capture(xl)
+            for _ in range(2):
+                rl.replay()
+            ls = max(4, a.steps // 4)
+
+            def runl():
+                for _ in range(ls):
+                    rl.replay()
+            el_l = _sync_time(world, dev, runl)
+        del rl, xl
+        torch.cuda.empty_cache()
+        large = {"inference": {"value": round(world * a.large_batch * ls / el_l, 3), "unit": "images/s",
+                               "ms_per_step": round(el_l / ls * 1e3, 3), "per_gpu_batch": a.large_batch,
+                               "steps": ls, "n_gpus": world,
+                               "model_tflops_reference_graph": round(1792.2 * world * a.large_batch * ls / el_l / 1e3, 2),
+                               "workload": "hybrid_vision base 1024x1024 inference (hipGraph replay), 20 Sinkhorn iters"}}
 
     train = None
-    if a.train if a.train is not None else world == 1:
-        train = train_bench(a, dev, world, rank)
+    if a.train if a.train is not None else True:
+        train = train_bench(a, dev, world, rank, a.size, a.train_batch, a.train_steps,
+                            2095.9 if a.size == 640 else None)
+        if large is not None:
+            large["training"] = train_bench(a, dev, world, rank, 1024, a.large_batch, max(2, a.train_steps // 2), None)
 
     imgs = world * a.batch * a.steps
     value = imgs / elapsed
     ms_step = elapsed / a.steps * 1e3
     if rank == 0:
-        base = cpu_baseline(cpu_sd, a.size, a.cpu_threads) if cpu_sd is not None else None
+        base = cpu_baseline(cpu_sd, a.size, a.cpu_threads or host_threads()) if cpu_sd is not None else None
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
@@ -270,7 +425,7 @@ def main():
                          "frac": round(gemm_tflops / BF16_PEAK_TFLOPS, 4),
                          "traffic": round(traffic) if traffic else None,
                          "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload "
-                                           "(FETCH x2 gfx950 correction), profiles/r01/pmc_traffic.json",
+                                           f"(FETCH x2 gfx950 correction), {os.path.relpath(tf, ROOT)}",
                          "algorithmic_bytes_per_launch": round(avg_bytes),
                          "launches_per_step": n_l, "avg_launch_ms": round(avg_ms, 4),
                          "avg_flop_per_launch": avg_flop},
@@ -279,6 +434,8 @@ def main():
                          if a.graph else "eager",
             "eager_ms_per_step": round(eager_ms, 3),
             "latency": lat,
+            "streaming": stream,
+            "large": large,
             "training": train,
             "cpu_baseline": base,
         }

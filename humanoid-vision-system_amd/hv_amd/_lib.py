@@ -147,6 +147,9 @@ _SIGS = {
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),
     "hv_preprocess": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp], i32),
+    "hv_pil_table_ints": ([i32, i32, i32, i32], C.c_size_t),
+    "hv_pil_resample_tables": ([i32, i32, i32, i32, vp], i32),
+    "hv_preprocess_pil": ([vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, vp], i32),
     "hv_nms": ([vp, i32, i32, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
     # ---- training step
     "hv_wgrad_work_floats": ([i32, i32, i32, i32], C.c_size_t),

@@ -34,6 +34,7 @@ import torch
 import torch.nn.functional as F  # noqa: F401
 
 from . import ops
+from .runtime import PRECISIONS as PRECISION_DTYPES
 
 logger = logging.getLogger(__name__)
 
@@ -65,21 +66,26 @@ class InferenceConfig:
     target_fps: int = 30
     use_graphs: bool = False
     collect_stability: bool = False
+    # frame resize: 'pil' = the reference's default (torchvision Resize on PIL, Pillow-exact),
+    # 'bilinear' = its kornia path (F.interpolate bilinear, align_corners=False)
+    resample: str = "pil"
 
 
-def preprocess_image(img: np.ndarray, height: int, width: int, device, dtype=torch.float32) -> torch.Tensor:
-    """uint8 HWC BGR frame -> normalised CHW (preprocessing.py:181-232 semantics: BGR->RGB,
-    bilinear resize, /255, ImageNet mean/std) in one HIP launch (hv_preprocess)."""
-    return preprocess_frames([img], height, width, device, dtype)[0]
+def preprocess_image(img: np.ndarray, height: int, width: int, device, dtype=torch.float32,
+                     resample: str = "pil") -> torch.Tensor:
+    """uint8 HWC BGR frame -> normalised CHW (preprocessing.py:181-276 semantics: BGR->RGB,
+    resize, /255, ImageNet mean/std) in one HIP launch (hv_preprocess_pil / hv_preprocess)."""
+    return preprocess_frames([img], height, width, device, dtype, resample)[0]
 
 
-def preprocess_frames(imgs: List[np.ndarray], height: int, width: int, device, dtype=torch.float32) -> torch.Tensor:
+def preprocess_frames(imgs: List[np.ndarray], height: int, width: int, device, dtype=torch.float32,
+                      resample: str = "pil") -> torch.Tensor:
     """Batch of same-size uint8 HWC BGR frames -> [n, 3, height, width]: one host->device copy
     of the raw bytes, one preprocessing launch."""
     if imgs[0].dtype != np.uint8 or imgs[0].ndim != 3 or imgs[0].shape[2] != 3:
         raise ValueError("expected uint8 HWC 3-channel frames")
     raw = torch.from_numpy(np.ascontiguousarray(np.stack(imgs))).to(device, non_blocking=True)
-    return ops.preprocess(raw, height, width, bgr=True, dtype=dtype)
+    return ops.preprocess(raw, height, width, bgr=True, dtype=dtype, resample=resample)
 
 
 class LazyStabilityMetrics(Mapping):
@@ -163,12 +169,14 @@ class InferenceEngine:
 
     def _to_tensor(self, image: Union[np.ndarray, torch.Tensor]) -> torch.Tensor:
         if isinstance(image, np.ndarray):
-            return preprocess_image(image, self.config.input_height, self.config.input_width, self.device)
+            return preprocess_image(image, self.config.input_height, self.config.input_width, self.device,
+                                    resample=self.config.resample)
         return image.to(self.device)
 
     def preprocess_batch(self, images: List[np.ndarray]) -> torch.Tensor:
         if all(isinstance(i, np.ndarray) for i in images) and len({i.shape for i in images}) == 1:
-            return preprocess_frames(images, self.config.input_height, self.config.input_width, self.device)
+            return preprocess_frames(images, self.config.input_height, self.config.input_width, self.device,
+                                     resample=self.config.resample)
         return torch.stack([self._to_tensor(i) for i in images])
 
     # ------------------------------------------------------------------ inference
@@ -300,6 +308,93 @@ class InferenceEngine:
         self.inference_times.clear()
         self.memory_usage.clear()
         self.stability_metrics.clear()
+
+
+class StreamingPipeline:
+    """Camera-to-detections path of config E (the reference's per-frame loop is
+    scripts/inference.py:224-291 -> process_image_frame: ImagePreprocessor.process, engine
+    infer, DetectionPostprocessor, at 1280x720 / 30 FPS): one host->device copy of the raw
+    uint8 BGR frame, then ONE hipGraph replay holding the Pillow-exact preprocessing
+    (hv_preprocess_pil, written straight into the model's NHWC input), the whole forward with
+    the coefficients frozen, the decode and the batched NMS (hv_nms), then one small
+    device->host copy of the detections.
+
+    Weights changed in place after capture (VersionWatch) trigger a re-capture before the
+    frame's result is read, as in GraphRunner."""
+
+    def __init__(self, model, frame_hw, input_hw=(640, 640), conf_threshold: float = 0.25,
+                 iou_threshold: float = 0.45, max_detections: int = 100, resample: str = "pil"):
+        self.model = model.eval()
+        self.model.freeze(True)
+        dev = next(model.parameters()).device
+        self.dtype = PRECISION_DTYPES[getattr(model, "hv_precision", "bf16")]
+        h, w = frame_hw
+        H, W = input_hw
+        self.frame_hw, self.input_hw, self.resample = (h, w), (H, W), resample
+        self.nms_args = (conf_threshold, iou_threshold, max_detections)
+        self.staging = torch.empty((1, h, w, 3), dtype=torch.uint8).pin_memory()
+        self.frame = torch.empty((1, h, w, 3), dtype=torch.uint8, device=dev)
+        self.inp = torch.empty((1, H, W, 3), dtype=self.dtype, device=dev)
+        md = max_detections
+        self.host = {"boxes": torch.empty((md, 4), dtype=torch.float32).pin_memory(),
+                     "scores": torch.empty(md, dtype=torch.float32).pin_memory(),
+                     "labels": torch.empty(md, dtype=torch.int64).pin_memory(),
+                     "count": torch.empty(1, dtype=torch.int32).pin_memory()}
+        self.recaptures = 0
+        self._capture()
+
+    def _forward(self):
+        H, W = self.input_hw
+        x = ops.preprocess(self.frame, H, W, bgr=True, dtype=self.dtype, nhwc=True, out=self.inp,
+                           resample=self.resample)
+        return self.model(x, task="detection")
+
+    def _capture(self):
+        """Graph 1: preprocess + forward + decode.  The NMS plan's device table is then built
+        (outside any capture) on graph 1's static decoded outputs, and graph 2 records its two
+        launches."""
+        self.graph = self.nms_graph = None
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s), torch.no_grad():
+            for _ in range(2):
+                out = self._forward()
+                ops.NmsPlan(out["decoded"], *self.nms_args).run()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        del out
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph), torch.no_grad():
+            self.outputs = self._forward()
+        self._nms = ops.NmsPlan(self.outputs["decoded"], *self.nms_args)
+        torch.cuda.synchronize()
+        self.nms_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.nms_graph):
+            self.dets = self._nms.run()
+        self.version = self.model._watch.snapshot()
+
+    def __call__(self, frame: np.ndarray) -> Dict[str, np.ndarray]:
+        """uint8 HWC BGR frame -> {'boxes' [k, 4] xyxy normalised, 'scores' [k], 'labels' [k]}."""
+        if frame.shape != (*self.frame_hw, 3) or frame.dtype != np.uint8:
+            raise ValueError(f"expected a uint8 {self.frame_hw + (3,)} frame")
+        self.staging[0].numpy()[...] = frame
+        self.frame.copy_(self.staging, non_blocking=True)
+        self.graph.replay()
+        if self.model._watch.snapshot() != self.version:
+            self.recaptures += 1
+            self._capture()
+            self.frame.copy_(self.staging, non_blocking=True)
+            self.graph.replay()
+        self.nms_graph.replay()
+        boxes, scores, labels, count = self.dets
+        self.host["count"].copy_(count, non_blocking=True)
+        self.host["boxes"].copy_(boxes[0], non_blocking=True)
+        self.host["scores"].copy_(scores[0], non_blocking=True)
+        self.host["labels"].copy_(labels[0], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        k = int(self.host["count"][0])
+        return {"boxes": self.host["boxes"][:k].numpy().copy(), "scores": self.host["scores"][:k].numpy().copy(),
+                "labels": self.host["labels"][:k].numpy().copy()}
 
 
 class AsyncInferenceEngine(InferenceEngine):

@@ -598,60 +598,106 @@ def clone_tree(tree):
 
 
 # ---------------------------------------------------------------------------- post-processing
+class NmsPlan:
+    """GPU post_process (hv_nms) over a FIXED set of decoded tensors: the device table and the
+    output / work buffers are built once, so run() is two kernel launches with no host work --
+    capturable inside a hipGraph (the streaming pipeline records it after the forward).
+    decoded: {scale_key: {'boxes' [B,A,H,W,4], 'class_scores' [B,A,H,W], 'class_indices'}}."""
+
+    def __init__(self, decoded, conf_thr: float, iou_thr: float, max_det: int):
+        keys = sorted(decoded)
+        ents = (L.NmsScale * len(keys))()
+        self._keep = []
+        B = dev = None
+        for i, k in enumerate(keys):
+            o = decoded[k]
+            bx, sc, ci = o["boxes"], o["class_scores"], o["class_indices"]
+            if bx.dtype != torch.float32 or sc.dtype != torch.float32 or ci.dtype != torch.int64 or \
+                    not (bx.is_contiguous() and sc.is_contiguous() and ci.is_contiguous()):
+                bx = bx.detach().float().contiguous()
+                sc = sc.detach().float().contiguous()
+                ci = ci.detach().to(torch.int64).contiguous()
+            _cuda(bx, sc, ci)
+            B = sc.shape[0]
+            dev = sc.device
+            cells = sc.numel() // B
+            if bx.numel() != B * cells * 4 or ci.numel() != B * cells:
+                raise ValueError("nms: boxes / scores / indices shapes disagree")
+            ents[i].boxes, ents[i].class_scores, ents[i].class_indices, ents[i].cells = \
+                bx.data_ptr(), sc.data_ptr(), ci.data_ptr(), cells
+            self._keep += [bx, sc, ci]
+        self.table = upload_table(ents, dev)
+        self.n_scales, self.B = len(keys), B
+        self.conf, self.iou, self.max_det = float(conf_thr), float(iou_thr), int(max_det)
+        self.boxes = torch.empty((B, max_det, 4), device=dev, dtype=torch.float32)
+        self.scores = torch.empty((B, max_det), device=dev, dtype=torch.float32)
+        self.labels = torch.empty((B, max_det), device=dev, dtype=torch.int64)
+        self.count = torch.empty(B, device=dev, dtype=torch.int32)
+        self.work = torch.empty(L.lib().hv_nms_work_bytes(B, len(keys), max_det), device=dev, dtype=torch.uint8)
+
+    def run(self):
+        check(L.lib().hv_nms(self.table.data_ptr(), self.n_scales, self.B, self.conf, self.iou, self.max_det,
+                             self.boxes.data_ptr(), self.scores.data_ptr(), self.labels.data_ptr(),
+                             self.count.data_ptr(), self.work.data_ptr(), stream_ptr()), "hv_nms")
+        return self.boxes, self.scores, self.labels, self.count
+
+
 def nms_batched(decoded, conf_thr: float, iou_thr: float, max_det: int):
     """GPU post_process (hv_nms): per-scale threshold + greedy NMS, then cross-scale NMS.
-    decoded: {scale_key: {'boxes' [B,A,H,W,4], 'class_scores' [B,A,H,W], 'class_indices'}}.
     Returns device tensors boxes [B, max_det, 4], scores [B, max_det], labels [B, max_det],
     count [B] (int32)."""
-    keys = sorted(decoded)
-    ents = (L.NmsScale * len(keys))()
-    keep = []
-    B = None
-    dev = None
-    for i, k in enumerate(keys):
-        o = decoded[k]
-        bx = o["boxes"].detach().float().contiguous()
-        sc = o["class_scores"].detach().float().contiguous()
-        ci = o["class_indices"].detach().to(torch.int64).contiguous()
-        _cuda(bx, sc, ci)
-        B = sc.shape[0]
-        dev = sc.device
-        cells = sc.numel() // B
-        if bx.numel() != B * cells * 4 or ci.numel() != B * cells:
-            raise ValueError("nms_batched: boxes / scores / indices shapes disagree")
-        ents[i].boxes, ents[i].class_scores, ents[i].class_indices, ents[i].cells = \
-            bx.data_ptr(), sc.data_ptr(), ci.data_ptr(), cells
-        keep += [bx, sc, ci]
-    table = upload_table(ents, dev)
-    boxes = torch.empty((B, max_det, 4), device=dev, dtype=torch.float32)
-    scores = torch.empty((B, max_det), device=dev, dtype=torch.float32)
-    labels = torch.empty((B, max_det), device=dev, dtype=torch.int64)
-    count = torch.empty(B, device=dev, dtype=torch.int32)
-    work = torch.empty(L.lib().hv_nms_work_bytes(B, len(keys), max_det), device=dev, dtype=torch.uint8)
-    check(L.lib().hv_nms(table.data_ptr(), len(keys), B, float(conf_thr), float(iou_thr), int(max_det),
-                         boxes.data_ptr(), scores.data_ptr(), labels.data_ptr(), count.data_ptr(), work.data_ptr(),
-                         stream_ptr()), "hv_nms")
-    return boxes, scores, labels, count
+    return NmsPlan(decoded, conf_thr, iou_thr, max_det).run()
 
 
 # ---------------------------------------------------------------------------- preprocessing
 IMAGENET_MEAN_STD = (0.485, 0.456, 0.406, 0.229, 0.224, 0.225)
 
 
+_PIL_TABLES = {}
+
+
+def pil_table(h: int, w: int, height: int, width: int, device) -> Tensor:
+    """Device copy of the Pillow-exact resample table for (h, w) -> (height, width), cached."""
+    key = (h, w, height, width, str(device))
+    t = _PIL_TABLES.get(key)
+    if t is None:
+        n = L.lib().hv_pil_table_ints(h, w, height, width)
+        host = torch.empty(n, dtype=torch.int32)
+        check(L.lib().hv_pil_resample_tables(h, w, height, width, host.data_ptr()), "hv_pil_resample_tables")
+        t = host.to(device)
+        _PIL_TABLES[key] = t
+    return t
+
+
 def preprocess(frames: Tensor, height: int, width: int, *, bgr: bool = True, dtype: torch.dtype = torch.float32,
-               nhwc: bool = False, mean_std=IMAGENET_MEAN_STD) -> Tensor:
+               nhwc: bool = False, mean_std=IMAGENET_MEAN_STD, resample: str = "pil",
+               out: Optional[Tensor] = None) -> Tensor:
     """uint8 [n, h, w, 3] device frames -> normalised [n, 3, height, width] (NCHW tensor, or the
-    NCHW-shaped view of NHWC storage when nhwc=True -- zero-copy for the model's input)."""
+    NCHW-shaped view of NHWC storage when nhwc=True -- zero-copy for the model's input).
+    resample: 'pil' (the reference's torchvision/Pillow path, bit-exact) or 'bilinear'
+    (F.interpolate / kornia semantics).  `out` (contiguous, the NHWC or NCHW buffer) is written
+    in place when given (the streaming pipeline's captured input)."""
     _cuda(frames)
     if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
         raise ValueError("preprocess expects uint8 [n, h, w, 3] frames")
     frames = frames.contiguous()
     n, h, w, _ = frames.shape
     code = {torch.float32: L.HV_F32, torch.bfloat16: L.HV_BF16, torch.float16: 2}[dtype]
-    out = torch.empty((n, height, width, 3) if nhwc else (n, 3, height, width), device=frames.device, dtype=dtype)
+    shape = (n, height, width, 3) if nhwc else (n, 3, height, width)
+    if out is None:
+        out = torch.empty(shape, device=frames.device, dtype=dtype)
+    elif tuple(out.shape) != shape or out.dtype != dtype or not out.is_contiguous():
+        raise ValueError(f"preprocess: out must be a contiguous {dtype} {shape} tensor")
     ms = (C.c_float * 6)(*mean_std)
-    check(L.lib().hv_preprocess(frames.data_ptr(), n, h, w, int(bgr), height, width, ms, code, int(nhwc),
-                                out.data_ptr(), stream_ptr()), "hv_preprocess")
+    if resample == "pil":
+        tab = pil_table(h, w, height, width, frames.device)
+        check(L.lib().hv_preprocess_pil(frames.data_ptr(), n, h, w, int(bgr), height, width, tab.data_ptr(), ms,
+                                        code, int(nhwc), out.data_ptr(), stream_ptr()), "hv_preprocess_pil")
+    elif resample == "bilinear":
+        check(L.lib().hv_preprocess(frames.data_ptr(), n, h, w, int(bgr), height, width, ms, code, int(nhwc),
+                                    out.data_ptr(), stream_ptr()), "hv_preprocess")
+    else:
+        raise ValueError("resample must be 'pil' or 'bilinear'")
     return out.permute(0, 3, 1, 2) if nhwc else out
 
 

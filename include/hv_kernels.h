@@ -353,6 +353,16 @@ int hv_nms(const hv_nms_scale* dev_scales, int nscales, int batch, float conf_th
 int hv_preprocess(const uint8_t* img, int n, int h, int w, int swap_rb, int out_h, int out_w,
                   const float* mean_std /* host [6] */, int out_dtype, int nhwc, void* out,
                   hv_stream_t stream);
+/* The reference's default (torchvision on PIL, preprocessing.py:104-131,268-274; kornia is not
+   in requirements.txt) = Pillow Image.resize(BILINEAR), reproduced bit-exactly: antialiased
+   triangle filter, 22-bit fixed-point taps, uint8-rounded horizontal then vertical pass; then
+   (u / 255 - mean) / std in fp32.  The resample table is built on the HOST
+   (hv_pil_resample_tables, hv_pil_table_ints int32 entries) and uploaded by the caller. */
+size_t hv_pil_table_ints(int in_h, int in_w, int out_h, int out_w);
+int hv_pil_resample_tables(int in_h, int in_w, int out_h, int out_w, int* table_host);
+int hv_preprocess_pil(const uint8_t* img, int n, int h, int w, int swap_rb, int out_h, int out_w,
+                      const int* table_dev, const float* mean_std /* host [6] */, int out_dtype, int nhwc,
+                      void* out, hv_stream_t stream);
 
 /* ====================================================================================
  * Training step: backward kernels, BatchNorm batch statistics,

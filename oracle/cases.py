@@ -80,3 +80,28 @@ def nms_case(seed: int, B: int = 2, grids=((8, 8), (4, 4), (2, 2)), A: int = 3, 
         lab = torch.randint(0, 80, (B, A, h, w), generator=g)
         out[f"scale_{s}"] = {"boxes": boxes.float(), "class_scores": sc.float(), "class_indices": lab}
     return out
+
+
+PIL_CASES = [  # (tag, frames, in_h, in_w, out_h, out_w, seed)
+    ("720x1280_640", 1, 720, 1280, 640, 640, 11),    # the reference webcam (scripts/inference.py:236-238)
+    ("480x640_640", 2, 480, 640, 640, 640, 12),      # vertical upscale, horizontal identity-ish
+    ("300x200_416", 1, 300, 200, 416, 416, 13),      # upscale both ways
+    ("37x53_29x71", 3, 37, 53, 29, 71, 14),          # ragged, mixed
+    ("64x64_64", 1, 64, 64, 64, 64, 15),             # identity
+    ("1x1_3x5", 1, 1, 1, 3, 5, 16),                  # degenerate
+]
+
+
+def camera_frames(seed: int, n: int, h: int, w: int):
+    """Deterministic uint8 BGR frames [n, h, w, 3]: smooth gradients + texture + noise, so the
+    resampler sees both flat regions and edges (numpy, identical on every machine)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    yy, xx = np.meshgrid(np.linspace(0, 1, h), np.linspace(0, 1, w), indexing="ij")
+    out = np.empty((n, h, w, 3), dtype=np.uint8)
+    for i in range(n):
+        for c in range(3):
+            base = 127 + 100 * np.sin(6.28 * (xx * (c + 1) + yy * (i + 2)))
+            tex = 40 * ((np.floor(xx * w / 7) + np.floor(yy * h / 5)) % 2)
+            out[i, :, :, c] = np.clip(base + tex + rng.normal(0, 20, (h, w)), 0, 255).astype(np.uint8)
+    return out

@@ -384,9 +384,28 @@ def gen_nms(yh):
         save(f"nms_{seed}", **rec)
 
 
+def gen_preproc():
+    """G7: the reference's default preprocessing resize -- torchvision Resize on a PIL image,
+    i.e. Pillow Image.resize(BILINEAR) (preprocessing.py:104-131,268-274; Pillow pinned 10.0.0 in
+    requirements.txt, the same Resample.c algorithm as the Pillow installed here).  Stores the
+    resized uint8 RGB images; inputs are regenerated from oracle/cases.camera_frames."""
+    print("G7 preprocessing (Pillow)")
+    import PIL
+    from PIL import Image
+    from oracle.cases import PIL_CASES, camera_frames
+    for tag, n, h, w, oh, ow, seed in PIL_CASES:
+        bgr = camera_frames(seed, n, h, w)
+        outs = []
+        for i in range(n):
+            rgb = bgr[i][:, :, ::-1].copy()                      # cv2.cvtColor(BGR2RGB), preprocessing.py:202-205
+            outs.append(np.asarray(Image.fromarray(rgb).resize((ow, oh), Image.BILINEAR)))
+        save(f"preproc_pil_{tag}", seed=seed, in_hw=np.array([n, h, w]), out_hw=np.array([oh, ow]),
+             resized_rgb=np.stack(outs), pillow_version=np.array(PIL.__version__))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train,nms")
+    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train,nms,preproc")
     ap.add_argument("--models", default="")
     ap.add_argument("--trains", default="")
     a = ap.parse_args()
@@ -407,6 +426,8 @@ def main():
         gen_train(hv, [m for m in a.trains.split(",") if m])
     if "nms" in parts:
         gen_nms(yh)
+    if "preproc" in parts:
+        gen_preproc()
 
 
 

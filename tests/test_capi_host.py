@@ -73,3 +73,26 @@ def test_oracle_not_imported_by_product():
             if f.endswith(".py"):
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in re.sub(r'""".*?"""', "", txt, flags=re.S).replace("# ", ""), f
+
+
+def test_pil_resample_tables_match_oracle():
+    """The host-side table builder of hv_preprocess_pil (Pillow Resample.c coefficients, no GPU
+    needed) equals the oracle's restatement, which is pinned bit-exactly against Pillow."""
+    import numpy as np
+    from hv_amd import _lib
+    from oracle import cases
+    from oracle import preproc as P
+    lib = _lib.lib()
+    for _, _, h, w, oh, ow, _ in cases.PIL_CASES + [("", 1, 720, 1280, 416, 416, 0), ("", 1, 1080, 1920, 640, 640, 0)]:
+        n = lib.hv_pil_table_ints(h, w, oh, ow)
+        tab = torch.empty(n, dtype=torch.int32)
+        assert lib.hv_pil_resample_tables(h, w, oh, ow, tab.data_ptr()) == 0
+        t = tab.numpy().astype(np.int64)
+        hb, hk = P.coeffs(w, ow)
+        vb, vk = P.coeffs(h, oh)
+        assert (t[0], t[1]) == (hk.shape[1], vk.shape[1])
+        o = 2
+        for arr in (hb, hk, vb, vk):
+            np.testing.assert_array_equal(t[o:o + arr.size], arr.reshape(-1))
+            o += arr.size
+        assert o == n

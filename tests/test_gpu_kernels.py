@@ -398,19 +398,20 @@ def test_gpu_nms_large_matches_oracle(gpu_device):
 
 @pytest.mark.parametrize("h,w,oh,ow", [(480, 640, 640, 640), (720, 1280, 640, 640), (64, 64, 64, 64), (300, 200, 416, 416)])
 def test_gpu_preprocess_matches_torch(gpu_device, h, w, oh, ow):
-    """§8f-2: uint8 BGR frames -> resize (bilinear, align_corners=False) -> /255 -> ImageNet norm."""
+    """§8f-2, the kornia path (K.Resize bilinear = F.interpolate, preprocessing.py:148-152):
+    uint8 BGR frames -> resize (bilinear, align_corners=False) -> /255 -> ImageNet norm."""
     from hv_amd import ops
     g = torch.Generator().manual_seed(h * w)
     frames = torch.randint(0, 256, (2, h, w, 3), generator=g, dtype=torch.uint8)
     t = frames.flip(-1).permute(0, 3, 1, 2).float() / 255.0
     t = F.interpolate(t, size=(oh, ow), mode="bilinear", align_corners=False)
     ref = (t - torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) / torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
-    out = ops.preprocess(frames.to(gpu_device), oh, ow)
+    out = ops.preprocess(frames.to(gpu_device), oh, ow, resample="bilinear")
     assert (out.cpu() - ref).abs().max().item() < 2e-5
-    nh = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.bfloat16, nhwc=True)
+    nh = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.bfloat16, nhwc=True, resample="bilinear")
     assert nh.permute(0, 2, 3, 1).is_contiguous()
     assert (nh.float().cpu() - ref).abs().max().item() < 2e-2
-    h16 = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.float16)
+    h16 = ops.preprocess(frames.to(gpu_device), oh, ow, dtype=torch.float16, resample="bilinear")
     assert (h16.float().cpu() - ref).abs().max().item() < 5e-3
 
 
@@ -430,3 +431,23 @@ def test_decode_argmax_first_index_on_ties(gpu_device, n, h, w):
     if cs is not None:
         assert torch.equal(cs, sc.max(dim=1).values)
     assert torch.equal(pr.cpu().reshape(-1), lg.reshape(n, h, w, 3, 85).permute(0, 3, 1, 2, 4).cpu().reshape(-1))
+
+
+@pytest.mark.parametrize("case", ["720x1280_640", "480x640_640", "300x200_416", "37x53_29x71", "64x64_64", "1x1_3x5"])
+def test_gpu_preprocess_pil_bit_exact(gpu_device, case):
+    """§8f-2, the reference's default preprocessing (torchvision Resize on a PIL image =
+    Pillow Image.resize(BILINEAR); kornia is not in requirements.txt): the resized uint8 image
+    must equal Pillow's BIT FOR BIT (tests/golden/preproc_pil_*, made by Pillow itself), and
+    the normalised tensor must equal torchvision's ToTensor + Normalize in fp32 exactly."""
+    from hv_amd import ops
+    from oracle import cases
+    g = golden(f"preproc_pil_{case}")
+    bgr = torch.from_numpy(cases.camera_frames(int(g["seed"]), *[int(v) for v in g["in_hw"]]))
+    oh, ow = (int(v) for v in g["out_hw"])
+    rgb_u8 = torch.from_numpy(g["resized_rgb"])                       # [n, oh, ow, 3] from Pillow
+    ref = (rgb_u8.permute(0, 3, 1, 2).float().div(255) - torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) \
+        / torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    out = ops.preprocess(bgr.to(gpu_device), oh, ow, resample="pil")
+    assert torch.equal(out.cpu(), ref)
+    nh = ops.preprocess(bgr.to(gpu_device), oh, ow, dtype=torch.bfloat16, nhwc=True, resample="pil")
+    assert torch.equal(nh.cpu(), ref.to(torch.bfloat16))

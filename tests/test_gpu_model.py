@@ -424,3 +424,33 @@ def test_engine_owned_outputs_recapture_and_stability(gpu_device):
     direct = m(f2)["predictions"]["scale_1"]
     torch.testing.assert_close(r3["outputs"]["predictions"]["scale_1"], direct, rtol=0, atol=1e-5)
     assert not torch.equal(r3["outputs"]["predictions"]["scale_1"], r2["outputs"]["predictions"]["scale_1"])
+
+
+def test_streaming_pipeline_matches_eager_path(gpu_device):
+    """Config E's pipeline (StreamingPipeline: uint8 camera frame -> Pillow-exact preprocessing
+    -> graphed forward -> graphed NMS -> host) returns exactly the detections of the eager path
+    on the same frame (ops.preprocess -> model.detect), keeps returning correct results across
+    frames, and re-captures after an in-place weight change."""
+    from hv_amd import ops
+    from inference.engine import StreamingPipeline
+    m = _build("tiny", "wc", "fp32", gpu_device)
+    frames = [cases.camera_frames(40 + i, 1, 96, 160)[0] for i in range(3)]
+    pipe = StreamingPipeline(m, (96, 160), (128, 128), conf_threshold=0.05, iou_threshold=0.45, max_detections=50)
+
+    def eager(fr):
+        x = ops.preprocess(torch.from_numpy(fr[None]).to(gpu_device), 128, 128, resample="pil")
+        return m.detect(x, 0.05, 0.45, 50)[0]
+    for fr in frames + frames[:1]:
+        got = pipe(fr)
+        ref = eager(fr)
+        assert len(got["scores"]) == ref["scores"].numel() > 0
+        np.testing.assert_array_equal(got["scores"], ref["scores"].cpu().numpy())
+        np.testing.assert_array_equal(got["labels"], ref["labels"].cpu().numpy())
+        np.testing.assert_array_equal(got["boxes"], ref["boxes"].cpu().numpy())
+    sd = {k: (v * 1.3 if k.endswith("pred_conv.bias") else v) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    got = pipe(frames[1])
+    assert pipe.recaptures == 1
+    m.freeze(False)
+    ref = eager(frames[1])
+    np.testing.assert_array_equal(got["scores"], ref["scores"].cpu().numpy())

@@ -233,3 +233,16 @@ def test_post_process_oracle_matches_reference(seed):
         np.testing.assert_array_equal(r["labels"].numpy(), g[f"labels{b}"])
         np.testing.assert_allclose(r["scores"].numpy(), g[f"scores{b}"], rtol=0, atol=0)
         np.testing.assert_allclose(r["boxes"].reshape(-1, 4).numpy(), g[f"boxes{b}"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("case", [c[0] for c in cases.PIL_CASES])
+def test_preprocess_oracle_matches_pillow(case):
+    """oracle/preproc.py (numpy restatement of Pillow's Resample.c) against Pillow's own output
+    for the reference's default preprocessing resize -- bit-exact."""
+    from oracle import preproc as P
+    g = golden(f"preproc_pil_{case}")
+    n, h, w = (int(v) for v in g["in_hw"])
+    oh, ow = (int(v) for v in g["out_hw"])
+    bgr = cases.camera_frames(int(g["seed"]), n, h, w)
+    rgb, _ = P.preprocess_frames(bgr, oh, ow)
+    np.testing.assert_array_equal(rgb, g["resized_rgb"])
