@@ -1066,6 +1066,70 @@ __global__ void __launch_bounds__(64) k_attention_general(const T* __restrict__ 
   }
 }
 
+
+// ---- one query row per workgroup (the CLS query of the encoder's last block, Lq = 1): the keys
+// are split over the 256 threads, each keeps an online-softmax partial (max, sum, acc[HD]); the
+// partials merge through wave shuffles and LDS.
+template <typename T, int HD>
+__global__ void __launch_bounds__(256) k_attention_row(const T* __restrict__ q, const T* __restrict__ k,
+                                                       const T* __restrict__ v, const unsigned char* __restrict__ mask,
+                                                       T* __restrict__ o, int Lq, int Lk, int heads, float scale) {
+  __shared__ float red[4][HD + 2];
+  const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int D = heads * HD;
+  float qr[HD], acc[HD];
+  const T* qp = q + ((long)b * Lq + i) * D + h * HD;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) {
+    qr[d] = Elem<T>::load(qp, d) * scale;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j = threadIdx.x; j < Lk; j += 256) {
+    if (mask && mask[(long)b * Lk + j]) continue;
+    const long off = ((long)b * Lk + j) * D + h * HD;
+    float sc = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) sc = fmaf(qr[d], Elem<T>::load(k, off + d), sc);
+    const float mn = fmaxf(m, sc);
+    const float corr = __expf(m - mn), p = __expf(sc - mn);
+    l = l * corr + p;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) acc[d] = fmaf(acc[d], corr, p * Elem<T>::load(v, off + d));
+    m = mn;
+  }
+  // merge (m, l, acc) across the wave, then across the 4 waves
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    const float m2 = __shfl_xor(m, sh, 64), l2 = __shfl_xor(l, sh, 64);
+    const float mn = fmaxf(m, m2);
+    const float c1 = mn == -INFINITY ? 0.f : __expf(m - mn), c2 = mn == -INFINITY ? 0.f : __expf(m2 - mn);
+    l = l * c1 + l2 * c2;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) acc[d] = acc[d] * c1 + __shfl_xor(acc[d], sh, 64) * c2;
+    m = mn;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = m;
+    red[w][1] = l;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) red[w][2 + d] = acc[d];
+  }
+  __syncthreads();
+  if (threadIdx.x < HD) {
+    float mm = -INFINITY;
+    for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, red[ww][0]);
+    float ll = 0.f, aa = 0.f;
+    for (int ww = 0; ww < 4; ++ww) {
+      const float c = mm == -INFINITY ? 0.f : __expf(red[ww][0] - mm);
+      ll += red[ww][1] * c;
+      aa += red[ww][2 + threadIdx.x] * c;
+    }
+    Elem<T>::store(o + ((long)b * Lq + i) * D + h * HD, threadIdx.x, ll > 0.f ? aa / ll : NAN);
+  }
+}
+
 // ---- batched byte-range copies (hv_copy_segments): 16 KiB per block, segment found by binary
 // search over the block prefix table passed by value
 constexpr int kCopyMax = 64;
@@ -1244,9 +1308,15 @@ extern "C" int hv_attention_general(int dtype, const void* q, const void* k, con
                                     const unsigned char* key_padding_mask, void* out, float* weights, int n,
                                     int Lq, int Lk, int heads, int hd, float sm_scale, hv_stream_t stream) {
   if (n <= 0 || Lq <= 0 || Lk <= 0 || heads <= 0 || !q || !k || !v || !out) return HV_EINVAL;
-  const dim3 g(hv_cdiv(Lq, 64), heads, n);
   hipStream_t s = (hipStream_t)stream;
-  hv_diag_count(HV_KF_ATTN_SCALAR);
+  hv_diag_count(HV_KF_ATTN_GENERAL);
+  if (!weights && Lq <= 4 && hd == 32) {      // CLS-query rows: keys split over a workgroup
+    HV_DISPATCH(dtype, (k_attention_row<T, 32><<<dim3(Lq, heads, n), 256, 0, s>>>(
+                            (const T*)q, (const T*)k, (const T*)v, key_padding_mask, (T*)out, Lq, Lk, heads, sm_scale)));
+    HV_CHECK_LAUNCH();
+    return HV_OK;
+  }
+  const dim3 g(hv_cdiv(Lq, 64), heads, n);
 #define HV_ATTN_GEN(HDV)                                                                            \
   HV_DISPATCH(dtype, (k_attention_general<T, HDV><<<g, 64, 0, s>>>((const T*)q, (const T*)k, (const T*)v, \
                                                                  key_padding_mask, (T*)out, weights, Lq, Lk,  \

@@ -393,6 +393,9 @@ class HybridVisionSystem(nn.Module):
                 if m.bias is not None:
                     nn.init.zeros_(m.bias)
         self._mhc_modules = [m for m in self.modules() if isinstance(m, ManifoldHyperConnection)]
+        from .manifold import MultiHeadManifoldAttention
+        self._qkv_groups = {id(a): (a.q_proj, a.k_proj, a.v_proj) for a in self.modules()
+                            if isinstance(a, MultiHeadManifoldAttention)}
         self._frozen: Optional[Tuple[Any, RunCtx]] = None
         self._sk_cache: Dict[str, Any] = {}
         self._watch = VersionWatch(self)
@@ -414,7 +417,7 @@ class HybridVisionSystem(nn.Module):
     def _make_ctx(self) -> RunCtx:
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
         key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=_PREP_OVERLAP)
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=_PREP_OVERLAP, groups=self._qkv_groups)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":

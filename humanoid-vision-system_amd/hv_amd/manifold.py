@@ -136,7 +136,8 @@ def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = N
     return ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x2.dtype, residual=residual)
 
 
-def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None, overlap: bool = False) -> None:
+def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None, overlap: bool = False,
+                  groups: Optional[dict] = None) -> None:
     """Sinkhorn + coefficient prep for every mHC module in `mods` through one grouped
     PrepProgram (reused from `cache` while `key` -- the owner's parameter/buffer storage --
     and the precision are unchanged, so a captured graph replays the same buffers)."""
@@ -148,7 +149,7 @@ def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None, ove
     if cache is not None and cache.get("key") == (key, ctx.dtype, FOLD_MAX_D):
         prog = cache["program"]
     if prog is None:
-        prog = PrepProgram(mods, ctx.dtype, mods[0].H_res_raw.device, FOLD_MAX_D)
+        prog = PrepProgram(mods, ctx.dtype, mods[0].H_res_raw.device, FOLD_MAX_D, groups)
         if cache is not None:
             cache["key"], cache["program"] = (key, ctx.dtype, FOLD_MAX_D), prog
     ctx.program = prog
@@ -283,6 +284,10 @@ class ManifoldHyperConnection(nn.Module):
 
 
 # ================================================================== attention / norms
+PARALLEL_QKV = False  # q / k / v on three streams: measured slower (22.30 vs 21.77 ms, tools/ab_vit.py)
+GROUP_QKV = True      # q / k / v GEMM1 as one N = 3*2Hd GEMM (shared LN statistics)
+
+
 class MultiHeadManifoldAttention(nn.Module):
     """Reference manifold_layers.py:349-434: four mHC projections around softmax(QK^T/sqrt(hd))V."""
 
@@ -302,15 +307,63 @@ class MultiHeadManifoldAttention(nn.Module):
         self.out_proj = ManifoldHyperConnection(embed_dim, **kw)
         self.dropout = nn.Dropout(dropout)
         self.scaling = self.head_dim ** -0.5
+        self._side = None
 
     def forward_tokens(self, x: torch.Tensor, n: int) -> torch.Tensor:
-        """Self-attention on x [n*L, D] (compute dtype); returns out_proj(attn) [n*L, D]."""
+        """Self-attention on x [n*L, D] (compute dtype); returns out_proj(attn) [n*L, D].
+        The q / k / v projections are independent mHC chains of small-M GEMMs (M = n*L, K =
+        256): with PARALLEL_QKV they run on three streams (three branches of a captured
+        graph), so their latency-bound launches overlap."""
         L = x.shape[0] // n
-        q = self.q_proj.forward_tokens(x).view(n, L, -1)
-        k = self.k_proj.forward_tokens(x).view(n, L, -1)
-        v = self.v_proj.forward_tokens(x).view(n, L, -1)
+        ctx = current()
+        grp = ctx.plans.get(("group", id(self))) if (ctx is not None and GROUP_QKV) else None
+        if grp is not None and not self.training:
+            q, k, v = (t.view(n, L, -1) for t in self._qkv_grouped(x, grp))
+            o = ops.attention(q, k, v, self.num_heads)
+            return self.out_proj.forward_tokens(o.view(n * L, -1))
+        if PARALLEL_QKV:
+            main = torch.cuda.current_stream()
+            if self._side is None:
+                self._side = (torch.cuda.Stream(device=x.device), torch.cuda.Stream(device=x.device))
+            sk, sv = self._side
+            sk.wait_stream(main)
+            sv.wait_stream(main)
+            with torch.cuda.stream(sk):
+                k = self.k_proj.forward_tokens(x)
+            with torch.cuda.stream(sv):
+                v = self.v_proj.forward_tokens(x)
+            q = self.q_proj.forward_tokens(x)
+            main.wait_stream(sk)
+            main.wait_stream(sv)
+            for t in (k, v):
+                t.record_stream(main)
+            x.record_stream(sk)
+            x.record_stream(sv)
+            q, k, v = q.view(n, L, -1), k.view(n, L, -1), v.view(n, L, -1)
+        else:
+            q = self.q_proj.forward_tokens(x).view(n, L, -1)
+            k = self.k_proj.forward_tokens(x).view(n, L, -1)
+            v = self.v_proj.forward_tokens(x).view(n, L, -1)
         o = ops.attention(q, k, v, self.num_heads)
         return self.out_proj.forward_tokens(o.view(n * L, -1))
+
+    def _qkv_grouped(self, x: torch.Tensor, grp):
+        """q / k / v mHC chains sharing x: ONE LayerNorm-statistics pass and ONE folded GEMM1
+        with N = 3 * 2Hd (prep.PrepProgram lays the three sites' operands out contiguously);
+        GEMM2 / GEMM3 / LN_post per site on column slices of the shared hidden activations."""
+        mods, a1g, c1g, csg = grp
+        ctx = current()
+        ctx.join_prep()
+        mean, rstd = ops.row_stats(x, 1e-5)
+        h1 = ops.gemm(x, a1g, bias=c1g, act="gelu", a_mean=mean, a_rstd=rstd, b_colsum=csg)
+        outs = []
+        for j, m in enumerate(mods):
+            p = ctx.plans[id(m)]
+            w = 2 * p.Hd
+            h2 = ops.gemm(h1[:, j * w:(j + 1) * w], p.w2, bias=p.bias2, act="gelu")
+            yc = ops.gemm(x, p.wct, a2=h2, out_dtype=torch.float32)
+            outs.append(ops.layernorm(yc, p.g_post, p.b_post, 1e-5, out_dtype=x.dtype))
+        return outs
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
         """manifold_layers.py:386-434: (out [n, Lq, D], attn_weights [n, heads, Lq, Lk] or None).

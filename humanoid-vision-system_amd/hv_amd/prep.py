@@ -44,7 +44,12 @@ def _upload(entries, device) -> torch.Tensor:
 
 
 class PrepProgram:
-    def __init__(self, mhc_mods: List[nn.Module], dtype: torch.dtype, device: torch.device, fold_max_d: int):
+    def __init__(self, mhc_mods: List[nn.Module], dtype: torch.dtype, device: torch.device, fold_max_d: int,
+                 groups: Optional[Dict[int, Tuple]] = None):
+        """groups: {key: (mHC, mHC, ...)} -- sites that read the same input (an attention's
+        q/k/v projections): their folded GEMM1 operands (a1, c1, row sums) are laid out
+        contiguously, so one GEMM with N = sum(2Hd) serves all of them (published in the plans
+        under ("group", key))."""
         self.dtype, self.device = dtype, device
         self.mods = list(mhc_mods)
         self.fold_max_d = fold_max_d
@@ -70,13 +75,35 @@ class PrepProgram:
         tot = [0, 0, 0, 0]
         blk = (L.i32 * 4)()
         self.wcasts: List[Tuple[torch.Tensor, torch.Tensor]] = []     # (src, dst) for the weight group
+        # contiguous GEMM1 operands for grouped sites
+        self.groups: Dict[object, Tuple] = {}
+        slot: Dict[int, Tuple] = {}
+        present = {id(m) for m in self.mods}
+        for gk, members in (groups or {}).items():
+            ms = list(members)
+            D0, H0 = ms[0].input_dim, ms[0].hidden_dim
+            if not all(id(m) in present and m.input_dim == D0 and m.hidden_dim == H0 for m in ms):
+                continue
+            if not (D0 <= fold_max_d and H0 % 32 == 0):
+                continue
+            g = len(ms)
+            a1g = torch.empty((g * 2 * H0, D0), device=device, dtype=dtype)
+            c1g = torch.empty(g * 2 * H0, device=device, dtype=torch.float32)
+            csg = torch.empty(g * 2 * H0, device=device, dtype=torch.float32)
+            for j, m in enumerate(ms):
+                sl = slice(j * 2 * H0, (j + 1) * 2 * H0)
+                slot[id(m)] = (a1g[sl], c1g[sl], csg[sl])
+            self.groups[gk] = (tuple(ms), a1g, c1g, csg)
         for i, m in enumerate(self.mods):
             D, Hd = m.input_dim, m.hidden_dim
             fold = D <= fold_max_d and Hd % 32 == 0
-            a1 = torch.empty((2 * Hd, D) if fold else (Hd, D), device=device, dtype=dtype)
-            c1 = torch.empty(2 * Hd if fold else Hd, device=device, dtype=torch.float32)
+            if id(m) in slot:
+                a1, c1, cs = slot[id(m)]
+            else:
+                a1 = torch.empty((2 * Hd, D) if fold else (Hd, D), device=device, dtype=dtype)
+                c1 = torch.empty(2 * Hd if fold else Hd, device=device, dtype=torch.float32)
+                cs = torch.empty(a1.shape[0], device=device, dtype=torch.float32)
             wct = torch.empty((D, D + Hd), device=device, dtype=dtype)
-            cs = torch.empty(a1.shape[0], device=device, dtype=torch.float32)
             w1 = _param(m.mlp[0].weight, "mlp[0].weight")
             w2 = _param(m.mlp[3].weight, "mlp[3].weight")
             w2c = self._cast_target(w2)
@@ -226,6 +253,8 @@ class PrepProgram:
                 D=m.input_dim, Hd=m.hidden_dim, fold=fold, dtype=self.dtype, b1=a1, c1=c1,
                 w1=w1c, bias1=None if fold else m.mlp[0].bias.detach(), w2=w2c, bias2=m.mlp[3].bias.detach(),
                 wct=wct, g_post=m.norm_post.weight.detach(), b_post=m.norm_post.bias.detach(), cs=cs)
+        for gk, grp in self.groups.items():
+            ctx.plans[("group", gk)] = grp
         for conv, bn, w, scale, bias_out, val in self.convs.values():
             ctx.plans[("conv", id(conv))] = val
         for lin, val in self.linears.values():

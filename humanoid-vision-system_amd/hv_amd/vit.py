@@ -24,6 +24,10 @@ def _positions(pe: torch.Tensor, tokens: int) -> torch.Tensor:
     return t
 
 
+# run the encoder's last block on the CLS rows only (TransformerEncoderBlock.forward_tokens_cls)
+CLS_ONLY_LAST_BLOCK = True
+
+
 class PatchEmbedding(nn.Module):
     """vit_encoder_decoder.py:11-108 (patch_size 1 use: 1x1 projection over the CNN grid)."""
 
@@ -89,6 +93,29 @@ class TransformerEncoderBlock(nn.Module):
         h = ops.gemm(ops.gemm(h, w0, bias=b0, act="gelu"), w3, bias=b3)
         return self.residual_mhc2.forward_tokens(h, residual=x)
 
+    def forward_tokens_cls(self, x: torch.Tensor, n: int) -> torch.Tensor:
+        """The block's output rows for the CLS tokens only, [n, D] (x: [n*L, D]).  Exact for a
+        final block whose only consumer is the CLS token (VisionTransformerEncoder :308-311,
+        HybridVisionEncoder :505-511): every op after attention's key/value projections is
+        per-token, so q_proj, out_proj, residual_mhc1, the MLP and residual_mhc2 run on n rows
+        instead of n*L (k_proj / v_proj still see every token)."""
+        L = x.shape[0] // n
+        att = self.attention
+        h = ops.rmsnorm(x, ops.f32(self.norm1.scale))
+        h_cls = ops.gather_rows(h, L)
+        x_cls = ops.gather_rows(x, L)
+        q = att.q_proj.forward_tokens(h_cls).view(n, 1, -1)
+        k = att.k_proj.forward_tokens(h).view(n, L, -1)
+        v = att.v_proj.forward_tokens(h).view(n, L, -1)
+        o, _ = ops.attention_general(q, k, v, att.num_heads)
+        a = att.out_proj.forward_tokens(o.view(n, -1))
+        x_cls = self.residual_mhc1.forward_tokens(a, residual=x_cls)
+        h = ops.rmsnorm(x_cls, ops.f32(self.norm2.scale))
+        w0, b0 = linear_prep(self.mlp[0], x.dtype)
+        w3, b3 = linear_prep(self.mlp[3], x.dtype)
+        h = ops.gemm(ops.gemm(h, w0, bias=b0, act="gelu"), w3, bias=b3)
+        return self.residual_mhc2.forward_tokens(h, residual=x_cls)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "TransformerEncoderBlock")
         if self.training:
@@ -128,11 +155,17 @@ class VisionTransformerEncoder(nn.Module):
         if features is not None:
             features.append(t)
         t = t.view(n * L, D)
-        for blk in self.blocks:
+        nb = len(self.blocks)
+        for i, blk in enumerate(self.blocks):
+            if i == nb - 1 and features is None and CLS_ONLY_LAST_BLOCK:
+                cls = blk.forward_tokens_cls(t, n)          # only the CLS rows survive (exact)
+                break
             t = blk.forward_tokens(t, n)
             if features is not None:
                 features.append(t.view(n, L, D))
-        cls = ops.rmsnorm(ops.gather_rows(t, L), ops.f32(self.norm.scale))   # only CLS survives
+        else:
+            cls = ops.gather_rows(t, L)
+        cls = ops.rmsnorm(cls, ops.f32(self.norm.scale))
         if head and isinstance(self.head, nn.Linear):
             w, b = linear_prep(self.head, cls.dtype)
             cls = ops.gemm(cls, w, bias=b)

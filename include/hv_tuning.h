@@ -46,6 +46,7 @@ enum hv_kernel_family {
   HV_KF_ATTN_MFMA = 7,       /* k_attention_mfma */
   HV_KF_ATTN_SCALAR = 8,     /* k_attention (fp32 / other head dims) */
   HV_KF_SINKHORN_GROUP = 9,  /* one grouped Sinkhorn forward (all its passes) */
+  HV_KF_ATTN_GENERAL = 10,   /* hv_attention_general (cross / masked / weights / CLS-row queries) */
   HV_KF_COUNT = 16
 };
 /* copies the HV_KF_COUNT launch counters into out[] */

@@ -368,7 +368,7 @@ def test_vit_return_features_and_extract(gpu_device):
     x = torch.randn(2, 64, 6, 6, generator=torch.Generator().manual_seed(3)).to(gpu_device)
     out, feats = enc(x, return_features=True)
     assert out.shape == (2, 10) and len(feats) == 3 and all(f.shape == (2, 37, 256) for f in feats)
-    assert torch.equal(out, enc(x))
+    torch.testing.assert_close(out, enc(x), rtol=0, atol=1e-5)     # enc(x): CLS-only last block
     cls = enc.extract_features(x)
     sd = {k: v.detach().cpu() for k, v in enc.state_dict().items()}
     ref_tok = O.rmsnorm(feats[-1].float().cpu(), sd["norm.scale"])[:, 0]
@@ -454,3 +454,30 @@ def test_streaming_pipeline_matches_eager_path(gpu_device):
     m.freeze(False)
     ref = eager(frames[1])
     np.testing.assert_array_equal(got["scores"], ref["scores"].cpu().numpy())
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_vit_shortcuts_match_plain_path(gpu_device, precision):
+    """The inference-path restructurings of the encoder are exact: the CLS-only last block
+    (only the CLS row survives, vit_encoder_decoder.py:308-311), the q/k/v projections on
+    three streams and the grouped q/k/v GEMM1 give the plain path's vit features (fp32: 1e-5; bf16: same GEMM kernels on
+    fewer rows -> rounding-level)."""
+    from hv_amd import manifold as MF
+    from hv_amd import vit as VT
+    m = _build("base", "wc", precision, gpu_device)
+    x = cases.model_input(2, 224).to(gpu_device)
+    outs = {}
+    for cls_only, par, grp in ((True, True, False), (False, False, False), (True, False, False),
+                               (True, False, True)):
+        VT.CLS_ONLY_LAST_BLOCK, MF.PARALLEL_QKV, MF.GROUP_QKV = cls_only, par, grp
+        try:
+            with torch.no_grad():
+                o = m(x)
+            outs[(cls_only, par, grp)] = (o["vit_features"].float().cpu(), o["predictions"]["scale_2"].cpu())
+        finally:
+            VT.CLS_ONLY_LAST_BLOCK, MF.PARALLEL_QKV, MF.GROUP_QKV = True, False, True
+    ref_v, ref_p = outs[(False, False, False)]
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    for key, (v, p) in outs.items():
+        assert (v - ref_v).abs().max().item() <= tol * max(1.0, ref_v.abs().max().item()), key
+    assert torch.equal(outs[(True, True, False)][0], outs[(True, False, False)][0])   # streams change no bits

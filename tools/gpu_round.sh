@@ -11,9 +11,9 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; } ; tail -3 $OUT/tests.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; } ; tail -2 $OUT/smoke.log ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
-    benchq) timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-latency > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
-    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --steps 20 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; } ; f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/prof_summary.txt; head -25 $OUT/prof_summary.txt ;;
-    profinf) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profinf -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --steps 20 > $OUT/profinf.log 2>&1 || { tail -30 $OUT/profinf.log; exit 1; } ; f=$(find $OUT/profinf -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/profinf_summary.txt; head -25 $OUT/profinf_summary.txt ;;
+    benchq) timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-stream --no-large --steps 20 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; } ; f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/prof_summary.txt; head -25 $OUT/prof_summary.txt ;;
+    profinf) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profinf -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 20 > $OUT/profinf.log 2>&1 || { tail -30 $OUT/profinf.log; exit 1; } ; f=$(find $OUT/profinf -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/profinf_summary.txt; head -25 $OUT/profinf_summary.txt ;;
     breakdown) timeout -k 10 300 python -u tools/gemm_breakdown.py > $OUT/gemm_breakdown.txt 2>&1 || { tail -30 $OUT/gemm_breakdown.txt; exit 1; } ; head -50 $OUT/gemm_breakdown.txt ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
