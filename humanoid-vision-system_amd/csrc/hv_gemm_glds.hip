@@ -489,6 +489,8 @@ std::atomic<int> g_train128{0};             // 128x128 tiles for the training ep
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
 extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
+std::atomic<int> g_force_tile{0};         // A/B: 0 auto, 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256
+extern "C" void hv_gemm_set_force_tile(int code) { g_force_tile = code; }
 std::atomic<int> g_conv_ktail{0};            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
 extern "C" void hv_gemm_set_conv_ktail(int on) { g_conv_ktail = on; }
 
@@ -504,6 +506,14 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   if (d.ldb % 8) return HV_EUNSUPPORTED;
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   const long t256 = (long)hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
+  switch (g_force_tile.load(std::memory_order_relaxed)) {
+    case 1: return launch<128, 128>(d, s);
+    case 2: return launch<64, 128>(d, s);
+    case 3: return launch<128, 64>(d, s);
+    case 4: return launch<64, 64>(d, s);
+    case 5: if (!d.epi_mode && d.K % 64 == 0) return launch256(d, s); break;
+    default: break;
+  }
   // 256x256 ping-pong kernel: long contractions with wide outputs on grids that still fill most
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
   // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for

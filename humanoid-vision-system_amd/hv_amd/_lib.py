@@ -119,6 +119,7 @@ _SIGS = {
     "hv_gemm_set_staged_epilogue": ([i32], None),
     "hv_gemm_set_deep_ring": ([i32], None),
     "hv_gemm_set_conv_ktail": ([i32], None),
+    "hv_gemm_set_force_tile": ([i32], None),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),
     "hv_layernorm": ([i32, vp, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp], i32),
     "hv_rmsnorm": ([i32, vp, i32, i32, f32, vp, vp, vp], i32),
@@ -185,6 +186,10 @@ _SIGS = {
     "hv_attention_train": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp], i32),
     "hv_attention_backward": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp,
                                vp, vp], i32),
+    "hv_attention_train_mfma_work_elems": ([i32, i32, i32], C.c_size_t),
+    "hv_attention_train_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp], i32),
+    "hv_attention_backward_mfma": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp, vp, vp],
+                                   i32),
     "hv_yolo_loss_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_yolo_loss": ([i32, vp, vp, i32, i32, i32, i32, i32, f32, f32, f32, f32, vp, i32, vp, vp, vp], i32),
     "hv_param_blocks": ([i64], i32),

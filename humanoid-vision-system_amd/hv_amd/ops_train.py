@@ -385,11 +385,27 @@ def scatter_rows(dy: Tensor, stride_rows: int) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- attention
+# bf16 attention with head_dim 32 runs on the matrix cores (hv_attention_*_mfma); False = the
+# scalar kernels (A/B and parity tests)
+ATTN_MFMA = True
+
+
+def _attn_mfma_ok(q: Tensor, heads: int) -> bool:
+    return ATTN_MFMA and q.dtype == torch.bfloat16 and q.shape[-1] == 32 * heads
+
+
 def attention_train(q: Tensor, k: Tensor, v: Tensor, heads: int, drop_p: float, seed: int):
     n, Lq, D = q.shape
     hd = D // heads
     o = torch.empty_like(q)
     lse = torch.empty((n, heads, Lq), device=q.device, dtype=torch.float32)
+    if _attn_mfma_ok(q, heads):
+        vt = torch.empty(L.lib().hv_attention_train_mfma_work_elems(n, Lq, heads), device=q.device, dtype=q.dtype)
+        check(L.lib().hv_attention_train_mfma(_contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
+                                              _contig(v, "v").data_ptr(), o.data_ptr(), lse.data_ptr(), n, Lq, heads,
+                                              hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, vt.data_ptr(),
+                                              stream_ptr()), "hv_attention_train_mfma")
+        return o, lse
     check(L.lib().hv_attention_train(dtype_code(q.dtype), _contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
                                      _contig(v, "v").data_ptr(), o.data_ptr(), lse.data_ptr(), n, Lq, heads, hd,
                                      hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, stream_ptr()),
@@ -401,6 +417,16 @@ def attention_backward(q, k, v, o, do, lse, heads: int, drop_p: float, seed: int
     n, Lq, D = q.shape
     hd = D // heads
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    if _attn_mfma_ok(q, heads) and do.dtype == q.dtype and o.dtype == q.dtype:
+        te = L.lib().hv_attention_train_mfma_work_elems(n, Lq, heads)
+        work = torch.empty(3 * te * 2 + n * heads * Lq * 4 + 64, device=q.device, dtype=torch.uint8)
+        check(L.lib().hv_attention_backward_mfma(_contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
+                                                 _contig(v, "v").data_ptr(), _contig(o, "o").data_ptr(),
+                                                 _contig(do, "dout").data_ptr(), lse.data_ptr(), n, Lq, heads,
+                                                 hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, dq.data_ptr(),
+                                                 dk.data_ptr(), dv.data_ptr(), work.data_ptr(), stream_ptr()),
+              "hv_attention_backward_mfma")
+        return dq, dk, dv
     work = _work(n * heads * Lq, q.device)
     check(L.lib().hv_attention_backward(dtype_code(q.dtype), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                                         _contig(do, "dout").data_ptr(), lse.data_ptr(), n, Lq, heads, hd, hd ** -0.5,

@@ -42,6 +42,14 @@ def mhc_group(name: str) -> int:
 class GradBuckets:
     """Flat gradient storage + bucketed, hook-driven all-reduce (average over ranks).
 
+    During the backward every parameter's .grad starts as None, so autograd STORES the
+    gradient its producer computed (no accumulate kernel per parameter, which at 1,149
+    parameters was ~1,250 tiny `add` launches per step).  When a bucket's last parameter has
+    its gradient, one segmented-copy launch (hv_copy_segments) moves the bucket into its span of
+    the flat buffer and, with world > 1, that span's all-reduce starts (RCCL over xGMI) while the
+    rest of the backward runs.  finish() leaves every param.grad as a view of the flat buffer
+    (zero for parameters that got no gradient) for the clipping / AdamW table.
+
     Works on any device / process-group backend: the CPU `gloo` tests drive it with plain
     torch modules, the GPU trainer with RCCL ('nccl')."""
 
@@ -53,10 +61,13 @@ class GradBuckets:
         total = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
         self.offsets: Dict[int, int] = {}
+        self.views: List[Tensor] = []
         off = 0
         for p in self.params:
             self.offsets[id(p)] = off
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            v = self.flat[off:off + p.numel()].view_as(p)
+            self.views.append(v)
+            p.grad = v
             off += p.numel()
         # buckets over the reverse order (backward produces the last layers first)
         self.buckets: List[List[Tensor]] = []
@@ -73,23 +84,17 @@ class GradBuckets:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self._pending: List = []
-        self._ready = [0] * len(self.buckets)
+        self._ready = [set() for _ in self.buckets]
+        self._flushed = [False] * len(self.buckets)
         # which parameters received a gradient this step: the optimizer skips the others like
-        # torch.optim skips grad=None (optimizer.py:144) -- the flat views are never None
+        # torch.optim skips grad=None (optimizer.py:144)
         self.received = [False] * len(self.params)
         self._index = {id(p): i for i, p in enumerate(self.params)}
         # the engine runs a leaf's hooks even when its producer returned None for it (e.g. the
         # grouped Sinkhorn's unused final-fusion projection), so receipt is read from the
-        # gradient itself in a tensor hook; bucket readiness stays on the post-accumulate hook
+        # gradient itself in a tensor hook; bucket readiness is counted in the post-accumulate hook
         self._hooks = [p.register_hook(self._flag_hook(i)) for i, p in enumerate(self.params)]
-        if self.world > 1:
-            self._hooks += [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
-
-    def _span(self, i: int):
-        b = self.buckets[i]
-        lo = min(self.offsets[id(p)] for p in b)
-        hi = max(self.offsets[id(p)] + p.numel() for p in b)
-        return lo, hi
+        self._hooks += [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def _flag_hook(self, idx: int):
         def hook(g):
@@ -97,39 +102,81 @@ class GradBuckets:
                 self.received[idx] = True
         return hook
 
-    def _on_grad(self, p: Tensor):
-        i = self.bucket_of[id(p)]
-        self._ready[i] += 1
-        if self._ready[i] == len(self.buckets[i]):
+    def _span(self, i: int):
+        b = self.buckets[i]
+        lo = min(self.offsets[id(p)] for p in b)
+        hi = max(self.offsets[id(p)] + p.numel() for p in b)
+        return lo, hi
+
+    def _flush(self, params) -> None:
+        """Move the stored (non-view) gradients of `params` into the flat buffer."""
+        pairs = []
+        for p in params:
+            g = p.grad
+            v = self.views[self._index[id(p)]]
+            if g is None or g.data_ptr() == v.data_ptr():
+                continue
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                g = g.float().contiguous()
+            pairs.append((g, v))
+        if not pairs:
+            return
+        if pairs[0][1].is_cuda:
+            from . import _lib as L
+            segs = (L.CopySegment * len(pairs))()
+            for j, (g, v) in enumerate(pairs):
+                segs[j].src, segs[j].dst, segs[j].bytes = g.data_ptr(), v.data_ptr(), g.numel() * 4
+            check(L.lib().hv_copy_segments(segs, len(pairs), stream_ptr()), "hv_copy_segments")
+        else:                                   # CPU (gloo tests): host copies
+            with torch.no_grad():
+                for g, v in pairs:
+                    v.copy_(g)
+        for g, v in pairs:                       # keep the sources alive until the copy ran
+            if g.is_cuda:
+                g.record_stream(torch.cuda.current_stream())
+
+    def _reduce(self, i: int) -> None:
+        if self.world > 1:
             lo, hi = self._span(i)
             view = self.flat[lo:hi]
             view.div_(self.world)
             self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
 
+    def _on_grad(self, p: Tensor):
+        i = self.bucket_of[id(p)]
+        self._ready[i].add(id(p))
+        if len(self._ready[i]) == len(self.buckets[i]) and not self._flushed[i]:
+            self._flush(self.buckets[i])
+            self._flushed[i] = True
+            for q in self.buckets[i]:            # free the stored gradients now
+                q.grad = self.views[self._index[id(q)]]
+            self._reduce(i)
+
     def zero(self):
-        for p in self.params:          # autograd may have replaced a view (e.g. set_to_none)
-            off = self.offsets[id(p)]
-            if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
-                p.grad = self.flat[off:off + p.numel()].view_as(p)
+        """Start a step: flat buffer zeroed (one fill), every param.grad set to None so the
+        backward stores rather than accumulates."""
         self.flat.zero_()
+        for p in self.params:
+            p.grad = None
         self.received = [False] * len(self.params)
-        self._ready = [0] * len(self.buckets)
+        self._ready = [set() for _ in self.buckets]
+        self._flushed = [False] * len(self.buckets)
         self._pending = []
 
     def finish(self):
-        """Wait for every bucket's all-reduce; buckets whose parameters got no gradient this
-        step (unused branches) are reduced here so every rank stays in lock-step."""
-        if self.world > 1:
-            for i, b in enumerate(self.buckets):
-                if self._ready[i] != len(b):
-                    lo, hi = self._span(i)
-                    view = self.flat[lo:hi]
-                    view.div_(self.world)
-                    self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
-                    self._ready[i] = len(b)
-            for w in self._pending:
-                w.wait()
+        """Flush and reduce the buckets not completed by the hooks (parameters that got no
+        gradient: every rank reduces the same spans, so ranks stay in lock-step), wait for the
+        all-reduces, and point every param.grad at its flat view."""
+        for i, b in enumerate(self.buckets):
+            if not self._flushed[i]:
+                self._flush(b)
+                self._flushed[i] = True
+                self._reduce(i)
+        for w in self._pending:
+            w.wait()
         self._pending = []
+        for p, v in zip(self.params, self.views):
+            p.grad = v
 
 
 class FusedAdamW:

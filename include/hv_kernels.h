@@ -502,6 +502,17 @@ int hv_attention_backward(int dtype, const void* q, const void* k, const void* v
                           const void* dout, const float* lse, int n, int L, int heads, int hd,
                           float sm_scale, float drop_p, unsigned int seed, void* dq, void* dk, void* dv,
                           float* work, hv_stream_t stream);
+/* The same two operations on the matrix cores (bf16, head_dim 32): identical dropout keep(i, j)
+   and lse convention, so the forward and backward of either path pair.  vt_work /  work hold
+   transposed zero-padded [n*heads, 32, Lp] operand copies (hv_attention_train_mfma_work_elems
+   bf16 elements each; the backward needs 3 of them followed by n*heads*L floats). */
+size_t hv_attention_train_mfma_work_elems(int n, int L, int heads);
+int hv_attention_train_mfma(const void* q, const void* k, const void* v, void* o, float* lse, int n, int L,
+                            int heads, float sm_scale, float drop_p, unsigned int seed, void* vt_work,
+                            hv_stream_t stream);
+int hv_attention_backward_mfma(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                               const float* lse, int n, int L, int heads, float sm_scale, float drop_p,
+                               unsigned int seed, void* dq, void* dk, void* dv, void* work, hv_stream_t stream);
 
 /* YOLOLoss for one scale (yolo_head.py:374-465): logits NHWC [n, h, w, A*P], targets
    [n, A, h, w, P] fp32.  Writes sums[0..3] = raw coord / obj / noobj / cls sums, sums[4] =

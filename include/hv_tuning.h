@@ -27,6 +27,8 @@ void hv_gemm_set_train128(int on);
 void hv_gemm_set_staged_epilogue(int on);
 /* deeper LDS-DMA rings (4 / 3 buffers) for the 64x64 / 64x128 / 128x64 tiles: 1 on (default), 0 = 2 */
 void hv_gemm_set_deep_ring(int on);
+/* force the LDS-DMA tile: 0 auto (default), 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256 ping-pong */
+void hv_gemm_set_force_tile(int code);
 /* convolutions with K % 64 != 0 (channels % 8 == 0) on the LDS-DMA kernel: 0 off (default), 1 on */
 void hv_gemm_set_conv_ktail(int on);
 /* fused mHC: 1 also dispatches (256, 512) to the fused kernel (off by default: slower) */

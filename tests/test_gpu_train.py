@@ -318,6 +318,36 @@ def test_attention_train_backward(gpu_device, prec):
         assert rel(a.float(), r.transpose(1, 2).reshape(n, L, H * hd)) < (1e-4 if prec == "fp32" else 3e-2)
 
 
+@pytest.mark.parametrize("L,p", [(1, 0.0), (17, 0.1), (50, 0.0), (401, 0.1), (130, 0.3)])
+def test_attention_train_mfma_matches_scalar(gpu_device, L, p):
+    """The bf16 matrix-core attention (forward with lse + dropout, key-parallel dK/dV and
+    query-parallel dQ backward) against the scalar kernels on the same inputs and the same
+    dropout seed: identical masks (keep(i, j) regenerated from (seed, element)), so the outputs
+    and gradients agree to bf16 rounding; L = 401 is the ViT at 640²."""
+    T = OT()
+    n, H, hd = 2, 8, 32
+    g = torch.Generator().manual_seed(L)
+    q, k, v, do = (torch.randn(n, L, H * hd, generator=g).to(torch.bfloat16).to(gpu_device) for _ in range(4))
+    res = {}
+    for mfma in (True, False):
+        T.ATTN_MFMA = mfma
+        try:
+            o, lse = T.attention_train(q, k, v, H, p, 1234)
+            dq, dk, dv = T.attention_backward(q, k, v, o, do, lse, H, p, 1234)
+        finally:
+            T.ATTN_MFMA = True
+        res[mfma] = (o, lse, dq, dk, dv)
+    assert (res[True][1] - res[False][1]).abs().max().item() < 2e-3           # lse
+    for a, b_ in zip(res[True][:1] + res[True][2:], res[False][:1] + res[False][2:]):
+        if b_.abs().max().item() == 0:      # L = 1: softmax of one key is 1, dS = 0 exactly; rounding only
+            assert a.float().abs().max().item() < 1e-2
+        else:
+            assert rel(a.float(), b_.float()) < 2e-2
+    dv = res[True][4].float()
+    assert abs((dv * v.float()).sum().item() - (do.float() * res[True][0].float()).sum().item()) \
+        < 2e-2 * max(1.0, abs((do.float() * res[True][0].float()).sum().item()))
+
+
 def test_attention_dropout_consistent(gpu_device):
     """With dropout the backward must see the forward's mask: check dv = (P*mask)^T do."""
     T = OT()
