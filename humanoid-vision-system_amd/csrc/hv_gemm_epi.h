@@ -206,7 +206,7 @@ __device__ __forceinline__ float4* epi_lds_chunk(unsigned char* smem, int r, int
 
 // Row tile A of the wave's accumulators -> LDS image rows lrow0 + A*16 + fr (fp32, activation
 // applied).  Template recursion over A keeps every acc index a constant.
-template <int A, bool LN_EPI, int RM, int RN, int CPR>
+template <int A, bool LN_EPI, int RM, int RN, int CPR, bool TRAIN = false>
 __device__ __forceinline__ void epi_stage_rows(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN], const EpiCols<RN>& k,
                                                int grow0, int lrow0, int lcol0, unsigned char* smem) {
   if constexpr (A < RM) {
@@ -225,18 +225,94 @@ __device__ __forceinline__ void epi_stage_rows(const hv_gemm_desc& d, const f32x
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float x = acc[A][b][j];
-        if constexpr (LN_EPI) x = rstd * (x - mean * k.cs[b][j]);
-        x = x * k.sc[b][j] + k.bi[b][j];
-        v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+        if constexpr (TRAIN) {
+          // training modes stage the pre-activation (mode 1) / the scaled product (mode 2); the
+          // write-out applies act + dropout (or their backward) on whole rows
+          if (d.epi_mode == 1) {
+            if constexpr (LN_EPI) x = rstd * (x - mean * k.cs[b][j]);
+            v[j] = x * k.sc[b][j] + k.bi[b][j];
+          } else {
+            v[j] = x * d.alpha;
+          }
+        } else {
+          if constexpr (LN_EPI) x = rstd * (x - mean * k.cs[b][j]);
+          x = x * k.sc[b][j] + k.bi[b][j];
+          v[j] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+        }
       }
       *epi_lds_chunk<CPR>(smem, lrow0 + A * 16 + fr, (lcol0 + b * 16) / 4 + fg) = make_float4(v[0], v[1], v[2], v[3]);
     }
-    epi_stage_rows<A + 1, LN_EPI, RM, RN, CPR>(d, acc, k, grow0, lrow0, lcol0, smem);
+    epi_stage_rows<A + 1, LN_EPI, RM, RN, CPR, TRAIN>(d, acc, k, grow0, lrow0, lcol0, smem);
   }
 }
 
 // Coalesced write-out of an LDS image of SLAB rows (tile rows r0 ..) x BN columns.
-template <int BN, int NT, int SLAB>
+// training write-out of 8 staged values (row, col .. col+7): mode 1 stores the pre-activation z
+// to aux (rounded like the fragment epilogue) and returns act(z) * keep; mode 2 reads aux and
+// returns z * keep * act'(aux).  keep(m, n) = hv_drop_scale(seed, m * N + n), as epi_train.
+__device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8], int row, int col, bool vec8) {
+  const bool aux_bf = d.aux_dtype == HV_BF16;
+  const long ai = (long)row * d.ld_aux + col;
+  const unsigned long long idx0 = (unsigned long long)row * d.N + col;
+  const bool av = vec8 && (d.ld_aux & 7) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
+  float z[8];
+  if (d.epi_mode == 1) {
+    if (av && aux_bf) {
+      const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                                  pack_bf16x2(v[6], v[7]));
+      *reinterpret_cast<uint4*>((unsigned short*)d.aux + ai) = pk;
+      const unsigned pw[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        z[2 * q] = __uint_as_float(pw[q] << 16);
+        z[2 * q + 1] = __uint_as_float(pw[q] & 0xffff0000u);
+      }
+    } else if (av) {
+      float* o = (float*)d.aux + ai;
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = v[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        z[j] = v[j];
+        if (col + j >= d.N) continue;
+        if (aux_bf) {
+          ((unsigned short*)d.aux)[ai + j] = f2bf(v[j]);
+          z[j] = bf2f(f2bf(v[j]));
+        } else {
+          ((float*)d.aux)[ai + j] = v[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
+  } else {
+    if (av && aux_bf) {
+      const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
+      const unsigned tw[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        z[2 * q] = __uint_as_float(tw[q] << 16);
+        z[2 * q + 1] = __uint_as_float(tw[q] & 0xffff0000u);
+      }
+    } else if (av) {
+      const float4 t0 = *reinterpret_cast<const float4*>((const float*)d.aux + ai);
+      const float4 t1 = *reinterpret_cast<const float4*>((const float*)d.aux + ai + 4);
+      z[0] = t0.x; z[1] = t0.y; z[2] = t0.z; z[3] = t0.w; z[4] = t1.x; z[5] = t1.y; z[6] = t1.z; z[7] = t1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        z[j] = col + j < d.N ? (aux_bf ? bf2f(((const unsigned short*)d.aux)[ai + j]) : ((const float*)d.aux)[ai + j])
+                             : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+  }
+}
+
+template <int BN, int NT, int SLAB, bool TRAIN = false>
 __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
   const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
   const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
@@ -252,6 +328,7 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
     if (row >= d.M || col >= d.N) continue;
     const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if constexpr (TRAIN) epi_train8(d, v, row, col, col + 8 <= d.N);
     const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
     if (vec && col + 8 <= d.N) {
       if (d.residual) {
@@ -295,7 +372,7 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
   }
 }
 
-template <int BM, int BN, bool LN_EPI, int WN, int RM, int RN, int NT, int SLAB>
+template <int BM, int BN, bool LN_EPI, int WN, int RM, int RN, int NT, int SLAB, bool TRAIN = false>
 __device__ __forceinline__ void gemm_epilogue_staged(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN], int m0, int n0,
                                                      unsigned char* smem) {
   static_assert(BN % 8 == 0 && SLAB % 16 == 0 && (BM == SLAB || BM == 2 * SLAB), "shape");
@@ -315,10 +392,11 @@ __device__ __forceinline__ void gemm_epilogue_staged(const hv_gemm_desc& d, cons
     }
   const int wrow0 = wr * (RM * 16);
   if constexpr (BM == SLAB) {
-    epi_stage_rows<0, LN_EPI, RM, RN, BN / 4>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);
+    epi_stage_rows<0, LN_EPI, RM, RN, BN / 4, TRAIN>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);
     __syncthreads();
-    epi_writeout<BN, NT, SLAB>(d, m0, n0, smem);
-  } else {                                      // two slabs: the waves of rows [0, SLAB) first
+    epi_writeout<BN, NT, SLAB, TRAIN>(d, m0, n0, smem);
+  } else {
+    static_assert(!TRAIN, "two-slab staging is inference-only");                                      // two slabs: the waves of rows [0, SLAB) first
     if (wrow0 < SLAB) epi_stage_rows<0, LN_EPI, RM, RN, BN / 4>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);
     __syncthreads();
     epi_writeout<BN, NT, SLAB>(d, m0, n0, smem);

@@ -192,9 +192,9 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 
   // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
   //      LN_EPI: LayerNorm after the product)
-  if constexpr (STAGED && !TRAIN) {
-    if (d.a_mean) gemm_epilogue_staged<BM, BN, true, 2, RM, RN, 256, BM>(d, acc, m0, n0, smem);
-    else gemm_epilogue_staged<BM, BN, false, 2, RM, RN, 256, BM>(d, acc, m0, n0, smem);
+  if constexpr (STAGED) {
+    if (d.a_mean) gemm_epilogue_staged<BM, BN, true, 2, RM, RN, 256, BM, TRAIN>(d, acc, m0, n0, smem);
+    else gemm_epilogue_staged<BM, BN, false, 2, RM, RN, 256, BM, TRAIN>(d, acc, m0, n0, smem);
   } else {
     if (d.a_mean) gemm_epilogue<BM, BN, true, TRAIN>(d, acc, m0, n0);
     else gemm_epilogue<BM, BN, false, TRAIN>(d, acc, m0, n0);
@@ -432,6 +432,7 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   }
 }
 
+std::atomic<int> g_staged_train{1};   // LDS-staged epilogue for the training modes (A/B knob)
 std::atomic<int> g_staged_epi{1};             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
 
 int launch256(const hv_gemm_desc& d, hipStream_t s) {
@@ -457,8 +458,13 @@ int launch_ns(const hv_gemm_desc& d, hipStream_t s) {
   hv_diag_count(BM == 128 && BN == 128 ? HV_KF_GEMM_GLDS_128x128 : BM == 64 && BN == 128 ? HV_KF_GEMM_GLDS_64x128
                 : BM == 128 ? HV_KF_GEMM_GLDS_128x64 : HV_KF_GEMM_GLDS_64x64);
   if (d.epi_mode) {
-    if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, false, NS><<<grid, 256, 0, s>>>(d);
-    else gemm_glds_kernel<BM, BN, false, true, false, NS><<<grid, 256, 0, s>>>(d);
+    if (g_staged_train) {
+      if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, true, NS><<<grid, 256, 0, s>>>(d);
+      else gemm_glds_kernel<BM, BN, false, true, true, NS><<<grid, 256, 0, s>>>(d);
+    } else {
+      if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, false, NS><<<grid, 256, 0, s>>>(d);
+      else gemm_glds_kernel<BM, BN, false, true, false, NS><<<grid, 256, 0, s>>>(d);
+    }
   } else if (g_staged_epi) {
     if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, true, NS><<<grid, 256, 0, s>>>(d);
     else gemm_glds_kernel<BM, BN, false, false, true, NS><<<grid, 256, 0, s>>>(d);
@@ -488,6 +494,7 @@ int hv_gemm_small_tile_mode();  // hv_gemm.hip
 std::atomic<int> g_train128{0};             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
+extern "C" void hv_gemm_set_staged_train(int on) { g_staged_train = on; }
 extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
 std::atomic<int> g_force_tile{0};         // A/B: 0 auto, 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256
 extern "C" void hv_gemm_set_force_tile(int code) { g_force_tile = code; }

@@ -120,6 +120,7 @@ _SIGS = {
     "hv_gemm_set_deep_ring": ([i32], None),
     "hv_gemm_set_conv_ktail": ([i32], None),
     "hv_gemm_set_force_tile": ([i32], None),
+    "hv_gemm_set_staged_train": ([i32], None),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),
     "hv_layernorm": ([i32, vp, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp], i32),
     "hv_rmsnorm": ([i32, vp, i32, i32, f32, vp, vp, vp], i32),

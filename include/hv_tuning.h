@@ -25,6 +25,8 @@ void hv_gemm_set_small_tile(int mode);
 void hv_gemm_set_train128(int on);
 /* LDS-staged coalesced epilogue for the LDS-DMA kernels (inference modes): 1 on (default), 0 off */
 void hv_gemm_set_staged_epilogue(int on);
+/* LDS-staged epilogue for the training modes (epi_mode 1/2) of the LDS-DMA kernels: 1 on (default), 0 off */
+void hv_gemm_set_staged_train(int on);
 /* deeper LDS-DMA rings (4 / 3 buffers) for the 64x64 / 64x128 / 128x64 tiles: 1 on (default), 0 = 2 */
 void hv_gemm_set_deep_ring(int on);
 /* force the LDS-DMA tile: 0 auto (default), 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256 ping-pong */

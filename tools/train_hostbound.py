@@ -15,6 +15,11 @@ from hv_amd.trainer import HVTrainer  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 640
 dev = torch.device("cuda")
+from hv_amd import _lib  # noqa: E402
+for knob, fn in (("HV_TRAIN128", "hv_gemm_set_train128"), ("HV_STAGED_TRAIN", "hv_gemm_set_staged_train")):
+    if os.environ.get(knob) is not None:
+        getattr(_lib.lib(), fn)(int(os.environ[knob]))
+        print(f"{knob}={os.environ[knob]}")
 torch.manual_seed(0)
 m = HybridVisionSystem({"image_size": S, "verbose": False}).to(dev).train()
 tr = HVTrainer(m)
