@@ -14,6 +14,9 @@
 // entries), nothing syncs with the host, and the a/b/r vectors of every iteration stay in
 // the workspace for the analytic backward.  Summation order is fixed -> bitwise
 // reproducible.
+#include <atomic>
+#include <mutex>
+
 #include "hv_common.h"
 
 namespace {
@@ -36,6 +39,14 @@ __device__ __forceinline__ Work carve(const hv_sinkhorn_entry& e) {
   w.r = w.b + (long)(e.iters + 1) * bm;
   w.part = w.r + (long)e.iters * bn;
   return w;
+}
+
+// Entries of at most 256 x 256 (65 of the model's 76 matrices: D = 32 .. 256) run the whole
+// projection in ONE workgroup (sk_small: K in registers, all iterations inside); the grouped
+// multi-launch passes below skip them and handle only the large ones (D = 512, 1024, 1792).
+// small_max = 0 sends every entry through the grouped passes (A/B knob hv_sinkhorn_set_small).
+__device__ __forceinline__ bool sk_is_small(const hv_sinkhorn_entry& e, int small_max) {
+  return e.batch == 1 && e.n <= small_max && e.m <= small_max;
 }
 
 // Find the entry whose [start, start+len) range contains idx (entries sorted by start).
@@ -66,12 +77,13 @@ __device__ __forceinline__ float sum_partials(const float* __restrict__ part, in
 
 // K = softmax(raw / tau, -1) * m (manifold_layers.py:56-57); a_0 = b_0 = 1.
 __global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restrict__ tab,
-                                               int count, int total_rows) {
+                                               int count, int total_rows, int small_max) {
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= total_rows) return;
   const int ei = find_entry<0>(tab, count, g);
   const hv_sinkhorn_entry e = tab[ei];
+  if (sk_is_small(e, small_max)) return;
   const int row = g - e.row_start;               // row within batch*n
   const float* src = e.raw + (long)row * e.m;
   float* dst = e.out + (long)row * e.m;
@@ -89,20 +101,21 @@ __global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restri
 }
 
 __global__ void __launch_bounds__(256) sk_init_cols(const hv_sinkhorn_entry* __restrict__ tab,
-                                                    int count, int total_cols) {
+                                                    int count, int total_cols, int small_max) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= total_cols) return;
   const hv_sinkhorn_entry e = tab[find_entry<2>(tab, count, g)];
+  if (sk_is_small(e, small_max)) return;
   carve(e).b[g - e.col_start] = 1.0f;
 }
 
 // Iteration t, pass 1: row dots -> r_t, a_t+1 ; column partial sums of a_t+1 (.) K.
 __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restrict__ tab,
-                                               int count, int t) {
+                                               int count, int t, int small_max) {
   __shared__ float colpart[4][64 * MAXQ];
   const int ei = find_entry<1>(tab, count, blockIdx.x);
   const hv_sinkhorn_entry e = tab[ei];
-  if (t >= e.iters) return;
+  if (t >= e.iters || sk_is_small(e, small_max)) return;
   const Work w = carve(e);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nrb = (e.n + RB - 1) / RB;
@@ -116,32 +129,46 @@ __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restri
   float* an = w.a + (long)(t + 1) * e.batch * n + (long)bidx * n;
   float* rt = w.r + (long)t * e.batch * n + (long)bidx * n;
 
-  float bq[MAXQ], acc[MAXQ];
+  // all RB/4 rows of this wave are loaded before any reduction: one memory round trip per
+  // pass instead of one per row (the row pass is latency-bound: 21 launches per forward)
+  constexpr int RW = RB / 4;
+  const int i0 = rb * RB + wv * RW;
+  float bq[MAXQ], acc[MAXQ], kv[RW][MAXQ];
 #pragma unroll
   for (int q = 0; q < MAXQ; ++q) {
     const int j = lane + 64 * q;
     bq[q] = (q < nq && j < m) ? bt[j] : 0.f;
     acc[q] = 0.f;
   }
-  for (int rr = 0; rr < RB / 4; ++rr) {
-    const int i = rb * RB + wv * (RB / 4) + rr;
-    if (i >= n) break;
-    const float* Ki = K + (long)i * m;
-    float kv[MAXQ];
-    float dot = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) {
+    const float* Ki = K + (long)(i0 + rr) * m;
+    const bool ok = i0 + rr < n;
 #pragma unroll
     for (int q = 0; q < MAXQ; ++q) {
       const int j = lane + 64 * q;
-      kv[q] = (q < nq && j < m) ? Ki[j] : 0.f;
-      dot += kv[q] * bq[q];
+      kv[rr][q] = (ok && q < nq && j < m) ? Ki[j] : 0.f;
     }
-    dot = wave_sum(dot);
+  }
+  float dot[RW];
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) {
+    dot[rr] = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) dot[rr] += kv[rr][q] * bq[q];
+  }
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) dot[rr] = wave_sum(dot[rr]);
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) {
+    const int i = i0 + rr;
+    if (i >= n) break;
     const float ai = at[i];
-    const float r = ai * dot;
+    const float r = ai * dot[rr];
     const float a1 = ai / (r + e.eps);
     if (lane == 0) { rt[i] = r; an[i] = a1; }
 #pragma unroll
-    for (int q = 0; q < MAXQ; ++q) acc[q] += a1 * kv[q];
+    for (int q = 0; q < MAXQ; ++q) acc[q] += a1 * kv[rr][q];
   }
 #pragma unroll
   for (int q = 0; q < MAXQ; ++q)
@@ -152,20 +179,41 @@ __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restri
     part[j] = (colpart[0][j] + colpart[1][j]) + (colpart[2][j] + colpart[3][j]);
 }
 
-// Iteration t, pass 2: c_t = b_t (.) sum(partials); b_t+1 = b_t / (c_t + eps).
+// Iteration t, pass 2: c_t = b_t (.) sum(partials); b_t+1 = b_t / (c_t + eps).  A block owns 64
+// consecutive columns; its 4 waves sum interleaved quarters of the nrb partial rows (8 loads in
+// flight each), combined in a fixed order through LDS.
 __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restrict__ tab,
-                                               int count, int total_cols, int t) {
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= total_cols) return;
-  const int ei = find_entry<2>(tab, count, g);
-  const hv_sinkhorn_entry e = tab[ei];
-  if (t >= e.iters) return;
+                                               int count, int total_cols, int t, int small_max) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = blockIdx.x * 64 + lane;
+  bool live = g < total_cols;
+  hv_sinkhorn_entry e;
+  if (live) {
+    e = tab[find_entry<2>(tab, count, g)];
+    live = t < e.iters && !sk_is_small(e, small_max);
+  }
+  float s = 0.f;
+  int c = 0;
+  if (live) {
+    c = g - e.col_start;                     // within batch*m
+    const int bidx = c / e.m, j = c % e.m;
+    const int nrb = (e.n + RB - 1) / RB;
+    const float* part = carve(e).part + (long)bidx * nrb * e.m + j;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = wv, k = 0;
+    for (; r + 28 < nrb; r += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += part[(long)(r + 4 * u) * e.m];
+    }
+    for (; r < nrb; r += 4, k = (k + 1) & 7) acc[k] += part[(long)r * e.m];
+    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv != 0 || !live) return;
+  s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   const Work w = carve(e);
-  const int c = g - e.col_start;           // within batch*m
-  const int bidx = c / e.m, j = c % e.m;
-  const int nrb = (e.n + RB - 1) / RB;
-  const float* part = w.part + (long)bidx * nrb * e.m + j;
-  const float s = sum_partials(part, nrb, e.m);
   const long bm = (long)e.batch * e.m;
   const float b = w.b[(long)t * bm + c];
   const float cs = b * s;
@@ -174,12 +222,13 @@ __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restri
 
 // M = diag(a_T) K diag(b_T) in place; history[t] = |mean_i r_t,i - 1| (:76-77).
 __global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restrict__ tab,
-                                                int count, int total_rows) {
+                                                int count, int total_rows, int small_max) {
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= total_rows) return;
   const int ei = find_entry<0>(tab, count, g);
   const hv_sinkhorn_entry e = tab[ei];
+  if (sk_is_small(e, small_max)) return;
   const Work w = carve(e);
   const int row = g - e.row_start;
   const int bidx = row / e.n;
@@ -199,6 +248,135 @@ __global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restr
   }
 }
 
+
+// ---- one workgroup per small entry (n, m <= 256): thread (tr, tc) of a 32 x 32 grid (1,024
+// threads) holds K rows tr + 32 i, columns tc + 32 j in registers (R x R, R <= 8) for all
+// iterations.  Row dots reduce over the 32 lanes of a row group (xor shuffles), column sums over
+// the 32 row groups through LDS in a fixed order -- deterministic.  Writes the same a/b/r
+// history as the grouped passes (the backward reads it) and M / convergence_history.
+constexpr int SKG = 32;                    // thread grid side
+template <int R>
+__device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float* sm) {
+  const int t = threadIdx.x, tr = t / SKG, tc = t % SKG;
+  const int n = e.n, m = e.m, iters = e.iters;
+  const Work w = carve(e);
+  float* bl = sm;                        // [256] current b
+  float* al = sm + 256;                  // [256] current a
+  float* part = sm + 512;                // [SKG][256] column partials
+  float* rh = sm + 512 + SKG * 256;      // [iters][256] row sums (history)
+  float kv[R][R];
+  const float inv_tau = 1.0f / e.tau;
+  // K = softmax(raw / tau, -1) * m
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = tr + SKG * i;
+    const bool rv = row < n;
+    float x[R];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int col = tc + SKG * j;
+      x[j] = (rv && col < m) ? e.raw[(long)row * m + col] * inv_tau : -INFINITY;
+      mx = fmaxf(mx, x[j]);
+    }
+#pragma unroll
+    for (int o = SKG / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      x[j] = (rv && tc + SKG * j < m) ? __expf(x[j] - mx) : 0.f;
+      sum += x[j];
+    }
+#pragma unroll
+    for (int o = SKG / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    const float k = rv ? (float)m / sum : 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) kv[i][j] = rv ? x[j] * k : 0.f;
+  }
+  if (t < m) { bl[t] = 1.0f; w.b[t] = 1.0f; }
+  if (t < n) { al[t] = 1.0f; w.a[t] = 1.0f; }
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    // rows: r_i = a_i (K b)_i ; a_i <- a_i / (r_i + eps)
+    float bj[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) bj[j] = (tc + SKG * j < m) ? bl[tc + SKG * j] : 0.f;
+    float anew[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j) d += kv[i][j] * bj[j];
+#pragma unroll
+      for (int o = SKG / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      const int row = tr + SKG * i;
+      const float ai = row < n ? al[row] : 0.f;
+      const float r = ai * d;
+      anew[i] = row < n ? ai / (r + e.eps) : 0.f;
+      if (tc == 0 && row < n) {
+        rh[it * 256 + row] = r;
+        w.r[(long)it * n + row] = r;
+        w.a[(long)(it + 1) * n + row] = anew[i];
+      }
+    }
+    __syncthreads();                       // every read of al / bl of this iteration done
+    // columns: partial over this thread's rows of a_new (.) K
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      float c = 0.f;
+#pragma unroll
+      for (int i = 0; i < R; ++i) c += anew[i] * kv[i][j];
+      if (tc + SKG * j < m) part[tr * 256 + tc + SKG * j] = c;
+    }
+    if (tc == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        if (tr + SKG * i < n) al[tr + SKG * i] = anew[i];
+    }
+    __syncthreads();
+    if (t < m) {
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < SKG; ++g) s += part[g * 256 + t];
+      const float b = bl[t];
+      const float c = b * s;
+      const float bn = b / (c + e.eps);
+      bl[t] = bn;
+      w.b[(long)(it + 1) * m + t] = bn;
+    }
+    __syncthreads();
+  }
+  // M = diag(a_T) K diag(b_T)
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = tr + SKG * i;
+    if (row >= n) continue;
+    const float ai = al[row];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int col = tc + SKG * j;
+      if (col < m) e.out[(long)row * m + col] = ai * kv[i][j] * bl[col];
+    }
+  }
+  // history[t] = |mean_i r_t,i - 1| (fixed-order sum)
+  if (e.history && t < iters) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += rh[t * 256 + i];
+    e.history[t] = fabsf(s / (float)n - 1.0f);
+  }
+}
+
+__global__ void __launch_bounds__(1024) sk_small(const hv_sinkhorn_entry* __restrict__ tab, int count, int small_max) {
+  extern __shared__ float sk_sm[];
+  const hv_sinkhorn_entry e = tab[blockIdx.x];
+  if (!sk_is_small(e, small_max)) return;
+  const int mx = e.n > e.m ? e.n : e.m;
+  if (mx <= 32) sk_small_body<1>(e, sk_sm);
+  else if (mx <= 64) sk_small_body<2>(e, sk_sm);
+  else if (mx <= 128) sk_small_body<4>(e, sk_sm);
+  else sk_small_body<8>(e, sk_sm);
+}
+
 }  // namespace
 
 extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
@@ -208,22 +386,58 @@ extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
          (size_t)batch * nrb * m;
 }
 
+namespace {
+std::atomic<int> g_sk_small{1};
+
+int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipStream_t s) {
+  // the small entries: one workgroup each, every iteration inside (LDS: a, b, partials, history)
+  const size_t lds = (size_t)(512 + SKG * 256 + (max_iters > 0 ? max_iters : 1) * 256) * sizeof(float);
+  if (lds > 160 * 1024) return HV_EUNSUPPORTED;
+  static std::once_flag attr;
+  std::call_once(attr, [] {
+    (void)hipFuncSetAttribute((const void*)sk_small, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  sk_small<<<count, 1024, lds, s>>>(tab, count, 256);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+int sk_launch_large(const hv_sinkhorn_entry* tab, int count, int total_rows, int total_row_blocks, int total_cols,
+                    int max_iters, hipStream_t s) {
+  const int sm = g_sk_small.load(std::memory_order_relaxed) ? 256 : 0;
+  sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows, sm);
+  sk_init_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, sm);
+  HV_CHECK_LAUNCH();
+  for (int t = 0; t < max_iters; ++t) {
+    sk_rows<<<total_row_blocks, 256, 0, s>>>(tab, count, t, sm);
+    sk_cols<<<hv_cdiv(total_cols, 64), 256, 0, s>>>(tab, count, total_cols, t, sm);
+  }
+  HV_CHECK_LAUNCH();
+  sk_final<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows, sm);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+}  // namespace
+
+extern "C" void hv_sinkhorn_set_small(int on) { g_sk_small = on; }
+
 extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count, int total_rows,
                                          int total_row_blocks, int total_cols, int max_iters,
                                          hv_stream_t stream) {
-  hv_diag_count(HV_KF_SINKHORN_GROUP);
-  if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0) return HV_EINVAL;
+  return hv_sinkhorn_group_forward_part(tab, count, total_rows, total_row_blocks, total_cols, max_iters, 0, stream);
+}
+
+extern "C" int hv_sinkhorn_group_forward_part(const hv_sinkhorn_entry* tab, int count, int total_rows,
+                                              int total_row_blocks, int total_cols, int max_iters, int part,
+                                              hv_stream_t stream) {
+  if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0 || part < 0 || part > 2) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
-  sk_init_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols);
-  HV_CHECK_LAUNCH();
-  for (int t = 0; t < max_iters; ++t) {
-    sk_rows<<<total_row_blocks, 256, 0, s>>>(tab, count, t);
-    sk_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, t);
+  hv_diag_count(HV_KF_SINKHORN_GROUP);
+  if (part != 2 && g_sk_small.load(std::memory_order_relaxed)) {
+    const int rc = sk_launch_small(tab, count, max_iters, s);
+    if (rc != HV_OK) return rc;
   }
-  HV_CHECK_LAUNCH();
-  sk_final<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows);
-  HV_CHECK_LAUNCH();
+  if (part != 1) return sk_launch_large(tab, count, total_rows, total_row_blocks, total_cols, max_iters, s);
   return HV_OK;
 }
 

@@ -105,12 +105,14 @@ _SIGS = {
     "hv_mhc_fused": ([vp, vp], i32),
     "hv_mhc_fused_enable_wide": ([i32], None),
     "hv_mhc_fused_set_variant": ([i32], None),
+    "hv_sinkhorn_set_small": ([i32], None),
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),
     "hv_struct_sizes": ([vp], None),
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_forward": ([vp, i32, i32, i32, i32, i32, vp], i32),
+    "hv_sinkhorn_group_forward_part": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
     "hv_gemm": ([vp, vp], i32),
     "hv_gemm_set_path": ([i32], None),
     "hv_gemm_set_big_tile": ([i32], None),

@@ -239,6 +239,9 @@ def rmsnorm(x: Tensor, scale: Tensor, eps: float = 1e-8) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- sinkhorn
+SINKHORN_SPLIT = False  # small / large entries on two streams (graph branches): measured 0.1 ms slower
+
+
 class SinkhornGroup:
     """A device table of Sinkhorn problems launched together (hv_sinkhorn_group_forward).
 
@@ -277,6 +280,9 @@ class SinkhornGroup:
             cs += b * m
         self.entries = entries
         self.totals = (rs, rbs, cs)
+        small = [e.batch == 1 and e.n <= 256 and e.m <= 256 for e in entries]
+        self.has_small, self.has_large = any(small), not all(small)
+        self._side = None
         self.table = None
         self._raw_ptrs = None
         self.device = device
@@ -290,7 +296,23 @@ class SinkhornGroup:
             self.table = upload_table(self.entries, self.device)
             self._raw_ptrs = rp
         rs, rbs, cs = self.totals
-        check(L.lib().hv_sinkhorn_group_forward(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
+        lib = L.lib()
+        if SINKHORN_SPLIT and self.has_small and self.has_large:
+            # small matrices (one workgroup each) on a side stream beside the grouped passes of the
+            # large ones: two branches of a captured graph
+            main = torch.cuda.current_stream()
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
+                                                         max(self.iters), 1, stream_ptr()),
+                      "hv_sinkhorn_group_forward_part")
+            check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
+                                                     max(self.iters), 2, stream_ptr()), "hv_sinkhorn_group_forward_part")
+            main.wait_stream(self._side)
+        else:
+            check(lib.hv_sinkhorn_group_forward(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
                                                 max(self.iters), stream_ptr()), "hv_sinkhorn_group_forward")
         return self.outs
 

@@ -62,6 +62,13 @@ size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters);
 int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* dev_table, int count,
                               int total_rows, int total_row_blocks, int total_cols,
                               int max_iters, hv_stream_t stream);
+/* The same, split for two streams (a captured graph's parallel branches): part 1 = the small
+   entries (<= 256 x 256: one workgroup each, all iterations inside one launch), part 2 = the
+   large ones (grouped row / column passes), 0 = both on `stream`.  Parts 1 and 2 touch
+   disjoint entries. */
+int hv_sinkhorn_group_forward_part(const hv_sinkhorn_entry* tab, int count, int total_rows,
+                                   int total_row_blocks, int total_cols, int max_iters, int part,
+                                   hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * MFMA GEMM with fused prologue/epilogue:  C[M,N] = epi( A'[M,K] . B[N,K]^T )

@@ -38,7 +38,9 @@ def test_sinkhorn_matches_reference_fixture(gpu_device, fam, D, it):
     np.testing.assert_allclose(M[idx].numpy(), g["rows"], rtol=2e-5, atol=1e-7)
     np.testing.assert_allclose(M.sum(0).numpy(), g["col_sums"], rtol=2e-5)
     np.testing.assert_allclose(M.sum(1).numpy(), g["row_sums"], rtol=2e-5)
-    np.testing.assert_allclose(hist.cpu().numpy(), g["history"], rtol=1e-3, atol=2e-7)
+    # history = |mean_i r_i - 1| with r_i ~ 1: the subtraction exposes the mean's own rounding
+    # (a few fp32 ulps of 1.0 = 1.2e-7 each, summation-order dependent) at full size
+    np.testing.assert_allclose(hist.cpu().numpy(), g["history"], rtol=1e-3, atol=5e-7)
     if "M" in g.files:
         np.testing.assert_allclose(M.numpy(), g["M"], rtol=2e-5, atol=1e-8)
 

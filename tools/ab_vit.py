@@ -9,6 +9,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
 from hv_amd import HybridVisionSystem  # noqa: E402
 from hv_amd import manifold as MF  # noqa: E402
+from hv_amd import _lib as LIB  # noqa: E402
+from hv_amd import ops as OPS  # noqa: E402
 from hv_amd import vit as VT  # noqa: E402
 
 SWITCHES = {
@@ -16,6 +18,8 @@ SWITCHES = {
     "parallel_qkv": lambda: setattr(MF, "PARALLEL_QKV", True),
     "no_cls_only": lambda: setattr(VT, "CLS_ONLY_LAST_BLOCK", False),
     "no_group_qkv": lambda: setattr(MF, "GROUP_QKV", False),
+    "sk_split": lambda: setattr(OPS, "SINKHORN_SPLIT", True),
+    "no_sk_small": lambda: LIB.lib().hv_sinkhorn_set_small(0),
 }
 
 
@@ -23,6 +27,8 @@ def reset():
     MF.PARALLEL_QKV = False
     MF.GROUP_QKV = True
     VT.CLS_ONLY_LAST_BLOCK = True
+    OPS.SINKHORN_SPLIT = False
+    LIB.lib().hv_sinkhorn_set_small(1)
 
 
 def main():
