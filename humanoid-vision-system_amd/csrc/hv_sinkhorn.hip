@@ -14,7 +14,6 @@
 // entries), nothing syncs with the host, and the a/b/r vectors of every iteration stay in
 // the workspace for the analytic backward.  Summation order is fixed -> bitwise
 // reproducible.
-#include <atomic>
 #include <mutex>
 
 #include "hv_common.h"
@@ -51,14 +50,42 @@ __device__ __forceinline__ bool sk_is_small(const hv_sinkhorn_entry& e, int smal
 
 // Find the entry whose [start, start+len) range contains idx (entries sorted by start).
 template <int FIELD>
+__device__ __forceinline__ int entry_start(const hv_sinkhorn_entry& e) {
+  return FIELD == 0 ? e.row_start : (FIELD == 1 ? e.row_block_start : e.col_start);
+}
+template <int FIELD>
 __device__ __forceinline__ int find_entry(const hv_sinkhorn_entry* t, int count, int idx) {
   int lo = 0, hi = count - 1;
   while (lo < hi) {
     int mid = (lo + hi + 1) >> 1;
-    int s = FIELD == 0 ? t[mid].row_start : (FIELD == 1 ? t[mid].row_block_start : t[mid].col_start);
-    if (s <= idx) lo = mid; else hi = mid - 1;
+    if (entry_start<FIELD>(t[mid]) <= idx) lo = mid; else hi = mid - 1;
   }
   return lo;
+}
+template <int FIELD>
+__device__ __forceinline__ int find_entry_wave(const hv_sinkhorn_entry* t, int count, int idx);
+// Per-lane idx inside [first, last] (wave-uniform bounds): when both ends fall in one entry (the
+// common case -- the large entries' column ranges are multiples of 64) two ballots decide it.
+template <int FIELD>
+__device__ __forceinline__ int find_entry_span(const hv_sinkhorn_entry* t, int count, int idx, int first,
+                                               int last) {
+  const int e0 = find_entry_wave<FIELD>(t, count, first);
+  const int e1 = find_entry_wave<FIELD>(t, count, last);
+  return e0 == e1 ? e0 : find_entry<FIELD>(t, count, idx);
+}
+// The same for a wave-uniform idx: each lane reads one entry's start, a ballot counts the starts
+// <= idx.  One memory round trip per 64 entries instead of log2(count) dependent ones (the
+// grouped passes are latency-bound launches, ~20 per forward).  Whole wave must be active.
+template <int FIELD>
+__device__ __forceinline__ int find_entry_wave(const hv_sinkhorn_entry* t, int count, int idx) {
+  const int lane = threadIdx.x & 63;
+  int n_le = 0;
+  for (int base = 0; base < count; base += 64) {
+    const int k = base + lane;
+    const int st = k < count ? entry_start<FIELD>(t[k]) : 0x7fffffff;
+    n_le += __popcll(__ballot(st <= idx));
+  }
+  return n_le - 1;
 }
 
 // Fixed-order sum of nrb row-block partials of one column (stride m): eight independent
@@ -81,8 +108,7 @@ __global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restri
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= total_rows) return;
-  const int ei = find_entry<0>(tab, count, g);
-  const hv_sinkhorn_entry e = tab[ei];
+  const hv_sinkhorn_entry e = tab[find_entry_wave<0>(tab, count, g)];
   if (sk_is_small(e, small_max)) return;
   const int row = g - e.row_start;               // row within batch*n
   const float* src = e.raw + (long)row * e.m;
@@ -103,9 +129,11 @@ __global__ void __launch_bounds__(256) sk_init(const hv_sinkhorn_entry* __restri
 __global__ void __launch_bounds__(256) sk_init_cols(const hv_sinkhorn_entry* __restrict__ tab,
                                                     int count, int total_cols, int small_max) {
   const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= total_cols) return;
-  const hv_sinkhorn_entry e = tab[find_entry<2>(tab, count, g)];
-  if (sk_is_small(e, small_max)) return;
+  const int w0 = g & ~63;
+  if (w0 >= total_cols) return;                  // wave-uniform
+  const int gl = g < total_cols ? g : total_cols - 1;
+  const hv_sinkhorn_entry e = tab[find_entry_span<2>(tab, count, gl, w0, min(w0 + 63, total_cols - 1))];
+  if (g >= total_cols || sk_is_small(e, small_max)) return;
   carve(e).b[g - e.col_start] = 1.0f;
 }
 
@@ -113,8 +141,7 @@ __global__ void __launch_bounds__(256) sk_init_cols(const hv_sinkhorn_entry* __r
 __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restrict__ tab,
                                                int count, int t, int small_max) {
   __shared__ float colpart[4][64 * MAXQ];
-  const int ei = find_entry<1>(tab, count, blockIdx.x);
-  const hv_sinkhorn_entry e = tab[ei];
+  const hv_sinkhorn_entry e = tab[find_entry_wave<1>(tab, count, blockIdx.x)];
   if (t >= e.iters || sk_is_small(e, small_max)) return;
   const Work w = carve(e);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -150,7 +177,9 @@ __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restri
       kv[rr][q] = (ok && q < nq && j < m) ? Ki[j] : 0.f;
     }
   }
-  float dot[RW];
+  float dot[RW], ar[RW];
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) ar[rr] = i0 + rr < n ? at[i0 + rr] : 0.f;
 #pragma unroll
   for (int rr = 0; rr < RW; ++rr) {
     dot[rr] = 0.f;
@@ -163,7 +192,7 @@ __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restri
   for (int rr = 0; rr < RW; ++rr) {
     const int i = i0 + rr;
     if (i >= n) break;
-    const float ai = at[i];
+    const float ai = ar[rr];
     const float r = ai * dot[rr];
     const float a1 = ai / (r + e.eps);
     if (lane == 0) { rt[i] = r; an[i] = a1; }
@@ -186,17 +215,17 @@ __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restri
                                                int count, int total_cols, int t, int small_max) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = blockIdx.x * 64 + lane;
-  bool live = g < total_cols;
-  hv_sinkhorn_entry e;
-  if (live) {
-    e = tab[find_entry<2>(tab, count, g)];
-    live = t < e.iters && !sk_is_small(e, small_max);
-  }
-  float s = 0.f;
+  const int g0 = blockIdx.x * 64;                // < total_cols by the grid
+  const int g = g0 + lane;
+  const int gl = g < total_cols ? g : total_cols - 1;
+  const hv_sinkhorn_entry e = tab[find_entry_span<2>(tab, count, gl, g0, min(g0 + 63, total_cols - 1))];
+  const bool live = g < total_cols && t < e.iters && !sk_is_small(e, small_max);
+  float s = 0.f, bprev = 0.f;
   int c = 0;
+  const long bm = (long)e.batch * e.m;
   if (live) {
     c = g - e.col_start;                     // within batch*m
+    if (wv == 0) bprev = carve(e).b[(long)t * bm + c];   // issued before the partial sums
     const int bidx = c / e.m, j = c % e.m;
     const int nrb = (e.n + RB - 1) / RB;
     const float* part = carve(e).part + (long)bidx * nrb * e.m + j;
@@ -213,11 +242,8 @@ __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restri
   __syncthreads();
   if (wv != 0 || !live) return;
   s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-  const Work w = carve(e);
-  const long bm = (long)e.batch * e.m;
-  const float b = w.b[(long)t * bm + c];
-  const float cs = b * s;
-  w.b[(long)(t + 1) * bm + c] = b / (cs + e.eps);
+  const float cs = bprev * s;
+  carve(e).b[(long)(t + 1) * bm + c] = bprev / (cs + e.eps);
 }
 
 // M = diag(a_T) K diag(b_T) in place; history[t] = |mean_i r_t,i - 1| (:76-77).
@@ -226,8 +252,7 @@ __global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restr
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (g >= total_rows) return;
-  const int ei = find_entry<0>(tab, count, g);
-  const hv_sinkhorn_entry e = tab[ei];
+  const hv_sinkhorn_entry e = tab[find_entry_wave<0>(tab, count, g)];
   if (sk_is_small(e, small_max)) return;
   const Work w = carve(e);
   const int row = g - e.row_start;
@@ -255,7 +280,7 @@ __global__ void __launch_bounds__(256) sk_final(const hv_sinkhorn_entry* __restr
 // the 32 row groups through LDS in a fixed order -- deterministic.  Writes the same a/b/r
 // history as the grouped passes (the backward reads it) and M / convergence_history.
 constexpr int SKG = 32;                    // thread grid side
-template <int R>
+template <int R, bool FULL>
 __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float* sm) {
   const int t = threadIdx.x, tr = t / SKG, tc = t % SKG;
   const int n = e.n, m = e.m, iters = e.iters;
@@ -270,13 +295,13 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = tr + SKG * i;
-    const bool rv = row < n;
+    const bool rv = FULL || row < n;
     float x[R];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int col = tc + SKG * j;
-      x[j] = (rv && col < m) ? e.raw[(long)row * m + col] * inv_tau : -INFINITY;
+      x[j] = (rv && (FULL || col < m)) ? e.raw[(long)row * m + col] * inv_tau : -INFINITY;
       mx = fmaxf(mx, x[j]);
     }
 #pragma unroll
@@ -284,7 +309,7 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      x[j] = (rv && tc + SKG * j < m) ? __expf(x[j] - mx) : 0.f;
+      x[j] = (rv && (FULL || tc + SKG * j < m)) ? __expf(x[j] - mx) : 0.f;
       sum += x[j];
     }
 #pragma unroll
@@ -300,7 +325,7 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
     // rows: r_i = a_i (K b)_i ; a_i <- a_i / (r_i + eps)
     float bj[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) bj[j] = (tc + SKG * j < m) ? bl[tc + SKG * j] : 0.f;
+    for (int j = 0; j < R; ++j) bj[j] = (FULL || tc + SKG * j < m) ? bl[tc + SKG * j] : 0.f;
     float anew[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -310,10 +335,10 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
 #pragma unroll
       for (int o = SKG / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
       const int row = tr + SKG * i;
-      const float ai = row < n ? al[row] : 0.f;
+      const float ai = (FULL || row < n) ? al[row] : 0.f;
       const float r = ai * d;
-      anew[i] = row < n ? ai / (r + e.eps) : 0.f;
-      if (tc == 0 && row < n) {
+      anew[i] = (FULL || row < n) ? ai / (r + e.eps) : 0.f;
+      if (tc == 0 && (FULL || row < n)) {
         rh[it * 256 + row] = r;
         w.r[(long)it * n + row] = r;
         w.a[(long)(it + 1) * n + row] = anew[i];
@@ -326,12 +351,12 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
       float c = 0.f;
 #pragma unroll
       for (int i = 0; i < R; ++i) c += anew[i] * kv[i][j];
-      if (tc + SKG * j < m) part[tr * 256 + tc + SKG * j] = c;
+      if (FULL || tc + SKG * j < m) part[tr * 256 + tc + SKG * j] = c;
     }
     if (tc == 0) {
 #pragma unroll
       for (int i = 0; i < R; ++i)
-        if (tr + SKG * i < n) al[tr + SKG * i] = anew[i];
+        if (FULL || tr + SKG * i < n) al[tr + SKG * i] = anew[i];
     }
     __syncthreads();
     if (t < m) {
@@ -350,12 +375,12 @@ __device__ __forceinline__ void sk_small_body(const hv_sinkhorn_entry& e, float*
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int row = tr + SKG * i;
-    if (row >= n) continue;
+    if (!FULL && row >= n) continue;
     const float ai = al[row];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int col = tc + SKG * j;
-      if (col < m) e.out[(long)row * m + col] = ai * kv[i][j] * bl[col];
+      if (FULL || col < m) e.out[(long)row * m + col] = ai * kv[i][j] * bl[col];
     }
   }
   // history[t] = |mean_i r_t,i - 1| (fixed-order sum)
@@ -371,10 +396,13 @@ __global__ void __launch_bounds__(1024) sk_small(const hv_sinkhorn_entry* __rest
   const hv_sinkhorn_entry e = tab[blockIdx.x];
   if (!sk_is_small(e, small_max)) return;
   const int mx = e.n > e.m ? e.n : e.m;
-  if (mx <= 32) sk_small_body<1>(e, sk_sm);
-  else if (mx <= 64) sk_small_body<2>(e, sk_sm);
-  else if (mx <= 128) sk_small_body<4>(e, sk_sm);
-  else sk_small_body<8>(e, sk_sm);
+  // FULL: n == m == 32 R (the model's D = 32, 64, 128, 256) -- no bounds masks, which keeps the
+  // R = 8 body (64 K values per thread) inside the 128 VGPRs of a 1,024-thread workgroup
+  const bool full = e.n == e.m && (e.n == 32 || e.n == 64 || e.n == 128 || e.n == 256);
+  if (mx <= 32) { if (full) sk_small_body<1, true>(e, sk_sm); else sk_small_body<1, false>(e, sk_sm); }
+  else if (mx <= 64) { if (full) sk_small_body<2, true>(e, sk_sm); else sk_small_body<2, false>(e, sk_sm); }
+  else if (mx <= 128) { if (full) sk_small_body<4, true>(e, sk_sm); else sk_small_body<4, false>(e, sk_sm); }
+  else { if (full) sk_small_body<8, true>(e, sk_sm); else sk_small_body<8, false>(e, sk_sm); }
 }
 
 }  // namespace
@@ -387,8 +415,6 @@ extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
 }
 
 namespace {
-std::atomic<int> g_sk_small{1};
-
 int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipStream_t s) {
   // the small entries: one workgroup each, every iteration inside (LDS: a, b, partials, history)
   const size_t lds = (size_t)(512 + SKG * 256 + (max_iters > 0 ? max_iters : 1) * 256) * sizeof(float);
@@ -404,7 +430,7 @@ int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipS
 
 int sk_launch_large(const hv_sinkhorn_entry* tab, int count, int total_rows, int total_row_blocks, int total_cols,
                     int max_iters, hipStream_t s) {
-  const int sm = g_sk_small.load(std::memory_order_relaxed) ? 256 : 0;
+  const int sm = 256;
   sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows, sm);
   sk_init_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, sm);
   HV_CHECK_LAUNCH();
@@ -419,8 +445,6 @@ int sk_launch_large(const hv_sinkhorn_entry* tab, int count, int total_rows, int
 }
 }  // namespace
 
-extern "C" void hv_sinkhorn_set_small(int on) { g_sk_small = on; }
-
 extern "C" int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* tab, int count, int total_rows,
                                          int total_row_blocks, int total_cols, int max_iters,
                                          hv_stream_t stream) {
@@ -433,7 +457,7 @@ extern "C" int hv_sinkhorn_group_forward_part(const hv_sinkhorn_entry* tab, int 
   if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0 || part < 0 || part > 2) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hv_diag_count(HV_KF_SINKHORN_GROUP);
-  if (part != 2 && g_sk_small.load(std::memory_order_relaxed)) {
+  if (part != 2) {
     const int rc = sk_launch_small(tab, count, max_iters, s);
     if (rc != HV_OK) return rc;
   }

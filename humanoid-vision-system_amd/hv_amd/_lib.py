@@ -105,7 +105,6 @@ _SIGS = {
     "hv_mhc_fused": ([vp, vp], i32),
     "hv_mhc_fused_enable_wide": ([i32], None),
     "hv_mhc_fused_set_variant": ([i32], None),
-    "hv_sinkhorn_set_small": ([i32], None),
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),

@@ -282,8 +282,22 @@ class SinkhornGroup:
         self.totals = (rs, rbs, cs)
         small = [e.batch == 1 and e.n <= 256 and e.m <= 256 for e in entries]
         self.has_small, self.has_large = any(small), not all(small)
+        # the grouped passes get a table of the large entries alone (own prefix sums): no idle
+        # blocks for the small ones and a short entry search; same work pointers as the full table
+        self._large_idx = [i for i, sm in enumerate(small) if not sm]
+        self.entries_large = (L.SinkhornEntry * max(1, len(self._large_idx)))()
+        rs_l = rbs_l = cs_l = 0
+        for k, i in enumerate(self._large_idx):
+            el = self.entries_large[k]
+            C.memmove(C.addressof(el), C.addressof(entries[i]), C.sizeof(el))
+            el.row_start, el.row_block_start, el.col_start = rs_l, rbs_l, cs_l
+            rs_l += el.batch * el.n
+            rbs_l += el.batch * ((el.n + 15) // 16)
+            cs_l += el.batch * el.m
+        self.totals_large = (rs_l, rbs_l, cs_l)
         self._side = None
         self.table = None
+        self.table_large = None
         self._raw_ptrs = None
         self.device = device
 
@@ -293,10 +307,25 @@ class SinkhornGroup:
         if rp != self._raw_ptrs:
             for e, p in zip(self.entries, rp):
                 e.raw = p
+            for k, i in enumerate(self._large_idx):
+                self.entries_large[k].raw = rp[i]
             self.table = upload_table(self.entries, self.device)
+            if self.has_large:
+                self.table_large = upload_table(self.entries_large, self.device)
             self._raw_ptrs = rp
-        rs, rbs, cs = self.totals
         lib = L.lib()
+        mx = max(self.iters)
+
+        def small():
+            rs, rbs, cs = self.totals
+            check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs, mx, 1,
+                                                     stream_ptr()), "hv_sinkhorn_group_forward_part")
+
+        def large():
+            rs, rbs, cs = self.totals_large
+            check(lib.hv_sinkhorn_group_forward_part(self.table_large.data_ptr(), len(self._large_idx), rs, rbs,
+                                                     cs, mx, 2, stream_ptr()), "hv_sinkhorn_group_forward_part")
+
         if SINKHORN_SPLIT and self.has_small and self.has_large:
             # small matrices (one workgroup each) on a side stream beside the grouped passes of the
             # large ones: two branches of a captured graph
@@ -305,15 +334,14 @@ class SinkhornGroup:
                 self._side = torch.cuda.Stream(device=self.device)
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
-                check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
-                                                         max(self.iters), 1, stream_ptr()),
-                      "hv_sinkhorn_group_forward_part")
-            check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
-                                                     max(self.iters), 2, stream_ptr()), "hv_sinkhorn_group_forward_part")
+                small()
+            large()
             main.wait_stream(self._side)
         else:
-            check(lib.hv_sinkhorn_group_forward(self.table.data_ptr(), len(self.entries), rs, rbs, cs,
-                                                max(self.iters), stream_ptr()), "hv_sinkhorn_group_forward")
+            if self.has_small:
+                small()
+            if self.has_large:
+                large()
         return self.outs
 
 

@@ -37,9 +37,6 @@ void hv_gemm_set_conv_ktail(int on);
 void hv_mhc_fused_enable_wide(int on);
 /* fused mHC workgroup shape: 0 default (4-wave groups), 1 three groups per CU, 2 one 8-wave group */
 void hv_mhc_fused_set_variant(int v);
-/* Sinkhorn: 1 (default) = entries <= 256 x 256 in one workgroup each (sk_small), 0 = every entry
-   through the grouped row / column passes. */
-void hv_sinkhorn_set_small(int on);
 
 /* kernel families counted by hv_diag_launch_counts */
 enum hv_kernel_family {

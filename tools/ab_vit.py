@@ -9,7 +9,6 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
 from hv_amd import HybridVisionSystem  # noqa: E402
 from hv_amd import manifold as MF  # noqa: E402
-from hv_amd import _lib as LIB  # noqa: E402
 from hv_amd import ops as OPS  # noqa: E402
 from hv_amd import vit as VT  # noqa: E402
 
@@ -19,7 +18,6 @@ SWITCHES = {
     "no_cls_only": lambda: setattr(VT, "CLS_ONLY_LAST_BLOCK", False),
     "no_group_qkv": lambda: setattr(MF, "GROUP_QKV", False),
     "sk_split": lambda: setattr(OPS, "SINKHORN_SPLIT", True),
-    "no_sk_small": lambda: LIB.lib().hv_sinkhorn_set_small(0),
 }
 
 
@@ -28,7 +26,6 @@ def reset():
     MF.GROUP_QKV = True
     VT.CLS_ONLY_LAST_BLOCK = True
     OPS.SINKHORN_SPLIT = False
-    LIB.lib().hv_sinkhorn_set_small(1)
 
 
 def main():
