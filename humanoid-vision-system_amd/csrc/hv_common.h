@@ -121,6 +121,16 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return t;
 }
 
+// Device-side bounds checks of the debug build (`make debug` -> libhvs_debug.so, -DHV_DEBUG):
+// a violation prints its file:line and condition; no trap (a trapping wave faults the device
+// for every process on it).  Release builds compile them out.
+#ifdef HV_DEBUG
+#define HV_DCHECK(cond) \
+  do { if (!(cond)) printf("HV_DCHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); } while (0)
+#else
+#define HV_DCHECK(cond) do {} while (0)
+#endif
+
 #define HV_CHECK_LAUNCH() \
   do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 

@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   }
   const int tm = bid / tilesN, tn = bid % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
+  HV_DCHECK(tm < tilesM && (CONV || d.K % 64 == 0) && (d.A2 == nullptr || d.k1 % 64 == 0));
 
   // ---- per-lane source rows: wave instruction i covers tile rows 8*(wid*AI+i) .. +7
   const int lrow = lane >> 3;               // row within the 8-row group
@@ -490,13 +491,14 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
 }  // namespace
 
 int hv_gemm_big_tile_mode();   // hv_gemm.hip
+int hv_gemm_smallk(const hv_gemm_desc& d, hipStream_t s, bool force);   // hv_gemm_sk.hip
 int hv_gemm_small_tile_mode();  // hv_gemm.hip
 std::atomic<int> g_train128{0};             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
 extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
 extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
 extern "C" void hv_gemm_set_staged_train(int on) { g_staged_train = on; }
 extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
-std::atomic<int> g_force_tile{0};         // A/B: 0 auto, 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256
+std::atomic<int> g_force_tile{0};         // A/B: 0 auto, 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256, 6 small-K
 extern "C" void hv_gemm_set_force_tile(int code) { g_force_tile = code; }
 std::atomic<int> g_conv_ktail{0};            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
 extern "C" void hv_gemm_set_conv_ktail(int on) { g_conv_ktail = on; }
@@ -519,7 +521,12 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
     case 3: return launch<128, 64>(d, s);
     case 4: return launch<64, 64>(d, s);
     case 5: if (!d.epi_mode && d.K % 64 == 0) return launch256(d, s); break;
-    default: break;
+    case 6: return hv_gemm_smallk(d, s, true);
+    default: {
+      const int rc = hv_gemm_smallk(d, s, false);             // persistent small-K kernel (hv_gemm_sk.hip)
+      if (rc != HV_EUNSUPPORTED) return rc;
+      break;
+    }
   }
   // 256x256 ping-pong kernel: long contractions with wide outputs on grids that still fill most
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024

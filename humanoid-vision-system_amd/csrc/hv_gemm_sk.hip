@@ -1,0 +1,310 @@
+// Persistent small-K bf16 GEMM for gfx950 (K <= 512): the LN-epilogue GEMM1s of the mHC sites
+// (25600x2048x256, 102400x1024x256, 6416x3072x256, 6400x4096x512 ...) and the 1x1 convolutions.
+//
+// At K <= 512 a 128x128 tile is 1-8 MFMA k-steps, so the non-persistent ring kernel spends most of
+// a tile's life in its prologue (first DMA round trip) and its epilogue (LDS staging + barriers),
+// and its output stream -- the dominant byte count here (25600x2048 bf16 = 105 MB against 14 MB
+// of operands) -- runs at 1.2-1.5 TB/s (tools/k256_probe2.py).  This kernel:
+//
+//  * is PERSISTENT: grid = 2 workgroups per CU, each walks tiles r*G + remap(bid) (XCD-aware per
+//    round, so the 16 N-tiles of one A row block share an L2);
+//  * keeps ONE continuous LDS-DMA k-stream across its tiles: the last k-step of tile t issues the
+//    DMA of tile t+1's first k-tile, so that round trip overlaps tile t's MFMAs and epilogue;
+//  * has a REGISTER epilogue with 16-byte stores and no LDS: the B tile's rows are loaded
+//    N-PERMUTED (LDS row b*16 + 4g + j of a wave's half <- physical column 16g + 4b + j), so after
+//    the transposed MFMAs lane (fr, g) holds 16 CONSECUTIVE output columns of one row across its
+//    four 16x16 sub-tiles -> two 16-byte bf16 stores (64 contiguous bytes per 4 lanes), LDS free
+//    for the next tile's DMA, no barrier in the epilogue.
+//
+// Same arithmetic as hv_gemm_epi.h (LN after the product, scale*alpha, bias, act, residual), same
+// MFMA k-order as the ring kernel -> identical results.
+#include <atomic>
+
+#include "hv_common.h"
+
+namespace {
+
+constexpr int SK_ROW = 128;                         // bytes per LDS row (64 bf16 of K)
+constexpr int SK_BM = 128, SK_BN = 128;
+constexpr int SK_STAGE = (SK_BM + SK_BN) * SK_ROW;  // 32 KiB per k-tile buffer
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void sk_glds16(const void* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// physical column (within a wave's 64) of LDS B row q = b*16 + 4g + j
+__device__ __forceinline__ int sk_perm(int q) { return ((q & 15) >> 2) * 16 + (q >> 4) * 4 + (q & 3); }
+
+// tile of round `round` for this workgroup: XCD-aware inside full rounds (consecutive tiles on
+// one XCD, as the ring kernel's remap), identity in the last partial round; -1 = done
+__device__ __forceinline__ int sk_tile(int round, int ntiles) {
+  const int G = gridDim.x, bid = blockIdx.x;
+  const long base = (long)round * G;
+  if (base + G <= ntiles) {
+    const int xcd = bid & 7, q = G >> 3, r = G & 7;
+    return (int)base + (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  return base + bid < ntiles ? (int)(base + bid) : -1;
+}
+
+// DIAG (hv_gemm_set_smallk 2 / 3, tools/k256_probe2.py only): 1 = skip the stores, 2 = skip the
+// k-loop (DMA + MFMA) -- the two halves of a tile's time, measured apart.  0 in the product.
+template <bool LN, int DIAG = 0>
+__global__ void __launch_bounds__(256, 2) gemm_sk_kernel(const hv_gemm_desc d, int ntiles) {
+  constexpr int AI = SK_BM / 32, BI = SK_BN / 32, RM = 4, RN = 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SK_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7, lchunk = pchunk ^ (lrow & 7);
+  const int tilesN = (d.N + SK_BN - 1) / SK_BN;
+  const int nk = d.K / 64;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+
+  // per-lane DMA source rows of a tile: A rows m0 + r, B rows n0 + permuted(r)
+  struct Src {
+    const unsigned short* a[AI];
+    const unsigned short* b[BI];
+  };
+  auto src_of = [&](int tile, Src& s) {
+    const int m0 = (tile / tilesN) * SK_BM, n0 = (tile % tilesN) * SK_BN;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = min(m0 + (wid * AI + i) * 8 + lrow, d.M - 1);
+      s.a[i] = (const unsigned short*)d.A + (long)row * d.lda;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int r = (wid * BI + i) * 8 + lrow;             // LDS B row 0..127
+      const int n = min(n0 + (r >> 6) * 64 + sk_perm(r & 63), d.N - 1);
+      s.b[i] = (const unsigned short*)d.B + (long)n * d.ldb;
+    }
+  };
+  auto stage = [&](const Src& s, int buf, int kt) {
+    const unsigned la = lds0 + buf * SK_STAGE + wu * AI * 1024;
+    const unsigned lb = lds0 + buf * SK_STAGE + SK_BM * SK_ROW + wu * BI * 1024;
+    const int k = kt * 64 + lchunk * 8;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) sk_glds16(s.a[i] + k, la + i * 1024);
+#pragma unroll
+    for (int i = 0; i < BI; ++i) sk_glds16(s.b[i] + k, lb + i * 1024);
+  };
+
+  int tile = sk_tile(0, ntiles);
+  if (tile < 0) return;                                    // workgroup-uniform
+  Src cur, nxt;
+  src_of(tile, cur);
+  stage(cur, 0, 0);
+  int buf = 0;
+  const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
+  const bool gelu_fast = c_bf && !d.residual;
+  const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
+                   (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
+
+  bool prev_full = false;       // the previous tile's epilogue issued exactly its full-tile stores
+  for (int round = 0;; ++round) {
+    const int next = sk_tile(round + 1, ntiles);
+    if (next >= 0) src_of(next, nxt);
+    const int m0 = (tile / tilesN) * SK_BM, n0 = (tile % tilesN) * SK_BN;
+    // epilogue constants fetched now, their latency under the k-loop's MFMAs
+    const int col0 = n0 + wc * 64 + fg * 16;
+    float sc[16], bi[16], cs[16], mean[RM], rstd[RM];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int col = col0 + j;
+      const bool ok = col < d.N;
+      sc[j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
+      bi[j] = (d.bias && ok) ? d.bias[col] : 0.f;
+      cs[j] = 0.f;
+      if constexpr (LN) cs[j] = ok ? d.b_colsum[col] : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < RM; ++a) {
+      const int row = min(m0 + wr * 64 + a * 16 + fr, d.M - 1);
+      mean[a] = 0.f;
+      rstd[a] = 1.f;
+      if constexpr (LN) {
+        mean[a] = d.a_mean[row];
+        rstd[a] = d.a_rstd[row];
+      }
+    }
+    // this wave stores whole 16-byte vectors for every row of its 64x64 sub-tile: exactly
+    // 2 (bf16) or 4 (fp32) stores per 16-row block, no scalar tail
+    const bool full = vec && m0 + wr * 64 + 64 <= d.M && n0 + wc * 64 + 64 <= d.N;
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int a = 0; a < RM; ++a)
+#pragma unroll
+      for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMAs of k-tile kt (and the previous tile's epilogue stores) done; every
+      // wave's reads of the other buffer retired -> it may be refilled
+      // (at kt = 0 the previous epilogue's >= 8 stores are younger than this k-tile's DMAs: a
+      // counted wait leaves them in flight instead of stalling on their write acknowledgements)
+      if (kt == 0 && prev_full) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < nk) stage(cur, buf ^ 1, kt + 1);
+      else if (next >= 0) stage(nxt, buf ^ 1, 0);         // next tile's first k-tile
+      const unsigned char* sa = smem + buf * SK_STAGE;
+      const unsigned char* sb = sa + SK_BM * SK_ROW;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int lc = s * 4 + fg;
+        uint4 fa[RM], fb[RN];
+#pragma unroll
+        for (int a = 0; a < RM; ++a) {
+          const int r = wr * (SK_BM / 2) + a * 16 + fr;
+          fa[a] = *reinterpret_cast<const uint4*>(sa + r * SK_ROW + ((lc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int b = 0; b < RN; ++b) {
+          const int r = wc * (SK_BN / 2) + b * 16 + fr;
+          fb[b] = *reinterpret_cast<const uint4*>(sb + r * SK_ROW + ((lc ^ (r & 7)) << 4));
+        }
+#pragma unroll
+        for (int a = 0; a < RM; ++a)
+#pragma unroll
+          for (int b = 0; b < RN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[b]),
+                                                                __builtin_bit_cast(bf16x8, fa[a]), acc[a][b], 0, 0, 0);
+      }
+      buf ^= 1;
+    }
+
+    // ---- register epilogue: lane (fr, fg) owns columns col0 .. col0+15 of rows m0 + wr*64 + a*16 + fr
+#pragma unroll
+    for (int a = 0; a < RM; ++a) {
+      if (DIAG == 1) continue;
+      const int row = m0 + wr * 64 + a * 16 + fr;           // this lane's row (may be >= M: no store)
+      const int rowc = min(row, d.M - 1);
+      float v[16];
+#pragma unroll
+      for (int b = 0; b < RN; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = b * 4 + j;
+          float x = acc[a][b][j];
+          if constexpr (LN) x = rstd[a] * (x - mean[a] * cs[c]);
+          x = x * sc[c] + bi[c];
+          v[c] = (gelu_fast && d.act == HV_ACT_GELU) ? hv_gelu_fast(x) : hv_act(x, d.act);
+        }
+      const long rrow = d.r_mod > 0 ? rowc % d.r_mod : rowc;
+      if (vec && col0 + 16 <= d.N) {                        // same for the lane pair (fr, fr ^ 8)
+        if (d.residual) {
+          if (r_bf) {
+            const unsigned short* rp = (const unsigned short*)d.residual + rrow * d.ldr + col0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint4 r4 = *reinterpret_cast<const uint4*>(rp + h * 8);
+              const uint32_t w4[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v[h * 8 + 2 * e] += __uint_as_float(w4[e] << 16);
+                v[h * 8 + 2 * e + 1] += __uint_as_float(w4[e] & 0xffff0000u);
+              }
+            }
+          } else {
+            const float* rp = (const float*)d.residual + rrow * d.ldr + col0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 r4 = *reinterpret_cast<const float4*>(rp + q * 4);
+              v[q * 4] += r4.x; v[q * 4 + 1] += r4.y; v[q * 4 + 2] += r4.z; v[q * 4 + 3] += r4.w;
+            }
+          }
+        }
+        if (c_bf) {
+          // whole 128-byte rows per store instruction: lanes fr and fr ^ 8 (DPP row_ror:8) swap one
+          // 16-byte half, so instruction 1 writes rows 0..7 of the block, instruction 2 rows 8..15,
+          // each row's 64 columns by 8 lanes (a lane's 16 columns alone make 64-byte pieces, which
+          // measured 1.6 TB/s against 6.2 for whole lines)
+          uint32_t p[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) p[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+          const bool lo = fr < 8;
+          uint32_t rv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            rv[e] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(lo ? p[4 + e] : p[e]), 0x128, 0xF, 0xF, false);
+          const uint4 s1 = lo ? make_uint4(p[0], p[1], p[2], p[3]) : make_uint4(rv[0], rv[1], rv[2], rv[3]);
+          const uint4 s2 = lo ? make_uint4(rv[0], rv[1], rv[2], rv[3]) : make_uint4(p[4], p[5], p[6], p[7]);
+          const int r1 = lo ? row : row - 8, r2 = lo ? row + 8 : row;
+          const int cc = col0 + (lo ? 0 : 8);
+          unsigned short* cb = (unsigned short*)d.C;
+          if (r1 < d.M) *reinterpret_cast<uint4*>(cb + (long)r1 * d.ldc + cc) = s1;
+          if (r2 < d.M) *reinterpret_cast<uint4*>(cb + (long)r2 * d.ldc + cc) = s2;
+        } else if (row < d.M) {
+          float* cp = (float*)d.C + (long)row * d.ldc + col0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<float4*>(cp + q * 4) = make_float4(v[q * 4], v[q * 4 + 1], v[q * 4 + 2], v[q * 4 + 3]);
+        }
+      } else if (row < d.M) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int col = col0 + c;
+          if (col >= d.N) break;
+          float x = v[c];
+          if (d.residual)
+            x += r_bf ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col])
+                      : ((const float*)d.residual)[rrow * d.ldr + col];
+          const long o = (long)row * d.ldc + col;
+          if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
+          else ((float*)d.C)[o] = x;
+        }
+      }
+    }
+    if (next < 0) break;
+    prev_full = full;
+    tile = next;
+    cur = nxt;
+  }
+}
+
+std::atomic<int> g_sk_on{1};     // persistent small-K kernel (A/B knob hv_gemm_set_smallk)
+std::atomic<int> g_cus{0};
+
+}  // namespace
+
+extern "C" void hv_gemm_set_smallk(int on) { g_sk_on = on; }
+
+// Returns HV_EUNSUPPORTED when the shape/mode is not this kernel's (the caller falls back).
+// force (hv_gemm_set_force_tile(6), tests): any supported shape, even below one round of tiles.
+int hv_gemm_smallk(const hv_gemm_desc& d0, hipStream_t s, bool force) {
+  if (!force && !g_sk_on.load(std::memory_order_relaxed)) return HV_EUNSUPPORTED;
+  hv_gemm_desc d = d0;
+  // a 1x1 stride-1 unpadded convolution is the plain GEMM over the NHWC pixel rows
+  if (d.conv_k == 1 && d.conv_stride == 1 && d.conv_pad == 0 && !d.conv_transposed) {
+    d.conv_k = 0;
+    d.lda = d.conv_c;
+  }
+  if (d.dtype != HV_BF16 || d.conv_k > 0 || d.conv_transposed || d.A2 || d.epi_mode) return HV_EUNSUPPORTED;
+  if (d.K % 64 || d.K > 512 || d.lda % 8 || d.ldb % 8) return HV_EUNSUPPORTED;
+  if (d.a_mean && !d.b_colsum) return HV_EUNSUPPORTED;
+  if (!force && d.N < 256) return HV_EUNSUPPORTED;        // narrow outputs: the ring kernel's tiles fill better
+  const long ntiles = (long)hv_cdiv(d.M, SK_BM) * hv_cdiv(d.N, SK_BN);
+  int cus = g_cus.load(std::memory_order_relaxed);
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0)
+      cus = 256;
+    g_cus = cus;
+  }
+  if (!force && ntiles < 2L * cus) return HV_EUNSUPPORTED;   // under one persistent round: nothing to overlap
+  const int grid = (int)(ntiles < 2L * cus ? ntiles : 2L * cus);
+  hv_diag_count(HV_KF_GEMM_SMALLK);
+  const int mode = g_sk_on.load(std::memory_order_relaxed);
+  if (mode == 2) gemm_sk_kernel<false, 1><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  else if (mode == 3) gemm_sk_kernel<false, 2><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  else if (d.a_mean) gemm_sk_kernel<true><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  else gemm_sk_kernel<false><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}

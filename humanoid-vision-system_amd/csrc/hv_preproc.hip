@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(256) k_preprocess_pil(const uint8_t* __restric
   const int ymin = vb[2 * oy], yn = vb[2 * oy + 1];
   const int* kx = hk + (long)ox * ksh;
   const int* ky = vk + (long)oy * ksv;
+  HV_DCHECK(xmin >= 0 && xn <= ksh && xmin + xn <= w && ymin >= 0 && yn <= ksv && ymin + yn <= h);
   const uint8_t* base = img + (long)b * h * w * 3;
   int acc[3] = {1 << (kPilPrec - 1), 1 << (kPilPrec - 1), 1 << (kPilPrec - 1)};
   for (int y = 0; y < yn; ++y) {

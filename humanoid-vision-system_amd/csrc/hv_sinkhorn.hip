@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(256) sk_rows(const hv_sinkhorn_entry* __restri
   const int nrb = (e.n + RB - 1) / RB;
   const int lb = blockIdx.x - e.row_block_start;  // local row block
   const int bidx = lb / nrb, rb = lb % nrb;
+  HV_DCHECK(lb >= 0 && bidx < e.batch && e.m <= 64 * MAXQ);
   const int m = e.m, n = e.n;
   const int nq = (m + 63) >> 6;
   const float* K = e.out + (long)bidx * n * m;
@@ -225,6 +226,7 @@ __global__ void __launch_bounds__(256) sk_cols(const hv_sinkhorn_entry* __restri
   const long bm = (long)e.batch * e.m;
   if (live) {
     c = g - e.col_start;                     // within batch*m
+    HV_DCHECK(c >= 0 && c < e.batch * e.m);
     if (wv == 0) bprev = carve(e).b[(long)t * bm + c];   // issued before the partial sums
     const int bidx = c / e.m, j = c % e.m;
     const int nrb = (e.n + RB - 1) / RB;

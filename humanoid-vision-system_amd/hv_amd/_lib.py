@@ -120,6 +120,7 @@ _SIGS = {
     "hv_gemm_set_staged_epilogue": ([i32], None),
     "hv_gemm_set_deep_ring": ([i32], None),
     "hv_gemm_set_conv_ktail": ([i32], None),
+    "hv_gemm_set_smallk": ([i32], None),
     "hv_gemm_set_force_tile": ([i32], None),
     "hv_gemm_set_staged_train": ([i32], None),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),

@@ -753,7 +753,7 @@ def preprocess(frames: Tensor, height: int, width: int, *, bgr: bool = True, dty
 
 # ---------------------------------------------------------------------------- diagnostics
 KERNEL_FAMILIES = ("gemm_pp256", "glds_128x128", "glds_64x128", "glds_128x64", "glds_64x64", "gemm_regstage",
-                   "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group", "attn_general")
+                   "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group", "attn_general", "gemm_smallk")
 
 
 def launch_counts(reset: bool = False) -> dict:

@@ -33,6 +33,8 @@ void hv_gemm_set_deep_ring(int on);
 void hv_gemm_set_force_tile(int code);
 /* convolutions with K % 64 != 0 (channels % 8 == 0) on the LDS-DMA kernel: 0 off (default), 1 on */
 void hv_gemm_set_conv_ktail(int on);
+/* persistent small-K (K <= 512) GEMM kernel: 1 on (default), 0 off */
+void hv_gemm_set_smallk(int on);
 /* fused mHC: 1 also dispatches (256, 512) to the fused kernel (off by default: slower) */
 void hv_mhc_fused_enable_wide(int on);
 /* fused mHC workgroup shape: 0 default (4-wave groups), 1 three groups per CU, 2 one 8-wave group */
@@ -51,6 +53,7 @@ enum hv_kernel_family {
   HV_KF_ATTN_SCALAR = 8,     /* k_attention (fp32 / other head dims) */
   HV_KF_SINKHORN_GROUP = 9,  /* one grouped Sinkhorn forward (all its passes) */
   HV_KF_ATTN_GENERAL = 10,   /* hv_attention_general (cross / masked / weights / CLS-row queries) */
+  HV_KF_GEMM_SMALLK = 11,    /* gemm_sk_kernel (persistent small-K, register epilogue) */
   HV_KF_COUNT = 16
 };
 /* copies the HV_KF_COUNT launch counters into out[] */

@@ -182,6 +182,75 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
     assert rel_err(fast, ref) < 1e-4
 
 
+SMALLK_CASES = [  # (kind, M, N, K): 1-8 k-tiles, ragged M / N (scalar store tail), every epilogue form
+    ("plain", 4096, 512, 64), ("plain", 1000, 777, 128), ("ln_gelu", 1500, 1024, 256), ("gelu_res", 2048, 768, 512),
+    ("res32_mod", 1200, 640, 256), ("scale_f32", 700, 384, 192), ("conv1x1", 2 * 40 * 40, 256, 128),
+    ("ln_gelu", 8192, 1024, 256)]
+
+
+@pytest.mark.parametrize("kind,M,N,K", SMALLK_CASES)
+def test_gemm_smallk_equals_ring(gpu_device, kind, M, N, K):
+    """The persistent small-K kernel (hv_gemm_sk.hip: N-permuted B rows, register epilogue with
+    16-byte stores, next tile's first k-tile prefetched across the epilogue) against the 128x128
+    LDS-DMA ring kernel: same per-element k order and epilogue arithmetic -> bit-identical; plus
+    a CPU fp32 check.  The 8192x1024x256 case (512 tiles) must take it without forcing."""
+    ops = _ops()
+    from hv_amd import _lib
+    g = torch.Generator().manual_seed(M * 3 + N + K)
+    bf = torch.bfloat16
+    a = torch.randn(M, K, generator=g).to(bf).to(gpu_device)
+    b = (torch.randn(N, K, generator=g) / K ** 0.5).to(bf).to(gpu_device)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    af, bfl = a.float().cpu(), b.float().cpu()
+    if kind == "plain":
+        run = lambda: ops.gemm(a, b, bias=bias, out_dtype=torch.float32)  # noqa: E731
+        ref = af @ bfl.T + bias.cpu()
+    elif kind == "ln_gelu":
+        mean = af.mean(1)
+        rstd = 1.0 / torch.sqrt(af.var(1, unbiased=False) + 1e-5)
+        cs = bfl.sum(1)
+        run = lambda: ops.gemm(a, b, bias=bias, act="gelu", a_mean=mean.to(gpu_device),  # noqa: E731
+                               a_rstd=rstd.to(gpu_device), b_colsum=cs.to(gpu_device))
+        ref = F.gelu(((af - mean[:, None]) * rstd[:, None]) @ bfl.T + bias.cpu())
+    elif kind == "gelu_res":
+        res = torch.randn(M, N, generator=g).to(bf).to(gpu_device)
+        run = lambda: ops.gemm(a, b, bias=bias, act="gelu", residual=res)  # noqa: E731
+        ref = F.gelu(af @ bfl.T + bias.cpu()) + res.float().cpu()
+    elif kind == "res32_mod":
+        res = torch.randn(400, N, generator=g).to(gpu_device)
+        run = lambda: ops.gemm(a, b, act="silu", residual=res, residual_mod=400, out_dtype=torch.float32)  # noqa: E731
+        ref = F.silu(af @ bfl.T) + res.cpu().repeat(3, 1)
+    elif kind == "scale_f32":
+        sc = torch.rand(N, generator=g).to(gpu_device) + 0.5
+        run = lambda: ops.gemm(a, b, bias=bias, scale=sc, alpha=0.75, act="relu", out_dtype=torch.float32)  # noqa: E731
+        ref = F.relu((af @ bfl.T) * 0.75 * sc.cpu() + bias.cpu())
+    else:  # 1x1 convolution over NHWC pixels
+        hw = int(round((M // 2) ** 0.5))
+        x = a.view(2, hw, hw, K)
+        run = lambda: ops.conv2d(x, b, 1, 1, 0, out_dtype=torch.float32)  # noqa: E731
+        ref = af @ bfl.T
+    lib = _lib.lib()
+    try:
+        lib.hv_gemm_set_force_tile(6)
+        ops.launch_counts(reset=True)
+        fast = run()
+        assert ops.launch_counts()["gemm_smallk"] == 1
+        lib.hv_gemm_set_force_tile(1)
+        ring = run()
+    finally:
+        lib.hv_gemm_set_force_tile(0)
+    if M * N >= 8192 * 1024:
+        ops.launch_counts(reset=True)
+        auto = run()
+        assert ops.launch_counts()["gemm_smallk"] == 1
+        assert torch.equal(auto, fast)
+    torch.cuda.synchronize()
+    assert torch.equal(fast.reshape(ring.shape), ring), \
+        f"max |diff| {(fast.float().reshape(ring.shape) - ring.float()).abs().max().item()}"
+    tol = 2e-2 if fast.dtype == torch.bfloat16 else 1e-4
+    assert rel_err(fast.reshape(ref.shape), ref) < tol
+
+
 PP256_CASES = [  # (kind, M, N, K): ragged M/N, 1-3 K-tiles (prologue/tail vmcnt branches), long K
     ("plain", 4096, 512, 1024), ("plain", 1000, 520, 640), ("plain", 300, 260, 64), ("plain", 513, 300, 128),
     ("plain", 700, 777, 192), ("gelu_res", 2048, 768, 2048), ("ln", 1500, 1024, 256), ("concat", 1024, 512, 768),

@@ -9,6 +9,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
 from hv_amd import HybridVisionSystem  # noqa: E402
 from hv_amd import manifold as MF  # noqa: E402
+from hv_amd import detect as DT  # noqa: E402
 from hv_amd import ops as OPS  # noqa: E402
 from hv_amd import vit as VT  # noqa: E402
 
@@ -18,6 +19,7 @@ SWITCHES = {
     "no_cls_only": lambda: setattr(VT, "CLS_ONLY_LAST_BLOCK", False),
     "no_group_qkv": lambda: setattr(MF, "GROUP_QKV", False),
     "sk_split": lambda: setattr(OPS, "SINKHORN_SPLIT", True),
+    "prep_overlap": lambda: setattr(DT, "_PREP_OVERLAP", True),
 }
 
 
@@ -26,6 +28,7 @@ def reset():
     MF.GROUP_QKV = True
     VT.CLS_ONLY_LAST_BLOCK = True
     OPS.SINKHORN_SPLIT = False
+    DT._PREP_OVERLAP = False
 
 
 def main():
