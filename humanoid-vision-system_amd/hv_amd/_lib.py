@@ -82,6 +82,10 @@ class MhcFusedArgs(C.Structure):
                 ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp)]
 
 
+class SymeigEntry(C.Structure):
+    _fields_ = [("h", vp), ("eig", vp), ("work", vp), ("n", i32), ("row_start", i32)]
+
+
 class MhcPrepEntry(C.Structure):
     _fields_ = [("h_pre_raw", vp), ("h_post_raw", vp), ("h_res", vp), ("gamma_pre", vp), ("beta_pre", vp),
                 ("w1", vp), ("b1", vp), ("a1", vp), ("c1", vp), ("wct", vp), ("scratch", vp), ("cs", vp),
@@ -109,6 +113,10 @@ _SIGS = {
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),
     "hv_struct_sizes": ([vp], None),
+    "hv_symeig_work_doubles": ([i32], C.c_size_t),
+    "hv_symeig_group": ([vp, vp, i32, vp], i32),
+    "hv_stability_work_floats": ([i32], C.c_size_t),
+    "hv_stability_stats": ([i32, vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp], i32),
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_forward": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "hv_sinkhorn_group_forward_part": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),

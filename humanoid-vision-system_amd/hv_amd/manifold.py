@@ -26,6 +26,28 @@ from . import ops
 from .runtime import RunCtx, current, require_cuda, resolve_dtype, use_ctx
 
 
+# ================================================================== stability monitor queue
+# (H_res, eigenvalues buffer) of every _monitor_stability call since the last flush, keyed by the
+# buffer (a site monitored twice keeps its latest matrix): solved together by one grouped
+# hv_symeig_group -- 2*(max n - 2) + 3 launches for all 76 sites instead of per site.
+_EIG_QUEUE: Dict[int, Any] = {}
+
+
+def queue_eigvals(h: torch.Tensor, out: torch.Tensor) -> None:
+    _EIG_QUEUE[id(out)] = (h, out)
+    if len(_EIG_QUEUE) >= 512:
+        flush_stability()
+
+
+def flush_stability() -> None:
+    """Solve every queued eigenvalue problem (manifold_layers.py:288-290) in one launch group."""
+    if not _EIG_QUEUE:
+        return
+    items = list(_EIG_QUEUE.values())
+    _EIG_QUEUE.clear()
+    ops.symeig_group([h for h, _ in items], [o for _, o in items])
+
+
 # ================================================================== Sinkhorn
 class SinkhornKnoppProjection(nn.Module):
     """Reference manifold_layers.py:10-101 (shim S1: 2-D input = batch of one)."""
@@ -239,26 +261,24 @@ class ManifoldHyperConnection(nn.Module):
 
     @torch.no_grad()
     def monitor_stability(self, H_res: torch.Tensor, x_in: torch.Tensor, x_out: torch.Tensor) -> None:
-        """_monitor_stability (manifold_layers.py:282-316), device-side: eigenvalues of the
-        symmetric part of H_res, the signal-growth ratio into the circular history, row/column
-        sum errors -- kept as device tensors (no .item() in the training forward; the host reads
-        happen in get_stability_metrics)."""
-        h = H_res.detach().float()
-        try:
-            self.eigenvalues.copy_(torch.linalg.eigvalsh((h + h.T) / 2))
-        except RuntimeError:
-            pass
-        ratio = x_out.detach().float().norm(dim=-1).mean() / (x_in.detach().float().norm(dim=-1).mean() + 1e-8)
-        self.signal_ratio_history[self.signal_ratio_idx % 1000] = ratio
+        """_monitor_stability (manifold_layers.py:282-316) on the device, no .item() in the
+        training forward: the signal-growth ratio (into the circular history) and the row/column
+        sum errors come from hv_stability_stats now; the eigenvalues of (H_res + H_res^T)/2 are
+        queued and solved for every queued site at once (hv_symeig_group) at the end of the
+        training forward or on the first metrics read (flush_stability)."""
+        h = H_res.detach().float().contiguous()
+        queue_eigvals(h, self.eigenvalues)
+        slot = self.signal_ratio_idx % 1000
+        st = ops.stability_stats(x_in, x_out, h, self.signal_ratio_history, slot)
         self.signal_ratio_idx += 1
-        self._monitor_dev = {"signal_ratio": ratio, "row_sum_error": (h.sum(dim=1).mean() - 1.0).abs(),
-                             "col_sum_error": (h.sum(dim=0).mean() - 1.0).abs()}
+        self._monitor_dev = {"signal_ratio": st[0], "row_sum_error": st[1], "col_sum_error": st[2]}
 
     @property
     def monitoring_metrics(self) -> Dict[str, float]:
         d = getattr(self, "_monitor_dev", None)
         if d is None:
             raise AttributeError("monitoring_metrics")
+        flush_stability()
         ev = self.eigenvalues
         out = {"max_eigenvalue": ev.max().item(), "min_eigenvalue": ev.min().item()}
         out.update({k: float(v) for k, v in d.items()})
@@ -266,6 +286,7 @@ class ManifoldHyperConnection(nn.Module):
 
     def get_stability_metrics(self) -> Dict[str, Any]:
         """manifold_layers.py:318-341 (host reads happen here, never in forward)."""
+        flush_stability()
         ev = self.eigenvalues
         metrics = {"max_eigenvalue": ev.max().item(), "min_eigenvalue": ev.min().item(),
                    "eigenvalue_range": (ev.max() - ev.min()).item(),

@@ -751,6 +751,61 @@ def preprocess(frames: Tensor, height: int, width: int, *, bgr: bool = True, dty
     return out.permute(0, 3, 1, 2) if nhwc else out
 
 
+# ---------------------------------------------------------------------------- stability monitor
+def symeig_group(mats, outs=None) -> list:
+    """Ascending eigenvalues of (H + H^T)/2 for every square fp32 matrix in `mats`, all in one
+    grouped launch sequence (hv_symeig_group) -- the eigvalsh of _monitor_stability
+    (manifold_layers.py:288-290).  `outs` (fp32 [n] each) are written in place when given."""
+    mats = [_contig(m.detach(), "H") for m in mats]
+    if not mats:
+        return []
+    _cuda(*mats)
+    for m in mats:
+        if m.dim() != 2 or m.shape[0] != m.shape[1] or m.dtype != torch.float32:
+            raise ValueError("symeig_group: square fp32 matrices")
+    dev = mats[0].device
+    if outs is None:
+        outs = [torch.empty(m.shape[0], device=dev, dtype=torch.float32) for m in mats]
+    lib = L.lib()
+    order = sorted(range(len(mats)), key=lambda i: -mats[i].shape[0])
+    entries = (L.SymeigEntry * len(mats))()
+    ns = (C.c_int * len(mats))()
+    works, rs = [], 0
+    for k, i in enumerate(order):
+        n = mats[i].shape[0]
+        if outs[i].numel() != n or outs[i].dtype != torch.float32 or not outs[i].is_contiguous():
+            raise ValueError("symeig_group: outputs must be contiguous fp32 [n]")
+        w = torch.empty(lib.hv_symeig_work_doubles(n), device=dev, dtype=torch.float64)
+        works.append(w)
+        e = entries[k]
+        e.h, e.eig, e.work, e.n, e.row_start = mats[i].data_ptr(), outs[i].data_ptr(), w.data_ptr(), n, rs
+        ns[k] = n
+        rs += n
+    table = upload_table(entries, dev)
+    check(lib.hv_symeig_group(table.data_ptr(), ns, len(mats), stream_ptr()), "hv_symeig_group")
+    return outs
+
+
+def stability_stats(x_in: Tensor, x_out: Tensor, h: Tensor, history: Optional[Tensor] = None,
+                    slot: int = 0) -> Tensor:
+    """[signal_ratio, row_sum_error, col_sum_error] (manifold_layers.py:296-315) as a device
+    fp32 [3]; history[slot] = signal_ratio when `history` is given (:300-303)."""
+    D = x_in.shape[-1]
+    xi = _contig(x_in.detach(), "x_in").reshape(-1, D)
+    xo = _contig(x_out.detach(), "x_out").reshape(-1, D)
+    if xo.dtype != xi.dtype:
+        xo = xo.to(xi.dtype)
+    hh = _contig(h.detach().float(), "H")
+    _cuda(xi, xo, hh)
+    lib = L.lib()
+    work = torch.empty(lib.hv_stability_work_floats(xi.shape[0]), device=xi.device, dtype=torch.float32)
+    out = torch.empty(3, device=xi.device, dtype=torch.float32)
+    check(lib.hv_stability_stats(dtype_code(xi.dtype), xi.data_ptr(), xo.data_ptr(), xi.shape[0], D,
+                                 hh.data_ptr(), hh.shape[0], work.data_ptr(), ptr(history), slot,
+                                 out.data_ptr(), stream_ptr()), "hv_stability_stats")
+    return out
+
+
 # ---------------------------------------------------------------------------- diagnostics
 KERNEL_FAMILIES = ("gemm_pp256", "glds_128x128", "glds_64x128", "glds_128x64", "glds_64x64", "gemm_regstage",
                    "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group", "attn_general", "gemm_smallk")

@@ -19,6 +19,7 @@ from . import ops
 from . import ops_train as OT
 from . import train_fn as TF
 from .layers import to_nchw_view, to_nhwc
+from .manifold import flush_stability
 from .runtime import PRECISIONS
 
 
@@ -304,6 +305,7 @@ def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection"
     bbv["raw_features"] = {k: to_nchw_view(v) for k, v in bb["raw_features"].items()}
     out["backbone_features"] = bbv
     out["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
+    flush_stability()              # this forward's monitored sites: one grouped eigensolve
     return out
 
 

@@ -550,6 +550,30 @@ int hv_adamw(const hv_param_entry* dev_table, int count, int total_blocks, const
              float lr, float beta1, float beta2, float eps, float weight_decay, int step,
              hv_stream_t stream);
 
+/* ------------------------------------------------------------------------------------
+ * Stability monitor (ManifoldHyperConnection._monitor_stability, reference
+ * src/models/manifold_layers.py:282-316), device-side and grouped over all mHC sites.
+ * hv_symeig_group: eig = ascending eigenvalues of (h + h^T)/2 for every entry (the
+ * torch.linalg.eigvalsh call, :288-290): fp64 Householder tridiagonalisation + Sturm
+ * bisection.  Entries sorted by n descending (host_n[] = their n, same order, n <= 2048);
+ * row_start = exclusive prefix of n over the table.  2*(max n - 2) + 3 launches, no host sync.
+ * ------------------------------------------------------------------------------------ */
+typedef struct hv_symeig_entry {
+  const float* h;      /* [n, n] fp32 row-major */
+  float* eig;          /* [n] */
+  double* work;        /* hv_symeig_work_doubles(n) */
+  int n;
+  int row_start;
+} hv_symeig_entry;
+size_t hv_symeig_work_doubles(int n);
+int hv_symeig_group(const hv_symeig_entry* dev_table, const int* host_n, int count, hv_stream_t stream);
+/* signal ratio mean_r|x_out[r]| / (mean_r|x_in[r]| + 1e-8) (:296-298) and the row/column-sum
+   errors |sum(h)/n - 1| (:306-315) -> out3[3]; history[slot] = ratio when history != NULL
+   (:300-303).  x_in/x_out: [rows, D] of `dtype`; h: [n, n] fp32; work: hv_stability_work_floats. */
+size_t hv_stability_work_floats(int rows);
+int hv_stability_stats(int dtype, const void* x_in, const void* x_out, int rows, int D, const float* h, int n,
+                       float* work, float* history, int slot, float* out3, hv_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

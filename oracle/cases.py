@@ -13,6 +13,8 @@ SK_CASES = [(8, 5), (8, 20), (32, 20), (64, 5), (64, 20), (128, 20), (256, 20), 
             (1024, 20), (1792, 20)]
 MHC_CASES = [(32, 4), (64, 4), (128, 4), (256, 4), (512, 4), (256, 2), (512, 2), (1024, 2),
              (1792, 2)]
+STAB_CASES = [(1, "wc"), (2, "wc"), (3, "wc"), (8, "wc"), (32, "wc"), (64, "init"), (128, "wc"),
+              (256, "wc"), (256, "init"), (512, "wc"), (1024, "wc"), (1792, "wc")]   # (D, family), 20 iters
 MODEL_CASES = [  # (tag, tiny, family, size, batch, subsample rows of scale_0)
     ("tiny_wc_224_b2", True, "wc", 224, 2, 1),
     ("tiny_init_224_b2", True, "init", 224, 2, 1),
@@ -105,3 +107,10 @@ def camera_frames(seed: int, n: int, h: int, w: int):
             tex = 40 * ((np.floor(xx * w / 7) + np.floor(yy * h / 5)) % 2)
             out[i, :, :, c] = np.clip(base + tex + rng.normal(0, 20, (h, w)), 0, 255).astype(np.uint8)
     return out
+
+
+def stab_inputs(D: int, family: str):
+    """Stability-monitor case: H = Sinkhorn(raw, 20) of sinkhorn_raw(D, 20, family), computed by
+    the caller; x_in / x_out [64, D] token rows."""
+    g = gen_seed(D, 20, 31 if family == "wc" else 32)
+    return torch.randn(64, D, generator=g), 1.7 * torch.randn(64, D, generator=g)

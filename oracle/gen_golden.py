@@ -28,8 +28,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, REF)
 
 from oracle import weights as W  # noqa: E402
-from oracle.cases import (MHC_CASES, MODEL_CASES, SK_CASES, gen_seed,  # noqa: E402
-                          mhc_input, sinkhorn_raw)
+from oracle.cases import (MHC_CASES, MODEL_CASES, SK_CASES, STAB_CASES, gen_seed,  # noqa: E402
+                          mhc_input, sinkhorn_raw, stab_inputs)
 
 _TINY = {"on": False}
 
@@ -188,6 +188,29 @@ def gen_sinkhorn(ml):
     mat = torch.randn(2, 5, 7, generator=g)
     sk = ml.SinkhornKnoppProjection(num_iterations=10)
     save("sk_batched_2x5x7", raw=mat, M=sk(mat), history=sk.convergence_history.clone())
+
+
+# ------------------------------------------------------------------ G1b stability monitor
+def gen_stability(ml):
+    """ManifoldHyperConnection._monitor_stability (manifold_layers.py:282-316) of the reference,
+    called on the reference's own Sinkhorn output: eigenvalues buffer (fp32 eigvalsh), the
+    monitoring_metrics dict and the circular-history entry."""
+    print("G1b stability")
+    for D, fam in STAB_CASES:
+        raw = sinkhorn_raw(D, 20, fam)
+        with torch.no_grad():
+            H = ml.SinkhornKnoppProjection(num_iterations=20)(raw)
+            x_in, x_out = stab_inputs(D, fam)
+            m = ml.ManifoldHyperConnection(D, expansion_rate=2)
+            m._monitor_stability(H, x_in, x_out)
+        mm = m.monitoring_metrics
+        rec = {"D": D, "eigenvalues": m.eigenvalues.clone(), "history0": m.signal_ratio_history[0].clone(),
+               "signal_ratio": mm["signal_ratio"], "row_sum_error": mm["row_sum_error"],
+               "col_sum_error": mm["col_sum_error"], "max_eigenvalue": mm["max_eigenvalue"],
+               "min_eigenvalue": mm["min_eigenvalue"]}
+        if D <= 256:
+            rec["H"] = H
+        save(f"stab_{fam}_D{D}", **rec)
 
 
 # ------------------------------------------------------------------ G2 mHC
@@ -405,7 +428,7 @@ def gen_preproc():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="sinkhorn,mhc,blocks,model,layout,train,nms,preproc")
+    ap.add_argument("--only", default="sinkhorn,stability,mhc,blocks,model,layout,train,nms,preproc")
     ap.add_argument("--models", default="")
     ap.add_argument("--trains", default="")
     a = ap.parse_args()
@@ -414,6 +437,8 @@ def main():
     parts = a.only.split(",")
     if "sinkhorn" in parts:
         gen_sinkhorn(ml)
+    if "stability" in parts:
+        gen_stability(ml)
     if "mhc" in parts:
         gen_mhc(ml)
     if "blocks" in parts:

@@ -70,6 +70,21 @@ def sinkhorn(raw: Tensor, iters: int, eps: float = 1e-8, tau: float = 1.0,
 
 
 # ----------------------------------------------------------------------------------------
+# a4: stability monitor (manifold_layers.py:282-316), fp64
+# ----------------------------------------------------------------------------------------
+def monitor_stability(H: Tensor, x_in: Tensor, x_out: Tensor) -> Dict[str, Tensor]:
+    """eigenvalues of (H + H^T)/2 ascending (:288-290, eigvalsh), signal ratio
+    mean|x_out| / (mean|x_in| + 1e-8) over the last dim (:296-298), |mean row/col sum - 1|
+    (:306-315).  Computed in fp64 from the given fp32 tensors."""
+    h = H.double()
+    ev = torch.linalg.eigvalsh((h + h.T) / 2)
+    ratio = x_out.double().norm(dim=-1).mean() / (x_in.double().norm(dim=-1).mean() + 1e-8)
+    return {"eigenvalues": ev, "signal_ratio": ratio,
+            "row_sum_error": (h.sum(dim=1).mean() - 1.0).abs(),
+            "col_sum_error": (h.sum(dim=0).mean() - 1.0).abs()}
+
+
+# ----------------------------------------------------------------------------------------
 # a2/a3: mHC layer (manifold_layers.py:205-280), eval mode (dropout = identity)
 # ----------------------------------------------------------------------------------------
 def mhc_coefficients(sd: Dict[str, Tensor], p: str, sk_iters: int):

@@ -246,3 +246,19 @@ def test_preprocess_oracle_matches_pillow(case):
     bgr = cases.camera_frames(int(g["seed"]), n, h, w)
     rgb, _ = P.preprocess_frames(bgr, oh, ow)
     np.testing.assert_array_equal(rgb, g["resized_rgb"])
+
+
+@pytest.mark.parametrize("D,fam", cases.STAB_CASES)
+def test_stability_monitor_oracle_matches_reference(D, fam):
+    """a4: the oracle's _monitor_stability restatement (fp64) vs the reference's fp32 run
+    (tests/golden/stab_*: eigvalsh eigenvalues, signal ratio, sum errors)."""
+    g = golden(f"stab_{fam}_D{D}")
+    H = torch.from_numpy(g["H"]) if "H" in g.files else O.sinkhorn(cases.sinkhorn_raw(D, 20, fam), 20)
+    x_in, x_out = cases.stab_inputs(D, fam)
+    r = O.monitor_stability(H, x_in, x_out)
+    # the reference's eigvalsh runs in fp32 (LAPACK ssyevd): |err| ~ n * eps32 * ||H||
+    np.testing.assert_allclose(r["eigenvalues"].numpy(), g["eigenvalues"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(float(r["signal_ratio"]), float(g["signal_ratio"]), rtol=1e-5)
+    np.testing.assert_allclose(float(g["history0"]), float(g["signal_ratio"]), rtol=1e-6)
+    for k in ("row_sum_error", "col_sum_error"):
+        np.testing.assert_allclose(float(r[k]), float(g[k]), rtol=0, atol=2e-6)
