@@ -322,6 +322,371 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
   return HV_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-hidden variant (D = 128, HD = 512).  The kernel above gives every wave 16 tokens end to
+// end, so each W2 fragment read from LDS (1 KB) feeds ONE MFMA: at D = 128 the loop is LDS- and
+// latency-bound (~400 TF/s).  Here a 4-wave workgroup owns TOK = 64 tokens and splits the HIDDEN
+// dimension: wave w accumulates h2 for hidden units [w*HD/4, (w+1)*HD/4) of all 64 tokens, so
+// every W2 fragment feeds TT = 4 MFMAs and every h1 fragment HQT = 8 (register blocking 8 x 4).
+//   GEMM1  wave w computes the h1 chunk (32 hidden, GELU) for ITS 16 tokens and writes it, already
+//          in the GEMM2 B-fragment layout, to an LDS slot (double-buffered by chunk parity)
+//   GEMM2  wave w: acc2[8 hidden tiles][4 token tiles] += W2 chunk rows (its quarter) . h1 chunk
+//   GEMM3  split-K over the waves: wave w contracts its h2 quarter (+ one 32-wide x chunk) into a
+//          partial y for all 64 tokens; the 4 partials meet in LDS (fixed order -> deterministic)
+//          in two column halves; LN_post + residual per token from registers.
+// Weight chunks (A1^T rows + W2 columns) stream through a 3-stage DMA ring, one barrier per chunk:
+// chunk c+2 is DMA'd while GEMM1(c+1) and GEMM2(c) run.
+template <int D, int HD, int NG>
+struct Cfg2 {
+  static constexpr int NW = 4 * NG, NT = 64 * NW;
+  static constexpr int TOKG = 32768 / HD, TOK = NG * TOKG, TT = TOKG / 16;   // tokens per group / WG
+  static constexpr int TW1 = TOK / NW, TBW = TW1 / 16;                         // GEMM1 tokens per wave
+  static constexpr int HQ = HD / 4, HQT = HQ / 16, KC = 32, NCH = 2 * HD / KC, KS1 = D / 32, CPA = D / 8;
+  static constexpr int A1B = KC * D * 2, W2B = HD * 64, STAGE = A1B + W2B, H1B = (TOK / 16) * 1024;
+  static constexpr int MAIN = 3 * STAGE + 2 * H1B + 2 * HD * 4;       // + c1 (fp32) kept in LDS
+  static constexpr int NP = 2 * NG, DP = D / NP, DT3 = DP / 16, KT3 = (D + HD) / 32;   // GEMM3 column parts
+  static constexpr int WCP = KT3 * DP * 64, PROW = DP + 4, PARTG = 4 * TOKG * PROW * 4;   // per group
+  static constexpr int RTW = TOKG / 4, LPT = 64 / RTW, CPL = DP / LPT;            // reduce: tokens / lanes
+  static constexpr int WPT = KT3 * DP * 4 / NT;                                   // Wc DMA pieces / thread
+  // GEMM3 phase: Wc parts ping-pong in the stages of chunks NCH, NCH+1 (mod 3); group 0's partials
+  // in the third stage, group 1's from 3*STAGE on (over the h1 slots and c1)
+  static constexpr int LDS3 = 3 * STAGE + (NG > 1 ? PARTG : 0);
+  static constexpr int LDS = MAIN > LDS3 ? MAIN : LDS3;
+  static_assert(TBW >= 1 && HQT % 2 == 0 && KS1 <= 4 && DT3 >= 1 && CPL % 4 == 0, "shape");
+  static_assert(WCP <= STAGE && PARTG <= STAGE && NG <= 2 && KT3 * DP * 4 % NT == 0, "GEMM3 layout");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int D, int HD, int NG>
+__global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
+    const unsigned short* __restrict__ x, int T, const unsigned short* __restrict__ a1t,
+    const float* __restrict__ c1, const unsigned short* __restrict__ w2, const float* __restrict__ b2,
+    const unsigned short* __restrict__ wct, const float* __restrict__ g_post, const float* __restrict__ b_post,
+    const unsigned short* __restrict__ res, unsigned short* __restrict__ out, int abl) {
+  using C = Cfg2<D, HD, NG>;
+  constexpr int KC = C::KC, TT = C::TT, TBW = C::TBW, HQT = C::HQT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* const h1s = smem + 3 * C::STAGE;
+  float* const c1s = reinterpret_cast<float*>(h1s + 2 * C::H1B);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int gq = w >> 2, qq = w & 3;                   // token group, hidden quarter of this wave
+  const int fr = lane & 15, fg = lane >> 4;
+  const long t0 = (long)blockIdx.x * C::TOK;
+  const long tg0 = t0 + gq * C::TOKG;                  // first token of this wave's group
+  const long tw = t0 + w * C::TW1;                     // first GEMM1 token of this wave
+
+  auto issue_chunk = [&](int ch, int st) {
+    unsigned char* sa = smem + st * C::STAGE;
+    unsigned char* sw = sa + C::A1B;
+#pragma unroll
+    for (int p0 = 0; p0 < KC * C::CPA; p0 += C::NT) {
+      const int p = p0 + tid;
+      if (p0 + (tid & ~63) < KC * C::CPA) {
+        const int r = p / C::CPA, pc = p % C::CPA;
+        dma16(a1t + (long)(ch * KC + r) * D + swzA<C::CPA>(r, pc) * 8, sa + (p - lane) * 16);
+      }
+    }
+#pragma unroll
+    for (int p0 = 0; p0 < HD * 4; p0 += C::NT) {
+      const int p = p0 + tid;
+      if (p0 + (tid & ~63) < HD * 4) {
+        const int r = p >> 2, pc = p & 3;
+        dma16(w2 + (long)r * (2 * HD) + ch * KC + swz64(r, pc) * 8, sw + (p - lane) * 16);
+      }
+    }
+  };
+
+  if (abl & 256) return;
+  // c1 goes to LDS once: a global load inside the chunk loop would be younger than the chunk
+  // DMA just issued, and vmcnt retires in order -- GEMM1 would wait for the whole DMA each chunk
+  for (int i = tid; i < 2 * HD; i += C::NT) c1s[i] = c1[i];
+  auto issue_wc = [&](int dp) {                        // Wc^T rows [dp*DP, +DP), all k -> stage (NCH+dp&1)%3
+    unsigned char* dst = smem + ((C::NCH + (dp & 1)) % 3) * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::WPT; ++i) {
+      const int p = i * C::NT + tid;
+      const int kc = p / (C::DP * 4), r = (p >> 2) % C::DP, pc = p & 3;
+      dma16(wct + (long)(dp * C::DP + r) * (D + HD) + kc * 32 + swz64(r, pc) * 8, dst + (p - lane) * 16);
+    }
+  };
+  issue_chunk(0, 0);
+  issue_chunk(1, 1);
+
+  // ---- LN_pre of this wave's GEMM1 tokens -> z fragments (B operand of GEMM1, standard k order)
+  uint4 zf[TBW][C::KS1];
+#pragma unroll
+  for (int tb = 0; tb < TBW; ++tb) {
+    const long tok = min(tw + tb * 16 + fr, (long)T - 1);
+    uint4 xf[C::KS1];
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      xf[ks] = *reinterpret_cast<const uint4*>(x + tok * D + ks * 32 + fg * 8);
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __uint_as_float(wv[e] << 16) + __uint_as_float(wv[e] & 0xffff0000u);
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(wv[e] << 16) - mu, b = __uint_as_float(wv[e] & 0xffff0000u) - mu;
+        q += a * a + b * b;
+      }
+    }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rs = rsqrtf(q * (1.0f / D) + 1e-5f);
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+      uint32_t zv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        zv[e] = pack_bf16x2((__uint_as_float(wv[e] << 16) - mu) * rs, (__uint_as_float(wv[e] & 0xffff0000u) - mu) * rs);
+      zf[tb][ks] = make_uint4(zv[0], zv[1], zv[2], zv[3]);
+    }
+  }
+
+  // GEMM1 of chunk ch for this wave's tokens -> h1 slot (ch & 1), in the GEMM2 B-fragment layout
+  auto gemm1 = [&](int ch) {
+    const unsigned char* sa = smem + (ch % 3) * C::STAGE;
+    const float4 cb0 = *reinterpret_cast<const float4*>(c1s + ch * KC + fg * 4);
+    const float4 cb1 = *reinterpret_cast<const float4*>(c1s + ch * KC + 16 + fg * 4);
+    unsigned char* slot = h1s + (ch & 1) * C::H1B;
+#pragma unroll
+    for (int tb = 0; tb < TBW; ++tb) {
+      f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < C::KS1; ++ks) {
+        const uint4 a0 = *reinterpret_cast<const uint4*>(sa + fr * (2 * D) + swzA<C::CPA>(fr, ks * 4 + fg) * 16);
+        const uint4 a1 = *reinterpret_cast<const uint4*>(sa + (16 + fr) * (2 * D) +
+                                                         swzA<C::CPA>(16 + fr, ks * 4 + fg) * 16);
+        g0 = mfma(a0, zf[tb][ks], g0);
+        g1v = mfma(a1, zf[tb][ks], g1v);
+      }
+      const uint4 hb = make_uint4(pack_bf16x2(hv_gelu_fast(g0[0] + cb0.x), hv_gelu_fast(g0[1] + cb0.y)),
+                                  pack_bf16x2(hv_gelu_fast(g0[2] + cb0.z), hv_gelu_fast(g0[3] + cb0.w)),
+                                  pack_bf16x2(hv_gelu_fast(g1v[0] + cb1.x), hv_gelu_fast(g1v[1] + cb1.y)),
+                                  pack_bf16x2(hv_gelu_fast(g1v[2] + cb1.z), hv_gelu_fast(g1v[3] + cb1.w)));
+      *reinterpret_cast<uint4*>(slot + ((w * TBW + tb) * 64 + lane) * 16) = hb;
+    }
+  };
+
+  f32x4 acc2[HQT][TT];
+#pragma unroll
+  for (int h = 0; h < HQT; ++h)
+#pragma unroll
+    for (int t = 0; t < TT; ++t) acc2[h][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                     // chunks 0, 1 landed
+  gemm1(0);
+  __syncthreads();                                     // h1(0) visible
+  if (abl & 512) return;
+
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    if (ch + 2 < C::NCH) {
+      if (!(abl & 1)) issue_chunk(ch + 2, (ch + 2) % 3);
+    } else {
+      issue_wc(ch + 2 - C::NCH);                       // GEMM3's first two Wc parts ride the tail
+    }
+    if (ch + 1 < C::NCH && !(abl & 4)) gemm1(ch + 1);
+    const unsigned char* sw = smem + (ch % 3) * C::STAGE + C::A1B;
+    const unsigned char* slot = h1s + (ch & 1) * C::H1B + gq * TT * 1024;
+    uint4 bf[TT];                                      // h1 chunk fragments of the group's tokens
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+      bf[t] = (abl & 32) ? make_uint4(t, lane, 1, 2) : *reinterpret_cast<const uint4*>(slot + (t * 64 + lane) * 16);
+#pragma unroll
+    for (int hl = 0; hl < HQT; ++hl) {
+      const int r = (qq * HQT + hl) * 16 + fr;
+      uint4 af = make_uint4(hl, r, 3, 4);
+      if (!(abl & 32)) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+      if (!(abl & 2)) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc2[hl][t] = mfma(af, bf[t], acc2[hl][t]);
+      } else {
+        acc2[hl][0][0] += __uint_as_float(af.x) + __uint_as_float(bf[0].y);
+      }
+    }
+    if (!(abl & 16)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  if ((abl & 1024) && acc2[0][0][0] != 12345.f) return;
+  // ---- h2 = GELU(acc2 + b2) as GEMM3 B fragments (pairs of hidden tiles, permuted k order)
+  uint4 h2f[HQT / 2][TT];
+#pragma unroll
+  for (int j = 0; j < HQT / 2; ++j) {
+    const int hb0 = (qq * HQT + 2 * j) * 16;
+    const float4 ba = *reinterpret_cast<const float4*>(b2 + hb0 + fg * 4);
+    const float4 bb = *reinterpret_cast<const float4*>(b2 + hb0 + 16 + fg * 4);
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      const f32x4 p = acc2[2 * j][t], q = acc2[2 * j + 1][t];
+      h2f[j][t] = make_uint4(pack_bf16x2(hv_gelu_fast(p[0] + ba.x), hv_gelu_fast(p[1] + ba.y)),
+                             pack_bf16x2(hv_gelu_fast(p[2] + ba.z), hv_gelu_fast(p[3] + ba.w)),
+                             pack_bf16x2(hv_gelu_fast(q[0] + bb.x), hv_gelu_fast(q[1] + bb.y)),
+                             pack_bf16x2(hv_gelu_fast(q[2] + bb.z), hv_gelu_fast(q[3] + bb.w)));
+    }
+  }
+  const bool has_x = qq < C::KS1;                      // x chunk qq (32 input columns) on quarter qq
+  uint4 xg[TT];
+  if (has_x) {
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+      xg[t] = *reinterpret_cast<const uint4*>(x + min(tg0 + t * 16 + fr, (long)T - 1) * D + qq * 32 + fg * 8);
+  }
+
+  // ---- GEMM3 (split-K over the 4 quarter waves of a group) + cross-wave reduce, NP column parts;
+  // part dp+2's Wc DMA overlaps the reduce of part dp and the MFMAs of part dp+1
+  if ((abl & 2048) && __uint_as_float(h2f[0][0].x ^ xg[0].y) != 12345.f) return;
+  float* const part = reinterpret_cast<float*>(gq == 0 ? smem + ((C::NCH + 2) % 3) * C::STAGE
+                                                       : smem + 3 * C::STAGE);
+  const int ltok = lane % C::RTW;                      // reduce / LN mapping: token, CPL columns
+  const int cb = (lane / C::RTW) * C::CPL;
+  float y[C::NP][C::CPL];
+#pragma unroll
+  for (int dp = 0; dp < C::NP; ++dp) {
+    if (dp + 1 < C::NP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::WPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                   // Wc part dp visible; part dp-1 reduced
+    if (abl & 8) {
+#pragma unroll
+      for (int c = 0; c < C::CPL; ++c) y[dp][c] = __uint_as_float(h2f[0][0].x) + c;
+      continue;
+    }
+    const unsigned char* wcp = smem + ((C::NCH + (dp & 1)) % 3) * C::STAGE;
+    f32x4 acc3[C::DT3][TT];
+#pragma unroll
+    for (int dt = 0; dt < C::DT3; ++dt)
+#pragma unroll
+      for (int t = 0; t < TT; ++t) acc3[dt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < HQT / 2; ++j) {
+      const int kc = (D + qq * C::HQ) / 32 + j;
+#pragma unroll
+      for (int dt = 0; dt < C::DT3; ++dt) {
+        const int r = dt * 16 + fr;
+        const unsigned char* row = wcp + (kc * C::DP + r) * 64;
+        const uint2 lo = *reinterpret_cast<const uint2*>(row + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(row + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, h2f[j][t], acc3[dt][t]);
+      }
+    }
+    if (has_x) {
+#pragma unroll
+      for (int dt = 0; dt < C::DT3; ++dt) {
+        const int r = dt * 16 + fr;
+        const uint4 af = *reinterpret_cast<const uint4*>(wcp + (qq * C::DP + r) * 64 + swz64(r, fg) * 16);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, xg[t], acc3[dt][t]);
+      }
+    }
+    // partial y^T tiles -> part[quarter][token][col]  (lane: token t*16 + fr, cols dt*16 + 4fg ..)
+    float* pw = part + (long)qq * C::TOKG * C::PROW;
+#pragma unroll
+    for (int dt = 0; dt < C::DT3; ++dt)
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        *reinterpret_cast<f32x4*>(pw + (t * 16 + fr) * C::PROW + dt * 16 + fg * 4) = acc3[dt][t];
+    __syncthreads();                                   // partials written; Wc part dp no longer read
+    if (dp + 2 < C::NP) issue_wc(dp + 2);
+    const float* pg = part + (qq * C::RTW + ltok) * C::PROW + cb;
+#pragma unroll
+    for (int c = 0; c < C::CPL; c += 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(pg + c);
+#pragma unroll
+      for (int s2 = 1; s2 < 4; ++s2) v += *reinterpret_cast<const f32x4*>(pg + s2 * C::TOKG * C::PROW + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[dp][c + j] = v[j];
+    }
+  }
+
+  if ((abl & 4096) && y[0][0] + y[C::NP - 1][C::CPL - 1] != 12345.f) return;
+  // ---- LN_post (+ residual) per token: lanes ltok, ltok + RTW, ... share a token
+  float s = 0.f;
+#pragma unroll
+  for (int dp = 0; dp < C::NP; ++dp)
+#pragma unroll
+    for (int c = 0; c < C::CPL; ++c) s += y[dp][c];
+#pragma unroll
+  for (int o = C::RTW; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int dp = 0; dp < C::NP; ++dp)
+#pragma unroll
+    for (int c = 0; c < C::CPL; ++c) { const float d0 = y[dp][c] - mu; q += d0 * d0; }
+#pragma unroll
+  for (int o = C::RTW; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
+  const float inv = rsqrtf(q * (1.0f / D) + 1e-5f);
+  const long tok = tg0 + qq * C::RTW + ltok;
+  if (tok < T) {
+#pragma unroll
+    for (int dp = 0; dp < C::NP; ++dp) {
+      const int col0 = dp * C::DP + cb;
+#pragma unroll
+      for (int c = 0; c < C::CPL; c += 8) {
+        const int col = col0 + c;
+        const float4 ga = *reinterpret_cast<const float4*>(g_post + col);
+        const float4 gb = *reinterpret_cast<const float4*>(g_post + col + 4);
+        const float4 ba = *reinterpret_cast<const float4*>(b_post + col);
+        const float4 bb = *reinterpret_cast<const float4*>(b_post + col + 4);
+        const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+        const float bv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (y[dp][c + e] - mu) * inv * gg[e] + bv[e];
+        if (res) {
+          const uint4 r4 = *reinterpret_cast<const uint4*>(res + tok * D + col);
+          const uint32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += __uint_as_float(rr[e] << 16);
+            v[2 * e + 1] += __uint_as_float(rr[e] & 0xffff0000u);
+          }
+        }
+        *reinterpret_cast<uint4*>(out + tok * D + col) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      }
+    }
+  }
+}
+
+std::atomic<int> g_ablate2{0};   // diagnostic (tools/mhc_ab.py): 1 no weight DMA, 2 no GEMM2, 4 no GEMM1, 8 no GEMM3
+template <int D, int HD, int NG>
+int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
+  using C = Cfg2<D, HD, NG>;
+  auto k = mhc_fused2_kernel<D, HD, NG>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hv_diag_count(HV_KF_MHC_FUSED);
+  k<<<hv_cdiv(a->T, C::TOK), C::NT, C::LDS, s>>>(
+      (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
+      a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
+      (unsigned short*)a->out, g_ablate2.load(std::memory_order_relaxed));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
 std::atomic<int> g_fused_wide{0};
 std::atomic<int> g_variant{0};
 
@@ -333,7 +698,9 @@ extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype) {
          (D == 256 && Hd == 512 && g_fused_wide);
 }
 extern "C" void hv_mhc_fused_enable_wide(int on) { g_fused_wide = on; }
-// tuning knob (tools/mhc_variants.py): 0 = default tokens-per-wave for D, 1 = half of it
+extern "C" void hv_mhc_fused_set_ablate(int a) { g_ablate2 = a; }
+// tuning knob (tools/mhc_ab.py): 0 = default, 1 = three 4-wave groups per CU, 2 = one 8-wave group,
+// 5 = (D = 128) the per-wave 4-wave kernel instead of the split-hidden one
 extern "C" void hv_mhc_fused_set_variant(int v) { g_variant = v; }
 
 extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
@@ -361,8 +728,12 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
     return launch<64, 256, 2, 2, 4>(a, s);
   }
   if (a->D == 128) {
+    // default: the split-hidden kernel (hidden dimension across 4 waves, 2 token groups per
+    // workgroup) -- tools/mhc_ab.py: 0.306 vs 0.329 ms at T = 102400, 0.073 vs 0.088 at 25600;
+    // variant 5 = the per-wave 4-wave kernel, 2 = per-wave 8-wave
     if (g_variant == 2) return launch<128, 512, 1, 1>(a, s);
-    return launch<128, 512, 1, 2, 4>(a, s);
+    if (g_variant == 5) return launch<128, 512, 1, 2, 4>(a, s);
+    return launch2<128, 512, 2>(a, s);
   }
   // D=256 (ViT, off by default): at T=6416 / 25600 the unfused chain wins (65 / 150 us vs
   // 94 / 139 us fused, tools/mhc_ab.py); 8-wave groups here, variant 1 = 4-wave

@@ -314,10 +314,45 @@ def test_mhc_fused_workgroup_shapes_bitwise_equal(gpu_device, D, T):
         try:
             lib.hv_mhc_fused_set_variant(2)
             y8 = m.forward_tokens(x).cpu()
+            lib.hv_mhc_fused_set_variant(5)          # D=128: the per-wave 4-wave kernel (default is split-hidden)
+            y4 = m.forward_tokens(x).cpu()
         finally:
             lib.hv_mhc_fused_set_variant(0)
-        y4 = m.forward_tokens(x).cpu()
     assert torch.equal(y4, y8)
+
+
+@pytest.mark.parametrize("T,with_res", [(64, False), (200, True), (1000, False), (6417, True)])
+def test_mhc_fused_split_hidden_matches_unfused(gpu_device, T, with_res):
+    """The split-hidden D=128 kernel (the default: hidden dimension across 4 waves, split-K
+    GEMM3 reduced in LDS) vs the unfused six-launch chain and the per-wave fused kernel (bf16),
+    ragged T, residual; deterministic (two runs bitwise equal)."""
+    import ctypes
+    from hv_amd import ManifoldHyperConnection, _lib
+    from hv_amd import manifold as MF
+    from hv_amd.runtime import RunCtx, use_ctx
+    lib = _lib.lib()
+    lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
+    m = ManifoldHyperConnection(128, expansion_rate=4, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(T, 128, generator=g).to(torch.bfloat16).to(gpu_device)
+    res = torch.randn(T, 128, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
+    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
+        try:
+            lib.hv_mhc_fused_set_variant(0)
+            y3 = m.forward_tokens(x, residual=res).float().cpu()
+            y3b = m.forward_tokens(x, residual=res).float().cpu()
+            lib.hv_mhc_fused_set_variant(2)
+            y2 = m.forward_tokens(x, residual=res).float().cpu()
+            MF.USE_FUSED = False
+            y0 = m.forward_tokens(x, residual=res).float().cpu()
+        finally:
+            MF.USE_FUSED = True
+            lib.hv_mhc_fused_set_variant(0)
+    assert torch.equal(y3, y3b)
+    assert rel_l2(y3.numpy(), y0.numpy()) < 1e-2 and (y3 - y0).abs().max() < 0.1
+    assert rel_l2(y3.numpy(), y2.numpy()) < 1e-2
 
 
 # ------------------------------------------------------------------------------ call-site surface (§8b)

@@ -35,7 +35,8 @@ for shp in shapes:
     p = m.plan()
     Hd = ex * D
     fl = 2.0 * T * (D * 2 * Hd + 2 * Hd * Hd + (Hd + D) * D)
-    cases = {"unfused": (False, 0), "fused_v0": (True, 0), "fused_v1": (True, 1), "fused_v2": (True, 2)}
+    cases = {"unfused": (False, 0), "fused_v0": (True, 0), "fused_v1": (True, 1), "fused_v2": (True, 2),
+             "fused_v5": (True, 5)}
     res = {k: [] for k in cases}
     with torch.no_grad():
         MF.USE_FUSED = False
