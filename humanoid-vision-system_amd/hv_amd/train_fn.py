@@ -233,7 +233,7 @@ class MhcFn(torch.autograd.Function):
         dW1 += torch.outer(dc1, u)
         db1 = dc1
         dGc = T.wgrad(dA1t, w1)                            # [D, Hd] = dA1t^T W1
-        du = torch.mv(w1.t(), dc1)                         # [Hd] = W1^T dc1
+        du = ops.gemv(T.transpose_cast(w1, torch.float32), dc1)   # [Hd] = W1^T dc1 (hv_gemv)
         dH_pre_raw, dg_pre, db_pre, dH_res, dH_post_raw = T.mhc_param_backward(
             dGc, du, H_pre_raw, g_pre, b_pre, dwc_x, dwc_h, H_post_raw)
         return (dx, dH_res, dH_pre_raw, dH_post_raw, dg_pre, db_pre, dW1, db1, dW2, db2, dg_post, db_post,
