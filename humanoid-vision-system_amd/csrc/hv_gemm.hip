@@ -349,6 +349,8 @@ static int hv_gemm_force_regstage() { return g_force_regstage.load(std::memory_o
 // 1: route every GEMM through the register-staged kernel (A/B testing of the two paths)
 extern "C" void hv_gemm_set_path(int regstage_only) { g_force_regstage = regstage_only; }
 
+int hv_conv3x3_c32(const hv_gemm_desc& d, hipStream_t s);   // hv_stem.hip
+
 extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (!dp) return HV_EINVAL;
   const hv_gemm_desc& d = *dp;
@@ -367,6 +369,10 @@ extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (((uintptr_t)d.A | (uintptr_t)d.B) & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (!hv_gemm_force_regstage()) {
+    if (d.conv_k == 3 && d.conv_c == 32) {               // halo-tiled 3x3 conv, Cin = 32 (hv_stem.hip)
+      const int rc = hv_conv3x3_c32(d, s);
+      if (rc != HV_EUNSUPPORTED) return rc;
+    }
     const int rc = hv_gemm_glds(d, s);
     if (rc != HV_EUNSUPPORTED) return rc;
   }

@@ -206,8 +206,17 @@ __global__ void k_wgrad_reduce(const float* __restrict__ work, int splits, int N
                                int accumulate) {
   const long total = (long)N1 * N2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += work[k * total + i];
+    // four independent accumulators (loads in flight), fixed combination order: deterministic
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 3 < splits; k += 4) {
+      s0 += work[k * total + i];
+      s1 += work[(k + 1) * total + i];
+      s2 += work[(k + 2) * total + i];
+      s3 += work[(k + 3) * total + i];
+    }
+    for (; k < splits; ++k) s0 += work[k * total + i];
+    const float s = (s0 + s1) + (s2 + s3);
     const long n1 = i / N2, n2 = i - n1 * N2;
     float* o = C + n1 * ldc + n2;
     *o = accumulate ? *o + s : s;

@@ -354,6 +354,37 @@ __global__ void k_maxpool2x2(const T* __restrict__ x, int n, int h, int w, int c
   Elem<T>::store(y, i, v);
 }
 
+// 2x2 max pool (stride 2) with the SE gate applied first, 8 channels per thread, 16-B loads:
+// max_q(x_q * g) = g * max_q(x_q) for the positive sigmoid gate, and storage rounding is
+// monotone, so this equals scale_residual (no identity) followed by k_maxpool2x2 bit for bit
+// while reading the un-pooled map once (gate == nullptr: plain max pool).
+template <typename T>
+__global__ void __launch_bounds__(256) k_scale_maxpool_v(const T* __restrict__ x, const float* gate, int n,
+                                                         int h, int w, int c, long total8, T* y) {
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i8 >= total8) return;
+  const int oh = h / 2, ow = w / 2, cv = c / 8;
+  const int cg = i8 % cv;
+  long p = i8 / cv;
+  const int ox = p % ow; p /= ow;
+  const int oy = p % oh;
+  const int b = p / oh;
+  const T* base = x + (((long)b * h + 2 * oy) * w + 2 * ox) * c + cg * 8;
+  float v0[8], v1[8], v2[8], v3[8];
+  Vec8<T>::load(base, v0);
+  Vec8<T>::load(base + c, v1);
+  Vec8<T>::load(base + (long)w * c, v2);
+  Vec8<T>::load(base + (long)w * c + c, v3);
+  float g[8];
+  if (gate) Vec8<float>::load(gate + (long)b * c + cg * 8, g);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v0[j] = fmaxf(fmaxf(v0[j], v1[j]), fmaxf(v2[j], v3[j]));
+    if (gate) v0[j] *= g[j];
+  }
+  Vec8<T>::store(y + i8 * 8, v0);
+}
+
 // channel sums over pixel chunks: part[n, chunk, c].  A block covers CM_UNROLL row steps of
 // RPI = 256 / (c / VEC) rows; each thread issues its CM_UNROLL 16-byte row-vector loads before
 // summing them (independent loads in flight instead of one dependent load per step), so the
@@ -871,6 +902,16 @@ extern "C" int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int 
   if (total <= 0) return HV_EINVAL;
   HV_DISPATCH(dtype, (k_maxpool2x2<T><<<hv_cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(
                           (const T*)x, n, h, w, c, (T*)y)));
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_scale_maxpool2x2(int dtype, const void* x, const float* gate, int n, int h, int w, int c,
+                                   void* y, hv_stream_t stream) {
+  const long total = (long)n * (h / 2) * (w / 2) * c;
+  if (total <= 0 || c % 8 || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gate) & 15)) return HV_EINVAL;
+  HV_DISPATCH(dtype, (k_scale_maxpool_v<T><<<hv_cdiv(total / 8, 256), 256, 0, (hipStream_t)stream>>>(
+                          (const T*)x, gate, n, h, w, c, total / 8, (T*)y)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -141,6 +141,8 @@ _SIGS = {
     "hv_bn_fold": ([i32, vp, vp, vp, vp, vp, f32, vp, vp, vp], i32),
     "hv_nchw_to_nhwc": ([vp, i32, i32, i32, i32, i32, vp, vp], i32),
     "hv_maxpool2x2": ([i32, vp, i32, i32, i32, i32, vp, vp], i32),
+    "hv_scale_maxpool2x2": ([i32, vp, vp, i32, i32, i32, i32, vp, vp], i32),
+    "hv_conv_stem": ([i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, i32, vp, vp], i32),
     "hv_channel_mean_work_floats": ([i32, i32, i32], C.c_size_t),
     "hv_channel_mean": ([i32, vp, i32, i32, i32, vp, vp, vp], i32),
     "hv_se_mlp": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),

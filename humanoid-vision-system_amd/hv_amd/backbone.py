@@ -12,9 +12,9 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .layers import ctx_scope, run_conv, to_nchw_view, to_nhwc
+from .layers import conv_prep, ctx_scope, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection
-from .runtime import require_cuda, resolve_dtype
+from .runtime import current, require_cuda, resolve_dtype
 
 
 class ConvMHCLayer(nn.Module):
@@ -48,8 +48,28 @@ class ConvMHCLayer(nn.Module):
         nn.init.ones_(self.bn.weight)
         nn.init.zeros_(self.bn.bias)
 
-    def forward_nhwc(self, x: torch.Tensor, extra_residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward_nhwc(self, x: torch.Tensor, extra_residual: Optional[torch.Tensor] = None,
+                     pool: bool = False) -> torch.Tensor:
+        """pool=True appends the stem's MaxPool2d(2, 2) (vision_backbone.py:248); with a gate and
+        no residual the gate multiply and the pool are one pass (ops.maxpool2x2(y, gate))."""
+        if pool:
+            if self.channel_attention is not None and not self.use_residual and extra_residual is None:
+                return self._forward_gated(x, pool=True)
+            return ops.maxpool2x2(self.forward_nhwc(x, extra_residual))
         y = run_conv(x, self.conv, self.bn, self.act_name, self)
+        return self._after_conv(x, y, extra_residual)
+
+    def forward_image(self, img: torch.Tensor, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """First backbone layer straight from the NCHW fp32 image: the direct stem conv
+        (ops.conv_stem) replaces the NCHW->NHWC pass + implicit GEMM.  None if not applicable."""
+        if self.use_residual:
+            return None
+        w, s, b = conv_prep(self.conv, self.bn, dtype, self)
+        y = ops.conv_stem(img, w, self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0], dtype,
+                          scale=s, bias=b, act=self.act_name)
+        return None if y is None else self._after_conv(None, y, None)
+
+    def _after_conv(self, x, y, extra_residual):
         if self.mhc is not None:
             n, h, w, c = y.shape
             y = self.mhc.forward_tokens(y.view(-1, c)).view(n, h, w, c)
@@ -65,6 +85,14 @@ class ConvMHCLayer(nn.Module):
         if extra_residual is not None:
             y = ops.add_scaled(y, extra_residual, 1.0)
         return y
+
+    def _forward_gated(self, x: torch.Tensor, pool: bool) -> torch.Tensor:
+        y = run_conv(x, self.conv, self.bn, self.act_name, self)
+        n, h, w, c = y.shape
+        y = self.mhc.forward_tokens(y.view(-1, c)).view(n, h, w, c)
+        ca = self.channel_attention
+        gate = ops.se_mlp(ops.channel_mean(y), ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
+        return ops.maxpool2x2(y, gate) if pool else ops.scale_residual(y, gate, None)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         require_cuda(x, "ConvMHCLayer")
@@ -146,10 +174,18 @@ class HybridVisionBackbone(nn.Module):
         if verbose:
             print(f"Backbone initialized with channels: {self.output_channels}")
 
-    def forward_nhwc(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
-        for lyr in list(self.stem)[:3]:
-            x = lyr.forward_nhwc(x)
-        x = ops.maxpool2x2(x)
+    def forward_nhwc(self, x: Optional[torch.Tensor], image: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """x: NHWC input; or image: the NCHW fp32 batch, whose first conv then runs as the direct
+        stem kernel (falls back to the NHWC conversion + implicit GEMM when not applicable)."""
+        layers = list(self.stem)[:3]
+        if image is not None:
+            dt = current().dtype
+            y = layers[0].forward_image(image, dt)
+            if y is None:
+                y = layers[0].forward_nhwc(to_nhwc(image, dt))
+            x, layers = y, layers[1:]
+        for i, lyr in enumerate(layers):
+            x = lyr.forward_nhwc(x, pool=lyr is self.stem[2])     # stem[3] MaxPool2d fused into stem[2]
         raw = {"stem": x}
         for i, st in enumerate(self.stages):
             for lyr in st:

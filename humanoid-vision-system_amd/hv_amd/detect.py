@@ -443,8 +443,10 @@ class HybridVisionSystem(nn.Module):
             return system_forward(self, x, targets, task, compute_loss)
         ctx = self._ctx()
         with torch.no_grad(), use_ctx(ctx):
-            xin = to_nhwc(x, ctx.dtype)
-            bb = self.backbone.forward_nhwc(xin)
+            if x.dtype == torch.float32 and x.is_contiguous():
+                bb = self.backbone.forward_nhwc(None, image=x)     # direct stem conv from NCHW
+            else:
+                bb = self.backbone.forward_nhwc(to_nhwc(x, ctx.dtype))
             outputs: Dict[str, Any] = {}
             if self.use_vit:
                 vit = self.vit_encoder.forward_nhwc(bb["scale_large"])

@@ -118,6 +118,28 @@ def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, b
     return out
 
 
+def conv_stem(img: Tensor, w: Tensor, k: int, stride: int, pad: int, dtype: torch.dtype, *, scale=None,
+              bias=None, act: str = "none") -> Optional[Tensor]:
+    """Direct 3x3 conv of an NCHW fp32 image (3 channels) -> NHWC `dtype` (hv_conv_stem), or
+    None when the shape is not one the direct kernel covers (the caller uses conv2d)."""
+    _cuda(img, w)
+    if img.dim() != 4 or img.dtype != torch.float32 or not img.is_contiguous() or w.dtype != dtype:
+        return None
+    n, c, h, wd = img.shape
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (wd + 2 * pad - k) // stride + 1
+    cout = w.shape[0]
+    if c != 3 or k != 3 or cout not in (32, 64) or w.shape[1] < 27 or w.stride(1) != 1 or oh <= 0 or ow <= 0:
+        return None
+    out = torch.empty((n, oh, ow, cout), device=img.device, dtype=dtype)
+    rc = L.lib().hv_conv_stem(dtype_code(dtype), img.data_ptr(), n, c, h, wd, k, stride, pad, w.data_ptr(),
+                              w.stride(0), cout, ptr(scale), ptr(bias), L.ACT[act], out.data_ptr(), stream_ptr())
+    if rc == -2:          # HV_EUNSUPPORTED
+        return None
+    check(rc, "hv_conv_stem")
+    return out
+
+
 # ---------------------------------------------------------------------------- parameters
 def conv_weight_prep(w: Tensor, dtype: torch.dtype, scale: Optional[Tensor] = None) -> Tensor:
     """[cout, cin, k, k] fp32 -> [cout, k*k*cin] (K padded to a 16-byte multiple)."""
@@ -405,9 +427,22 @@ def nchw_to_nhwc(x: Tensor, dtype: torch.dtype) -> Tensor:
     return y
 
 
-def maxpool2x2(x: Tensor) -> Tensor:
+def maxpool2x2(x: Tensor, gate: Optional[Tensor] = None) -> Tensor:
+    """MaxPool2d(2, 2) on NHWC; with gate [n, c] fp32 (SE sigmoid gate, > 0) it returns
+    maxpool(x * gate) in one pass (bitwise equal to scale_residual followed by the pool)."""
     n, h, w, c = x.shape
     y = torch.empty((n, h // 2, w // 2, c), device=x.device, dtype=x.dtype)
+    _contig(x, "x")
+    if gate is not None:
+        _contig(gate, "gate")
+        if gate.dtype != torch.float32 or gate.numel() != n * c:
+            raise ValueError("maxpool2x2 gate must be fp32 [n, c]")
+    if c % 8 == 0 and (x.data_ptr() | y.data_ptr() | (gate.data_ptr() if gate is not None else 0)) % 16 == 0:
+        check(L.lib().hv_scale_maxpool2x2(dtype_code(x.dtype), x.data_ptr(), ptr(gate), n, h, w, c, y.data_ptr(),
+                                          stream_ptr()), "hv_scale_maxpool2x2")
+        return y
+    if gate is not None:
+        x = scale_residual(x, gate, None)
     check(L.lib().hv_maxpool2x2(dtype_code(x.dtype), _contig(x, "x").data_ptr(), n, h, w, c, y.data_ptr(),
                                 stream_ptr()), "hv_maxpool2x2")
     return y

@@ -253,9 +253,22 @@ int hv_wprep_group(const hv_wprep_entry* dev_table, int count, int total_blocks,
 /* NCHW fp32 image -> NHWC (fp32|bf16) */
 int hv_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int y_dtype, void* y,
                     hv_stream_t stream);
+/* Direct 3x3 stem convolution from the NCHW fp32 image (vision_backbone.py:230: Conv2d(3, C, 3,
+ * stride, pad) + folded BN affine + act, the first ConvMHCLayer's conv): y NHWC [n, oh, ow, cout]
+ * in `dtype`, weights [cout, ldw] as from hv_conv_weight_prep (K order kh, kw, cin).  The image
+ * is rounded to `dtype` on load (as hv_nchw_to_nhwc would store it).  cin == 3, k == 3,
+ * cout in {32, 64}; HV_EUNSUPPORTED otherwise (callers use hv_gemm's implicit-GEMM conv). */
+int hv_conv_stem(int dtype, const float* x, int n, int cin, int h, int w, int k, int stride, int pad,
+                 const void* wt, int ldw, int cout, const float* scale, const float* bias, int act,
+                 void* y, hv_stream_t stream);
 /* MaxPool2d(2, 2) (vision_backbone.py:248) */
 int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int c, void* y,
                   hv_stream_t stream);
+/* SE gate then MaxPool2d(2, 2): y = maxpool(x * gate[n, c]) in one pass (the stem's last
+ * ConvMHCLayer gate followed by vision_backbone.py:248's pool; gate NULL = plain pool).
+ * c % 8 == 0, 16-B aligned x / y / gate.  Bitwise equal to hv_scale_residual + hv_maxpool2x2. */
+int hv_scale_maxpool2x2(int dtype, const void* x, const float* gate, int n, int h, int w, int c,
+                        void* y, hv_stream_t stream);
 /* global average pool over H*W -> fp32 [n, c]  (vision_backbone.py:78; hybrid_vision.py:387) */
 size_t hv_channel_mean_work_floats(int n, int hw, int c);
 int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out, float* work,

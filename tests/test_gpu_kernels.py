@@ -365,6 +365,78 @@ def test_conv_implicit_gemm_vs_torch(gpu_device, prec, cin, cout, k, s, p, hw):
     assert rel_err(out.permute(0, 3, 1, 2), ref) < TOL[prec]
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("cout,s,h,w", [(32, 2, 33, 36), (32, 2, 640, 640), (64, 1, 17, 9), (32, 1, 1, 1)])
+def test_conv_stem_direct_vs_torch_and_gemm(gpu_device, prec, cout, s, h, w):
+    """hv_conv_stem (NCHW fp32 image, 3 channels) vs CPU fp32 torch conv+affine+SiLU of the
+    storage-rounded operands, and vs the implicit-GEMM conv of the same operands (summation
+    order is the only difference)."""
+    ops = _ops()
+    dt = DT[prec]
+    n = 1 if h >= 640 else 2
+    g = torch.Generator().manual_seed(cout + s + h)
+    x = torch.randn(n, 3, h, w, generator=g)
+    wt = torch.randn(cout, 3, 3, 3, generator=g) / 27 ** 0.5
+    sc, bi = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)
+    wd = ops.conv_weight_prep(wt.to(gpu_device), dt)
+    out = ops.conv_stem(x.to(gpu_device), wd, 3, s, 1, dt, scale=sc.to(gpu_device), bias=bi.to(gpu_device),
+                        act="silu")
+    assert out is not None and out.dtype == dt
+    xr, wr = x.to(dt).float(), wt.to(dt).float()
+    if h < 640:
+        ref = F.silu(F.conv2d(xr, wr, None, s, 1) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1))
+        assert rel_err(out.float().permute(0, 3, 1, 2), ref) < TOL[prec]
+    gem = ops.conv2d(ops.nchw_to_nhwc(x.to(gpu_device), dt), wd, 3, s, 1, scale=sc.to(gpu_device),
+                     bias=bi.to(gpu_device), act="silu")
+    d = (out.float() - gem.float()).abs().max().item()
+    assert d <= (2e-5 if prec == "fp32" else 2 ** -7 * max(1.0, gem.float().abs().max().item())), d
+
+
+@pytest.mark.parametrize("cout,h,w", [(32, 20, 23), (64, 7, 70), (32, 320, 320), (64, 9, 130)])
+def test_conv3x3_c32_halo_kernel_vs_torch_and_regstage(gpu_device, cout, h, w):
+    """The halo-tiled MFMA conv (hv_stem.hip, bf16 3x3 s1 p1, Cin 32, Cout 32/64: stem[1], stem[2])
+    vs CPU fp32 torch and vs the register-staged implicit GEMM on the same bf16 operands."""
+    from hv_amd import _lib
+    ops = _ops()
+    dt = torch.bfloat16
+    n = 1 if h >= 320 else 2
+    g = torch.Generator().manual_seed(cout * 7 + h + w)
+    x = torch.randn(n, 32, h, w, generator=g).to(dt).float()
+    wt = (torch.randn(cout, 32, 3, 3, generator=g) / 288 ** 0.5).to(dt).float()
+    sc, bi = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)
+    xd = ops.nchw_to_nhwc(x.to(gpu_device), dt)
+    wd = ops.conv_weight_prep(wt.to(gpu_device), dt)
+    kw = dict(scale=sc.to(gpu_device), bias=bi.to(gpu_device), act="silu")
+    out = ops.conv2d(xd, wd, 3, 1, 1, **kw)
+    _lib.lib().hv_gemm_set_path(1)
+    try:
+        reg = ops.conv2d(xd, wd, 3, 1, 1, **kw)
+    finally:
+        _lib.lib().hv_gemm_set_path(0)
+    d = (out.float() - reg.float()).abs()
+    assert d.max().item() <= 2 ** -7 * max(1.0, reg.float().abs().max().item())
+    assert (d > 0).float().mean().item() < 0.02            # equal up to rare 1-ulp roundings
+    if h < 320:
+        ref = F.silu(F.conv2d(x, wt, None, 1, 1) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1))
+        assert rel_err(out.float().permute(0, 3, 1, 2), ref) < TOL["bf16"]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("n,h,w,c", [(2, 8, 6, 64), (1, 320, 320, 64), (3, 5, 7, 8)])
+def test_scale_maxpool_equals_scale_then_pool(gpu_device, prec, n, h, w, c):
+    """maxpool2x2(x, gate) == maxpool2x2(scale_residual(x, gate)) bit for bit (gate > 0)."""
+    ops = _ops()
+    dt = DT[prec]
+    g = torch.Generator().manual_seed(h * w + c)
+    x = torch.randn(n, h, w, c, generator=g).to(dt).to(gpu_device)
+    gate = torch.sigmoid(torch.randn(n, c, generator=g)).to(gpu_device)
+    fused = ops.maxpool2x2(x, gate)
+    ref = ops.maxpool2x2(ops.scale_residual(x, gate, None))
+    assert torch.equal(fused, ref)
+    plain = ops.maxpool2x2(x)
+    assert torch.equal(plain.cpu(), F.max_pool2d(x.float().cpu().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1).to(dt))
+
+
 # ------------------------------------------------------------------------------ pointwise / norms
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_norms_and_pointwise_vs_torch(gpu_device, prec):
