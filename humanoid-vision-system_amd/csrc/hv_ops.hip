@@ -469,6 +469,39 @@ __global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int 
   }
 }
 
+// Batched SE MLP over many workgroups (the one-block-per-image kernel above leaves B=1 on ONE
+// workgroup whose threads walk whole weight rows with strided loads: ~10 us per site).  Stage 1:
+// one wave per hidden unit o, lanes across the input channels (coalesced weight-row reads), the
+// dots of up to NB images accumulated together and reduced by xor shuffles; stage 2 the same per
+// output channel over the hidden vector.  Fixed summation order: deterministic.
+template <int NB, int ACT>
+__global__ void __launch_bounds__(256) k_se_fc(const float* __restrict__ in, int n, int k, int nout,
+                                               const float* __restrict__ w, const float* __restrict__ bias,
+                                               float* __restrict__ out) {
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int b0 = blockIdx.y * NB;
+  if (o >= nout) return;
+  float acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = 0.f;
+  const float* wr = w + (long)o * k;
+  for (int i = lane; i < k; i += 64) {
+    const float wv = wr[i];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      if (b0 + j < n) acc[j] += wv * in[(long)(b0 + j) * k + i];
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = wave_sum(acc[j]);
+  if (lane < NB && b0 + lane < n) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) if (j == lane) v = acc[j];
+    v += bias[o];
+    out[(long)(b0 + lane) * nout + o] = ACT == 0 ? hv_silu(v) : 1.0f / (1.0f + expf(-v));
+  }
+}
+
 template <typename T>
 __global__ void k_scale_residual(const T* __restrict__ x, const float* gate, const T* identity,
                                  int hw, int c, long total, T* y) {
@@ -939,10 +972,28 @@ extern "C" int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, f
   return HV_OK;
 }
 
+extern "C" int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
+                          const float* w2, const float* b2, float* hidden, float* gate, hv_stream_t stream);
 extern "C" int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
                          const float* w2, const float* b2, float* gate, hv_stream_t stream) {
+  return hv_se_mlp2(pooled, n, c, cr, w1, b1, w2, b2, nullptr, gate, stream);
+}
+extern "C" int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
+                          const float* w2, const float* b2, float* hidden, float* gate, hv_stream_t stream) {
   if (n <= 0 || c <= 0 || cr <= 0) return HV_EINVAL;
-  k_se_mlp<<<n, 256, (c + cr) * sizeof(float), (hipStream_t)stream>>>(pooled, c, cr, w1, b1, w2, b2, gate);
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 4 && hidden) {      // measured: at n = 16 the per-image kernel wins (9.8 vs 15.8 + 8.2 us)
+    // batched two-stage form (many workgroups); the hidden vector goes through caller scratch
+    if (n == 1) {
+      k_se_fc<1, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(pooled, n, c, cr, w1, b1, hidden);
+      k_se_fc<1, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
+    } else {
+      k_se_fc<4, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(pooled, n, c, cr, w1, b1, hidden);
+      k_se_fc<4, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
+    }
+  } else {
+    k_se_mlp<<<n, 256, (c + cr) * sizeof(float), s>>>(pooled, c, cr, w1, b1, w2, b2, gate);
+  }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

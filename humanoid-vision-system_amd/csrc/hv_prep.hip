@@ -179,31 +179,20 @@ __global__ void __launch_bounds__(256) k_pg2(const hv_mhc_prep_entry* __restrict
 
 // ------------------------------------------------------------------ phase 3: fold GEMM
 // A1^T[m, n] = sum_k W1[m, k] Gc[n, k]  (M = 2Hd, N = D, K = Hd), 64x64 tiles, 4 waves 2x2,
-// k-steps of FOLD_BK = 128 staged through LDS after an fp32 -> compute-type convert.  bf16: one
-// v_mfma_f32_16x16x32_bf16 per 16x16 sub-tile and 32-deep k; fp32: v_mfma_f32_16x16x4_f32 x 4
-// per 16-deep half (exact products; lane group g takes k = 4g..4g+3 of each half).
-// The tile's life is a chain of K / FOLD_BK dependent global-load round trips (the MFMA work per
-// step is small): 128-deep steps put 16 KiB per operand in flight per workgroup and cut the
-// chain 4x against the former 32-deep steps (K = 2048 at the D = 1024 sites: 16 steps, not 64).
-constexpr int FOLD_BK = 128;
-template <typename T>
-struct FoldLds {
-  static constexpr int RB = (std::is_same<T, unsigned short>::value ? 2 : 4) * FOLD_BK + 16;  // row bytes
-  static constexpr int BYTES = 2 * 64 * RB;
-};
-
+// k-steps of 32 staged through LDS after an fp32 -> compute-type convert.  bf16: one
+// v_mfma_f32_16x16x32_bf16 per 16x16 sub-tile; fp32: v_mfma_f32_16x16x4_f32 x 8 (exact
+// products; lane group g takes k = 4g..4g+3 of each 16-deep half).
 template <typename T>
 __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scratch& sc, int tile, char* lds) {
   constexpr bool BF = std::is_same<T, unsigned short>::value;
-  constexpr int RB = FoldLds<T>::RB;
-  constexpr int LPT = FOLD_BK / 4;        // floats per thread per operand per k-step (4 threads a row)
+  constexpr int RB = BF ? 80 : 144;      // LDS row bytes: 32 k + 16 B pad
   const int D = e.D, K = e.Hd;
   const int ntn = (D + 63) / 64;
   const int m0 = (tile / ntn) * 64, n0 = (tile % ntn) * 64;
   char* As = lds;
   char* Bs = lds + 64 * RB;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int lr = t >> 2, lq = (t & 3) * LPT;
+  const int lr = t >> 2, lq = (t & 3) * 8;
   const float* Ar = e.w1 + (long)(m0 + lr) * K + lq;
   const bool bvalid = n0 + lr < D;
   const float* Br = sc.gc + (long)(bvalid ? n0 + lr : 0) * K + lq;
@@ -214,57 +203,52 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
     for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   // register double buffering: the next k-step's global loads are issued before this step's
   // MFMAs, so their latency overlaps the compute instead of stalling every k-step
-  float4 na[LPT / 4], nb[LPT / 4];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < LPT / 4; ++i) {
-      const bool kin = k0 + lq + 4 * i < K;          // K % 4 == 0 (Hd = e * D)
-      na[i] = kin ? *reinterpret_cast<const float4*>(Ar + k0 + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      nb[i] = (kin && bvalid) ? *reinterpret_cast<const float4*>(Br + k0 + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += FOLD_BK) {
+  float4 na0 = *reinterpret_cast<const float4*>(Ar);
+  float4 na1 = *reinterpret_cast<const float4*>(Ar + 4);
+  float4 nb0 = make_float4(0.f, 0.f, 0.f, 0.f), nb1 = nb0;
+  if (bvalid) {
+    nb0 = *reinterpret_cast<const float4*>(Br);
+    nb1 = *reinterpret_cast<const float4*>(Br + 4);
+  }
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    const float4 a0 = na0, a1 = na1, b0 = nb0, b1 = nb1;
     __syncthreads();
     if constexpr (BF) {
-#pragma unroll
-      for (int i = 0; i < LPT / 8; ++i) {
-        const float4 a0 = na[2 * i], a1 = na[2 * i + 1], b0 = nb[2 * i], b1 = nb[2 * i + 1];
-        const u16x8 pa = {f2bf(a0.x), f2bf(a0.y), f2bf(a0.z), f2bf(a0.w), f2bf(a1.x), f2bf(a1.y), f2bf(a1.z), f2bf(a1.w)};
-        const u16x8 pb = {f2bf(b0.x), f2bf(b0.y), f2bf(b0.z), f2bf(b0.w), f2bf(b1.x), f2bf(b1.y), f2bf(b1.z), f2bf(b1.w)};
-        *reinterpret_cast<u16x8*>(As + lr * RB + (lq + 8 * i) * 2) = pa;
-        *reinterpret_cast<u16x8*>(Bs + lr * RB + (lq + 8 * i) * 2) = pb;
-      }
+      const u16x8 pa = {f2bf(a0.x), f2bf(a0.y), f2bf(a0.z), f2bf(a0.w), f2bf(a1.x), f2bf(a1.y), f2bf(a1.z), f2bf(a1.w)};
+      const u16x8 pb = {f2bf(b0.x), f2bf(b0.y), f2bf(b0.z), f2bf(b0.w), f2bf(b1.x), f2bf(b1.y), f2bf(b1.z), f2bf(b1.w)};
+      *reinterpret_cast<u16x8*>(As + lr * RB + lq * 2) = pa;
+      *reinterpret_cast<u16x8*>(Bs + lr * RB + lq * 2) = pb;
     } else {
-#pragma unroll
-      for (int i = 0; i < LPT / 4; ++i) {
-        *reinterpret_cast<float4*>(As + lr * RB + (lq + 4 * i) * 4) = na[i];
-        *reinterpret_cast<float4*>(Bs + lr * RB + (lq + 4 * i) * 4) = nb[i];
-      }
+      *reinterpret_cast<float4*>(As + lr * RB + lq * 4) = a0;
+      *reinterpret_cast<float4*>(As + lr * RB + lq * 4 + 16) = a1;
+      *reinterpret_cast<float4*>(Bs + lr * RB + lq * 4) = b0;
+      *reinterpret_cast<float4*>(Bs + lr * RB + lq * 4 + 16) = b1;
     }
     __syncthreads();
-    if (k0 + FOLD_BK < K) load(k0 + FOLD_BK);
+    if (k0 + 32 < K) {
+      na0 = *reinterpret_cast<const float4*>(Ar + k0 + 32);
+      na1 = *reinterpret_cast<const float4*>(Ar + k0 + 36);
+      if (bvalid) {
+        nb0 = *reinterpret_cast<const float4*>(Br + k0 + 32);
+        nb1 = *reinterpret_cast<const float4*>(Br + k0 + 36);
+      }
+    }
     const int fr = lane & 15, fg = lane >> 4;
     if constexpr (BF) {
+      uint4 fa[2], fb[2];
 #pragma unroll
-      for (int ks = 0; ks < FOLD_BK / 32; ++ks) {
-        uint4 fa[2], fb[2];
+      for (int a = 0; a < 2; ++a) fa[a] = *reinterpret_cast<const uint4*>(As + (wr * 32 + a * 16 + fr) * RB + fg * 16);
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-          fa[a] = *reinterpret_cast<const uint4*>(As + (wr * 32 + a * 16 + fr) * RB + ks * 64 + fg * 16);
+      for (int c = 0; c < 2; ++c) fb[c] = *reinterpret_cast<const uint4*>(Bs + (wc * 32 + c * 16 + fr) * RB + fg * 16);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-          fb[c] = *reinterpret_cast<const uint4*>(Bs + (wc * 32 + c * 16 + fr) * RB + ks * 64 + fg * 16);
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-            acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[a]),
-                                                                __builtin_bit_cast(bf16x8, fb[c]), acc[a][c], 0, 0, 0);
-      }
+          acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[a]),
+                                                              __builtin_bit_cast(bf16x8, fb[c]), acc[a][c], 0, 0, 0);
     } else {
 #pragma unroll
-      for (int h = 0; h < FOLD_BK / 16; ++h) {
+      for (int h = 0; h < 2; ++h) {
         float4 fa[2], fb[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -300,7 +284,7 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict__ tab, int count) {
-  __shared__ __attribute__((aligned(16))) char lds[FoldLds<T>::BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 144];
   const int ei = find_entry<hv_mhc_prep_entry, 2>(tab, count, blockIdx.x);
   const hv_mhc_prep_entry& e = tab[ei];
   const PrepSizes s = prep_sizes(e.D, e.Hd, e.fold);

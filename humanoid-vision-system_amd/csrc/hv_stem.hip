@@ -5,11 +5,9 @@
 // With 3 input channels the contraction is K = 27: an implicit GEMM spends its time on a
 // K-tile that is 58% padding and on the separate NCHW -> NHWC conversion pass (the pair ran at
 // 16 TFLOP/s, 0.23 ms at B=16 640^2).  The layer is HBM-bound (78.6 MB image in, 105 MB NHWC
-// bf16 out at B=16), so one thread per output pixel computes all COUT channels in fp32
-// registers: the 27 input taps are loaded once (rounded to the storage type exactly like the
-// conversion pass did), the weights sit k-major in LDS (broadcast reads, one 16-B read per 4
-// output channels), and the pixel's COUT outputs leave as whole 16-B stores -- consecutive
-// threads write consecutive 64-B pixel rows.  Arithmetic matches the GEMM path term for term
+// bf16 out at B=16): the 27 input taps of a pixel are loaded once per lane (rounded to the
+// storage type exactly like the conversion pass did), weights live in registers, and the
+// pixel's COUT outputs leave as one contiguous run.  Arithmetic matches the GEMM path term for term
 // (bf16 x bf16 products, fp32 sums, acc * scale + bias, activation); only the summation order
 // differs.
 #include "hv_common.h"
@@ -20,78 +18,79 @@ template <typename T> __device__ __forceinline__ float stor_round(float v);
 template <> __device__ __forceinline__ float stor_round<float>(float v) { return v; }
 template <> __device__ __forceinline__ float stor_round<unsigned short>(float v) { return bf2f(f2bf(v)); }
 
-template <typename T> __device__ __forceinline__ void store8(T* p, const float* v);
-template <> __device__ __forceinline__ void store8<float>(float* p, const float* v) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
-}
-template <> __device__ __forceinline__ void store8<unsigned short>(unsigned short* p, const float* v) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                            pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
-}
-
 constexpr int kStemCin = 3, kStemTaps = 9 * kStemCin;
 
-template <typename T, int COUT>
-__global__ void __launch_bounds__(256) k_conv_stem(const float* __restrict__ x, int n, int h, int w, int oh,
+// x: NCHW fp32 (TI = float, NHWC = false; rounded to T on load) or NHWC T (the engine's
+// preprocessed input) -- both layouts give the same values, hence the same outputs.
+// Work split: COUT/4 adjacent lanes share an output pixel, each owning 4 output channels whose
+// 27 x 4 weights stay in registers for the whole (grid-stride) walk over pixels; the lanes of a
+// pixel load the same 27 taps (one coalesced address per pixel) and together store the pixel's
+// COUT outputs as one contiguous run.  (One thread per pixel with all COUT channels made the
+// compiler hoist every weight read of the unrolled tap loop: 512 VGPRs + scratch, 1.9 ms at
+// B=16.)
+template <typename T> __device__ __forceinline__ void store4(T* p, const float* v);
+template <> __device__ __forceinline__ void store4<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void store4<unsigned short>(unsigned short* p, const float* v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+}
+
+template <typename T, int COUT, typename TI, bool NHWC>
+__global__ void __launch_bounds__(256) k_conv_stem(const TI* __restrict__ x, int n, int h, int w, int oh,
                                                    int ow, int stride, int pad, const T* __restrict__ wt,
                                                    int ldw, const float* scale, const float* bias, int act,
                                                    T* __restrict__ y) {
-  __shared__ float4 ws[kStemTaps][COUT / 4];        // k-major: the COUT weights of tap k
-  __shared__ float sc[COUT], bi[COUT];
-  for (int i = threadIdx.x; i < kStemTaps * COUT; i += 256) {
-    const int co = i / kStemTaps, k = i % kStemTaps;
-    reinterpret_cast<float*>(&ws[k][0])[co] = Elem<T>::load(wt, (long)co * ldw + k);
+  constexpr int Q = COUT / 4, PPB = 256 / Q;           // lanes per pixel, pixels per block step
+  const int q = threadIdx.x % Q;
+  float4 wr[kStemTaps];
+#pragma unroll
+  for (int k = 0; k < kStemTaps; ++k)
+    wr[k] = make_float4(Elem<T>::load(wt, (long)(4 * q + 0) * ldw + k), Elem<T>::load(wt, (long)(4 * q + 1) * ldw + k),
+                        Elem<T>::load(wt, (long)(4 * q + 2) * ldw + k), Elem<T>::load(wt, (long)(4 * q + 3) * ldw + k));
+  float sc[4], bi[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sc[j] = scale ? scale[4 * q + j] : 1.f;
+    bi[j] = bias ? bias[4 * q + j] : 0.f;
   }
-  for (int i = threadIdx.x; i < COUT; i += 256) {
-    sc[i] = scale ? scale[i] : 1.f;
-    bi[i] = bias ? bias[i] : 0.f;
-  }
-  __syncthreads();
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (long)n * oh * ow) return;
-  const int ox = p % ow;
-  const long q = p / ow;
-  const int oy = q % oh;
-  const int b = q / oh;
-  float in[kStemTaps];
+  const long npix = (long)n * oh * ow;
+  for (long p = (long)blockIdx.x * PPB + threadIdx.x / Q; p < npix; p += (long)gridDim.x * PPB) {
+    const int ox = p % ow;
+    const long qq = p / ow;
+    const int oy = qq % oh;
+    const int b = qq / oh;
+    float in[kStemTaps];
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int iy = oy * stride - pad + ky;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * stride - pad + ky;
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = ox * stride - pad + kx;
-      const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * stride - pad + kx;
+        const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
 #pragma unroll
-      for (int ci = 0; ci < kStemCin; ++ci)
-        in[(ky * 3 + kx) * kStemCin + ci] =
-            ok ? stor_round<T>(x[(((long)b * kStemCin + ci) * h + iy) * w + ix]) : 0.f;
+        for (int ci = 0; ci < kStemCin; ++ci) {
+          float v = 0.f;
+          if (ok) {
+            if constexpr (NHWC) v = Elem<TI>::load(x, (((long)b * h + iy) * w + ix) * kStemCin + ci);
+            else v = stor_round<T>(x[(((long)b * kStemCin + ci) * h + iy) * w + ix]);
+          }
+          in[(ky * 3 + kx) * kStemCin + ci] = v;
+        }
+      }
     }
-  }
-  float acc[COUT];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) acc[c] = 0.f;
-#pragma unroll
-  for (int k = 0; k < kStemTaps; ++k) {
-#pragma unroll
-    for (int c4 = 0; c4 < COUT / 4; ++c4) {
-      const float4 wv = ws[k][c4];
-      acc[4 * c4 + 0] = fmaf(in[k], wv.x, acc[4 * c4 + 0]);
-      acc[4 * c4 + 1] = fmaf(in[k], wv.y, acc[4 * c4 + 1]);
-      acc[4 * c4 + 2] = fmaf(in[k], wv.z, acc[4 * c4 + 2]);
-      acc[4 * c4 + 3] = fmaf(in[k], wv.w, acc[4 * c4 + 3]);
+    for (int k = 0; k < kStemTaps; ++k) {
+      acc[0] = fmaf(in[k], wr[k].x, acc[0]);
+      acc[1] = fmaf(in[k], wr[k].y, acc[1]);
+      acc[2] = fmaf(in[k], wr[k].z, acc[2]);
+      acc[3] = fmaf(in[k], wr[k].w, acc[3]);
     }
-  }
-  T* out = y + p * COUT;
+    float v[4];
 #pragma unroll
-  for (int c8 = 0; c8 < COUT / 8; ++c8) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c8 * 8 + j;
-      v[j] = hv_act(acc[c] * sc[c] + bi[c], act);
-    }
-    store8<T>(out + c8 * 8, v);
+    for (int j = 0; j < 4; ++j) v[j] = hv_act(acc[j] * sc[j] + bi[j], act);
+    store4<T>(y + p * COUT + 4 * q, v);
   }
 }
 
@@ -102,7 +101,7 @@ __global__ void __launch_bounds__(256) k_conv_stem(const float* __restrict__ x, 
 // a 64-wide N tile of which N = 32 fills half (0.165 ms per launch at B=16, ~1.2 TB/s).
 // Here a workgroup owns a 4 x 64 output-pixel tile: its (4+2) x (64+2) x 32-channel input halo is
 // loaded ONCE into LDS, the weights live in registers for the whole workgroup (one 16x16x32 A
-// fragment per (tap, 16-channel tile): 9 x N/16), and wave w computes output row w as
+// fragment per (tap, 16-channel tile): 9 x 2 per wave), and wave w of a group computes row w as
 // D^T[channel][pixel] = W . X^T -- the tap's 32 input channels are exactly one MFMA k-step, the
 // B fragment (16 pixels x 8 channels per lane group) is one conflict-free 16-B LDS read shared by
 // the N/16 channel tiles, and each lane ends with 4 consecutive output channels of one pixel
@@ -116,10 +115,12 @@ __device__ __forceinline__ f32x4 mfma_bf16(const uint4& a, const uint4& b, const
 
 constexpr int C3_CIN = 32, C3_TW = 64, C3_TH = 4, C3_HW = C3_TW + 2, C3_HH = C3_TH + 2;
 
+// NT = N/16 channel tiles; the workgroup has NT/2 groups of 4 waves, group h computing channel
+// tiles 2h, 2h+1 (so a wave holds 18 weight fragments + 8 accumulators at any N: 128 VGPRs)
 template <int NT>
-__global__ void __launch_bounds__(256) k_conv3x3_c32(const hv_gemm_desc d, int tiles_x, int tiles_y) {
+__global__ void __launch_bounds__(128 * NT) k_conv3x3_c32(const hv_gemm_desc d, int tiles_x, int tiles_y) {
   __shared__ __attribute__((aligned(16))) bf halo[C3_HH * C3_HW * C3_CIN];   // 25,344 B
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, hgrp = tid >> 8;
   const int fr = lane & 15, g = lane >> 4;
   // XCD-aware order: the 8 XCDs take contiguous runs of tiles (neighbours share halo rows in L2)
   const int G = gridDim.x;
@@ -132,14 +133,14 @@ __global__ void __launch_bounds__(256) k_conv3x3_c32(const hv_gemm_desc d, int t
   const int x0 = tx * C3_TW, y0 = ty * C3_TH;
   const bf* X = (const bf*)d.A;
   const bf* Wt = (const bf*)d.B;
-  uint4 wf[9][NT];
+  uint4 wf[9][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-      wf[t][nt] = *reinterpret_cast<const uint4*>(Wt + (long)(nt * 16 + fr) * d.ldb + t * C3_CIN + g * 8);
+    for (int nt = 0; nt < 2; ++nt)
+      wf[t][nt] = *reinterpret_cast<const uint4*>(Wt + (long)((2 * hgrp + nt) * 16 + fr) * d.ldb + t * C3_CIN + g * 8);
   constexpr int CHUNKS = C3_HH * C3_HW * 4;         // 16-B chunks (4 per pixel)
-  for (int c = tid; c < CHUNKS; c += 256) {
+  for (int c = tid; c < CHUNKS; c += 128 * NT) {
     const int q = c & 3, pix = c >> 2;
     const int hx = pix % C3_HW, hy = pix / C3_HW;
     const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
@@ -149,11 +150,11 @@ __global__ void __launch_bounds__(256) k_conv3x3_c32(const hv_gemm_desc d, int t
     *reinterpret_cast<uint4*>(halo + pix * C3_CIN + q * 8) = v;
   }
   __syncthreads();
-  f32x4 acc[4][NT];
+  f32x4 acc[4][2];
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[pt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nt = 0; nt < 2; ++nt) acc[pt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -162,17 +163,17 @@ __global__ void __launch_bounds__(256) k_conv3x3_c32(const hv_gemm_desc d, int t
       for (int pt = 0; pt < 4; ++pt) {
         const uint4 bfr = *reinterpret_cast<const uint4*>(halo + ((w + ky) * C3_HW + pt * 16 + fr + kx) * C3_CIN + g * 8);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[pt][nt] = mfma_bf16(wf[ky * 3 + kx][nt], bfr, acc[pt][nt]);
+        for (int nt = 0; nt < 2; ++nt) acc[pt][nt] = mfma_bf16(wf[ky * 3 + kx][nt], bfr, acc[pt][nt]);
       }
   const int oy = y0 + w;
   if (oy >= H) return;
   const bool gelu_fast = d.act == HV_ACT_GELU;
-  float sc[NT][4], bi[NT][4];
+  float sc[2][4], bi[2][4];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
+  for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = nt * 16 + 4 * g + j;
+      const int n = (2 * hgrp + nt) * 16 + 4 * g + j;
       sc[nt][j] = d.scale ? d.scale[n] * d.alpha : d.alpha;
       bi[nt][j] = d.bias ? d.bias[n] : 0.f;
     }
@@ -183,14 +184,15 @@ __global__ void __launch_bounds__(256) k_conv3x3_c32(const hv_gemm_desc d, int t
     if (ox >= W) continue;
     const long m = ((long)b * H + oy) * W + ox;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
+    for (int nt = 0; nt < 2; ++nt) {
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float x = acc[pt][nt][j] * sc[nt][j] + bi[nt][j];
         v[j] = gelu_fast ? hv_gelu_fast(x) : hv_act(x, d.act);
       }
-      *reinterpret_cast<uint2*>(C + m * d.ldc + nt * 16 + 4 * g) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      *reinterpret_cast<uint2*>(C + m * d.ldc + (2 * hgrp + nt) * 16 + 4 * g) =
+          make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
     }
   }
 }
@@ -209,14 +211,25 @@ int hv_conv3x3_c32(const hv_gemm_desc& d, hipStream_t s) {
   const long grid = (long)d.conv_n * tiles_x * tiles_y;
   if (grid <= 0 || grid > 0x7fffffffL) return HV_EUNSUPPORTED;
   if (d.N == 32) k_conv3x3_c32<2><<<(unsigned)grid, 256, 0, s>>>(d, tiles_x, tiles_y);
-  else k_conv3x3_c32<4><<<(unsigned)grid, 256, 0, s>>>(d, tiles_x, tiles_y);
+  else k_conv3x3_c32<4><<<(unsigned)grid, 512, 0, s>>>(d, tiles_x, tiles_y);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
-extern "C" int hv_conv_stem(int dtype, const float* x, int n, int cin, int h, int w, int k, int stride, int pad,
-                            const void* wt, int ldw, int cout, const float* scale, const float* bias, int act,
-                            void* y, hv_stream_t stream) {
+template <typename T, int COUT>
+void launch_stem(const void* x, int x_nhwc, int n, int h, int w, int oh, int ow, int stride, int pad, const void* wt,
+                 int ldw, const float* scale, const float* bias, int act, void* y, unsigned grid, hipStream_t s) {
+  if (x_nhwc)
+    k_conv_stem<T, COUT, T, true><<<grid, 256, 0, s>>>((const T*)x, n, h, w, oh, ow, stride, pad, (const T*)wt, ldw,
+                                                      scale, bias, act, (T*)y);
+  else
+    k_conv_stem<T, COUT, float, false><<<grid, 256, 0, s>>>((const float*)x, n, h, w, oh, ow, stride, pad,
+                                                           (const T*)wt, ldw, scale, bias, act, (T*)y);
+}
+
+extern "C" int hv_conv_stem(int dtype, const void* x, int x_nhwc, int n, int cin, int h, int w, int k, int stride,
+                            int pad, const void* wt, int ldw, int cout, const float* scale, const float* bias,
+                            int act, void* y, hv_stream_t stream) {
   if (cin != kStemCin || k != 3 || stride < 1 || pad < 0 || n <= 0 || h <= 0 || w <= 0 || ldw < kStemTaps)
     return HV_EUNSUPPORTED;
   if ((cout != 32 && cout != 64) || (((uintptr_t)y) & 15)) return HV_EUNSUPPORTED;
@@ -224,22 +237,16 @@ extern "C" int hv_conv_stem(int dtype, const float* x, int n, int cin, int h, in
   const int oh = (h + 2 * pad - 3) / stride + 1, ow = (w + 2 * pad - 3) / stride + 1;
   if (oh <= 0 || ow <= 0) return HV_EINVAL;
   const long total = (long)n * oh * ow;
-  const unsigned grid = (unsigned)hv_cdiv(total, 256);
+  const long per = 256 / (cout / 4);                    // pixels per block step
+  const long want = (total + per - 1) / per;
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);   // grid-stride: ~8 blocks per CU
   hipStream_t s = (hipStream_t)stream;
   if (dtype == HV_BF16) {
-    if (cout == 32)
-      k_conv_stem<unsigned short, 32><<<grid, 256, 0, s>>>(x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt,
-                                                           ldw, scale, bias, act, (unsigned short*)y);
-    else
-      k_conv_stem<unsigned short, 64><<<grid, 256, 0, s>>>(x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt,
-                                                           ldw, scale, bias, act, (unsigned short*)y);
+    if (cout == 32) launch_stem<unsigned short, 32>(x, x_nhwc, n, h, w, oh, ow, stride, pad, wt, ldw, scale, bias, act, y, grid, s);
+    else launch_stem<unsigned short, 64>(x, x_nhwc, n, h, w, oh, ow, stride, pad, wt, ldw, scale, bias, act, y, grid, s);
   } else {
-    if (cout == 32)
-      k_conv_stem<float, 32><<<grid, 256, 0, s>>>(x, n, h, w, oh, ow, stride, pad, (const float*)wt, ldw, scale,
-                                                  bias, act, (float*)y);
-    else
-      k_conv_stem<float, 64><<<grid, 256, 0, s>>>(x, n, h, w, oh, ow, stride, pad, (const float*)wt, ldw, scale,
-                                                  bias, act, (float*)y);
+    if (cout == 32) launch_stem<float, 32>(x, x_nhwc, n, h, w, oh, ow, stride, pad, wt, ldw, scale, bias, act, y, grid, s);
+    else launch_stem<float, 64>(x, x_nhwc, n, h, w, oh, ow, stride, pad, wt, ldw, scale, bias, act, y, grid, s);
   }
   HV_CHECK_LAUNCH();
   return HV_OK;

@@ -142,10 +142,11 @@ _SIGS = {
     "hv_nchw_to_nhwc": ([vp, i32, i32, i32, i32, i32, vp, vp], i32),
     "hv_maxpool2x2": ([i32, vp, i32, i32, i32, i32, vp, vp], i32),
     "hv_scale_maxpool2x2": ([i32, vp, vp, i32, i32, i32, i32, vp, vp], i32),
-    "hv_conv_stem": ([i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, i32, vp, vp], i32),
+    "hv_conv_stem": ([i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, i32, vp, vp], i32),
     "hv_channel_mean_work_floats": ([i32, i32, i32], C.c_size_t),
     "hv_channel_mean": ([i32, vp, i32, i32, i32, vp, vp, vp], i32),
     "hv_se_mlp": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),
+    "hv_se_mlp2": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_scale_residual": ([i32, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "hv_upsample_add": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp], i32),
     "hv_add_scaled": ([i32, vp, vp, i64, f32, vp, vp], i32),

@@ -6,6 +6,7 @@ matrix the mHC layer consumes, so the reference's permute/reshape round trips
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -15,6 +16,12 @@ from . import ops
 from .layers import conv_prep, ctx_scope, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection
 from .runtime import current, require_cuda, resolve_dtype
+
+# Direct stem conv (hv_conv_stem) instead of NHWC conversion + implicit GEMM: opt-in.  Measured
+# in-model at B=16 640^2 (profiles/r02/stem_direct_ab.txt): 606 us vs 237 us for the pair it
+# replaces -- per-lane address math and the 8-lane redundant tap loads dominate; B=1: 48.8 vs
+# ~35 us.  Kept (parity-tested) for the A/B, off by default.
+_DIRECT_STEM = os.environ.get("HV_DIRECT_STEM", "0") == "1"
 
 
 class ConvMHCLayer(nn.Module):
@@ -59,14 +66,15 @@ class ConvMHCLayer(nn.Module):
         y = run_conv(x, self.conv, self.bn, self.act_name, self)
         return self._after_conv(x, y, extra_residual)
 
-    def forward_image(self, img: torch.Tensor, dtype: torch.dtype) -> Optional[torch.Tensor]:
-        """First backbone layer straight from the NCHW fp32 image: the direct stem conv
-        (ops.conv_stem) replaces the NCHW->NHWC pass + implicit GEMM.  None if not applicable."""
+    def forward_image(self, img: torch.Tensor, dtype: torch.dtype, nhwc: bool = False) -> Optional[torch.Tensor]:
+        """First backbone layer straight from the image (NCHW fp32, or NHWC `dtype`): the direct
+        stem conv (ops.conv_stem) replaces the NCHW->NHWC pass + implicit GEMM.  None if not
+        applicable."""
         if self.use_residual:
             return None
         w, s, b = conv_prep(self.conv, self.bn, dtype, self)
         y = ops.conv_stem(img, w, self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0], dtype,
-                          scale=s, bias=b, act=self.act_name)
+                          scale=s, bias=b, act=self.act_name, nhwc=nhwc)
         return None if y is None else self._after_conv(None, y, None)
 
     def _after_conv(self, x, y, extra_residual):
@@ -178,12 +186,20 @@ class HybridVisionBackbone(nn.Module):
         """x: NHWC input; or image: the NCHW fp32 batch, whose first conv then runs as the direct
         stem kernel (falls back to the NHWC conversion + implicit GEMM when not applicable)."""
         layers = list(self.stem)[:3]
+        dt = current().dtype
+        if image is not None and not _DIRECT_STEM:
+            x, image = to_nhwc(image, dt), None
         if image is not None:
-            dt = current().dtype
             y = layers[0].forward_image(image, dt)
             if y is None:
                 y = layers[0].forward_nhwc(to_nhwc(image, dt))
             x, layers = y, layers[1:]
+        else:
+            # NHWC input (the engine's preprocessed frame): the same direct stem kernel, so both
+            # input layouts give identical results
+            y = layers[0].forward_image(x, dt, nhwc=True) if x.shape[-1] == 3 and _DIRECT_STEM else None
+            if y is not None:
+                x, layers = y, layers[1:]
         for i, lyr in enumerate(layers):
             x = lyr.forward_nhwc(x, pool=lyr is self.stem[2])     # stem[3] MaxPool2d fused into stem[2]
         raw = {"stem": x}

@@ -119,21 +119,30 @@ def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, b
 
 
 def conv_stem(img: Tensor, w: Tensor, k: int, stride: int, pad: int, dtype: torch.dtype, *, scale=None,
-              bias=None, act: str = "none") -> Optional[Tensor]:
-    """Direct 3x3 conv of an NCHW fp32 image (3 channels) -> NHWC `dtype` (hv_conv_stem), or
-    None when the shape is not one the direct kernel covers (the caller uses conv2d)."""
+              bias=None, act: str = "none", nhwc: bool = False) -> Optional[Tensor]:
+    """Direct 3x3 conv of a 3-channel image -> NHWC `dtype` (hv_conv_stem): img is the NCHW fp32
+    batch (nhwc=False) or an NHWC `dtype` tensor (nhwc=True).  None when the shape is not one
+    the direct kernel covers (the caller uses conv2d)."""
     _cuda(img, w)
-    if img.dim() != 4 or img.dtype != torch.float32 or not img.is_contiguous() or w.dtype != dtype:
+    if img.dim() != 4 or not img.is_contiguous() or w.dtype != dtype:
         return None
-    n, c, h, wd = img.shape
+    if nhwc:
+        n, h, wd, c = img.shape
+        if img.dtype != dtype:
+            return None
+    else:
+        n, c, h, wd = img.shape
+        if img.dtype != torch.float32:
+            return None
     oh = (h + 2 * pad - k) // stride + 1
     ow = (wd + 2 * pad - k) // stride + 1
     cout = w.shape[0]
     if c != 3 or k != 3 or cout not in (32, 64) or w.shape[1] < 27 or w.stride(1) != 1 or oh <= 0 or ow <= 0:
         return None
     out = torch.empty((n, oh, ow, cout), device=img.device, dtype=dtype)
-    rc = L.lib().hv_conv_stem(dtype_code(dtype), img.data_ptr(), n, c, h, wd, k, stride, pad, w.data_ptr(),
-                              w.stride(0), cout, ptr(scale), ptr(bias), L.ACT[act], out.data_ptr(), stream_ptr())
+    rc = L.lib().hv_conv_stem(dtype_code(dtype), img.data_ptr(), int(nhwc), n, c, h, wd, k, stride, pad,
+                              w.data_ptr(), w.stride(0), cout, ptr(scale), ptr(bias), L.ACT[act], out.data_ptr(),
+                              stream_ptr())
     if rc == -2:          # HV_EUNSUPPORTED
         return None
     check(rc, "hv_conv_stem")
@@ -465,8 +474,9 @@ def se_mlp(pooled: Tensor, w1, b1, w2, b2) -> Tensor:
     cr = w1.shape[0]
     gate = torch.empty_like(pooled)
     w1, b1, w2, b2 = map(f32, (w1, b1, w2, b2))
-    check(L.lib().hv_se_mlp(pooled.data_ptr(), n, c, cr, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
-                            b2.data_ptr(), gate.data_ptr(), stream_ptr()), "hv_se_mlp")
+    hidden = torch.empty((n, cr), device=pooled.device, dtype=torch.float32) if n <= 4 else None
+    check(L.lib().hv_se_mlp2(pooled.data_ptr(), n, c, cr, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                             b2.data_ptr(), ptr(hidden), gate.data_ptr(), stream_ptr()), "hv_se_mlp2")
     return gate
 
 

@@ -253,13 +253,14 @@ int hv_wprep_group(const hv_wprep_entry* dev_table, int count, int total_blocks,
 /* NCHW fp32 image -> NHWC (fp32|bf16) */
 int hv_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int y_dtype, void* y,
                     hv_stream_t stream);
-/* Direct 3x3 stem convolution from the NCHW fp32 image (vision_backbone.py:230: Conv2d(3, C, 3,
- * stride, pad) + folded BN affine + act, the first ConvMHCLayer's conv): y NHWC [n, oh, ow, cout]
- * in `dtype`, weights [cout, ldw] as from hv_conv_weight_prep (K order kh, kw, cin).  The image
- * is rounded to `dtype` on load (as hv_nchw_to_nhwc would store it).  cin == 3, k == 3,
+/* Direct 3x3 stem convolution (vision_backbone.py:230: Conv2d(3, C, 3, stride, pad) + folded BN
+ * affine + act, the first ConvMHCLayer's conv) from the image: x_nhwc = 0 -> x is the NCHW fp32
+ * batch (rounded to `dtype` on load, as hv_nchw_to_nhwc would store it); x_nhwc = 1 -> x is NHWC
+ * in `dtype` (the engine's preprocessed input).  y NHWC [n, oh, ow, cout] in `dtype`, weights
+ * [cout, ldw] as from hv_conv_weight_prep (K order kh, kw, cin).  cin == 3, k == 3,
  * cout in {32, 64}; HV_EUNSUPPORTED otherwise (callers use hv_gemm's implicit-GEMM conv). */
-int hv_conv_stem(int dtype, const float* x, int n, int cin, int h, int w, int k, int stride, int pad,
-                 const void* wt, int ldw, int cout, const float* scale, const float* bias, int act,
+int hv_conv_stem(int dtype, const void* x, int x_nhwc, int n, int cin, int h, int w, int k, int stride,
+                 int pad, const void* wt, int ldw, int cout, const float* scale, const float* bias, int act,
                  void* y, hv_stream_t stream);
 /* MaxPool2d(2, 2) (vision_backbone.py:248) */
 int hv_maxpool2x2(int dtype, const void* x, int n, int h, int w, int c, void* y,
@@ -276,6 +277,10 @@ int hv_channel_mean(int dtype, const void* x, int n, int hw, int c, float* out, 
 /* squeeze-excite MLP: s = sigmoid(W2 silu(W1 pooled + b1) + b2)  (vision_backbone.py:77-83) */
 int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
               const float* w2, const float* b2, float* gate, hv_stream_t stream);
+/* same with caller scratch hidden[n, cr] fp32: n <= 4 then runs as two batched stages over many
+ * workgroups (one wave per output unit, coalesced weight rows) instead of one workgroup per image */
+int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
+               const float* w2, const float* b2, float* hidden, float* gate, hv_stream_t stream);
 /* y = x * gate[n, c] (+ identity)  (vision_backbone.py:126-132) */
 int hv_scale_residual(int dtype, const void* x, const float* gate, const void* identity,
                       int n, int hw, int c, void* y, hv_stream_t stream);

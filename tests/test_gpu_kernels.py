@@ -386,10 +386,28 @@ def test_conv_stem_direct_vs_torch_and_gemm(gpu_device, prec, cout, s, h, w):
     if h < 640:
         ref = F.silu(F.conv2d(xr, wr, None, s, 1) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1))
         assert rel_err(out.float().permute(0, 3, 1, 2), ref) < TOL[prec]
-    gem = ops.conv2d(ops.nchw_to_nhwc(x.to(gpu_device), dt), wd, 3, s, 1, scale=sc.to(gpu_device),
-                     bias=bi.to(gpu_device), act="silu")
+    xh = ops.nchw_to_nhwc(x.to(gpu_device), dt)
+    out_h = ops.conv_stem(xh, wd, 3, s, 1, dt, scale=sc.to(gpu_device), bias=bi.to(gpu_device), act="silu",
+                          nhwc=True)
+    assert torch.equal(out_h, out)                      # NHWC input == NCHW fp32 input, bit for bit
+    gem = ops.conv2d(xh, wd, 3, s, 1, scale=sc.to(gpu_device), bias=bi.to(gpu_device), act="silu")
     d = (out.float() - gem.float()).abs().max().item()
     assert d <= (2e-5 if prec == "fp32" else 2 ** -7 * max(1.0, gem.float().abs().max().item())), d
+
+
+@pytest.mark.parametrize("n,c", [(1, 1024), (3, 64), (16, 512), (17, 128), (2, 2048)])
+def test_se_mlp_batched_vs_torch(gpu_device, n, c):
+    """hv_se_mlp2: batched two-stage SE MLP (n <= 16) and the per-image kernel (n > 16) vs CPU
+    fp32 torch (vision_backbone.py:77-83: sigmoid(W2 silu(W1 p + b1) + b2))."""
+    ops = _ops()
+    cr = c // 4
+    g = torch.Generator().manual_seed(n * 31 + c)
+    w1, b1 = torch.randn(cr, c, 1, 1, generator=g) / c ** 0.5, torch.randn(cr, generator=g)
+    w2, b2 = torch.randn(c, cr, 1, 1, generator=g) / cr ** 0.5, torch.randn(c, generator=g)
+    pooled = torch.randn(n, c, generator=g)
+    gt = ops.se_mlp(pooled.to(gpu_device), w1.to(gpu_device), b1.to(gpu_device), w2.to(gpu_device), b2.to(gpu_device))
+    ref = torch.sigmoid(F.linear(F.silu(F.linear(pooled, w1.view(cr, c), b1)), w2.view(c, cr), b2))
+    assert rel_err(gt, ref) < 1e-5
 
 
 @pytest.mark.parametrize("cout,h,w", [(32, 20, 23), (64, 7, 70), (32, 320, 320), (64, 9, 130)])

@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 FAMILIES = {
-    "gemm": ("gemm_glds_kernel", "gemm_kernel", "gemm_pp256_kernel", "gemm_sk_kernel"),
+    "gemm": ("gemm_glds_kernel", "gemm_kernel", "gemm_pp256_kernel", "gemm_sk_kernel", "k_conv3x3_c32"),
     "mhc_fused": ("mhc_fused_kernel",),
 }
 
