@@ -17,6 +17,7 @@ for step in "$@"; do
     breakdown) timeout -k 10 300 python -u tools/gemm_breakdown.py > $OUT/gemm_breakdown.txt 2>&1 || { tail -30 $OUT/gemm_breakdown.txt; exit 1; } ; head -50 $OUT/gemm_breakdown.txt ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE; do timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { tail -30 $OUT/pmc_$c.log; exit 1; } ; done ; python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_traffic.json ;;
     latprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/latprof -o run --output-format csv -- python tools/lat_prof.py > $OUT/latprof.log 2>&1 || { tail -30 $OUT/latprof.log; exit 1; } ; f=$(find $OUT/latprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 1 40 > $OUT/latprof_summary.txt; head -25 $OUT/latprof_summary.txt ;;
+    trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trainprof -o run --output-format csv -- python tools/train_diag.py time 16 640 > $OUT/trainprof.log 2>&1 || { tail -30 $OUT/trainprof.log; exit 1; } ; f=$(find $OUT/trainprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 6 45 > $OUT/trainprof_summary.txt; head -30 $OUT/trainprof_summary.txt ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done
