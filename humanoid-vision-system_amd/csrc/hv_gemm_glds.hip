@@ -40,7 +40,7 @@ __device__ __forceinline__ void glds16_asm(const void* src, unsigned lds_addr) {
 }
 #pragma clang diagnostic pop
 
-template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2>
+template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2, bool SPLIT = false>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
@@ -138,14 +138,17 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
 #pragma unroll
     for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (d.K + 63) / 64;          // conv: K % 64 != 0 allowed, the tail reads zeros
+  const int nkt = (d.K + 63) / 64;         // conv: K % 64 != 0 allowed, the tail reads zeros
+  // split-K: this workgroup's slice [kb, kb + nk) of the K-tiles (blockIdx.y = slice)
+  const int kb = SPLIT ? (int)(((long)nkt * blockIdx.y) / d.splitk) : 0;
+  const int nk = SPLIT ? (int)(((long)nkt * (blockIdx.y + 1)) / d.splitk) - kb : nkt;
   constexpr int DPT = AI + BI;              // DMA instructions per wave per K-tile
   // ring of NS buffers, NS-1 K-tiles in flight.  Iteration kt: wait for this wave's DMAs of tile
   // kt (the younger tiles stay in flight), barrier (every wave's tile kt landed, every wave's
   // reads of tile kt-1 retired), refill the buffer of tile kt-1 with tile kt+NS-1, compute kt.
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) stage(t, t);
+    if (t < nk) stage(t, kb + t);
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
@@ -162,7 +165,7 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kt + NS - 1);
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kb + kt + NS - 1);
     const unsigned char* sa = smem + (kt % NS) * STAGE_BYTES;
     const unsigned char* sb = sa + BM * ROW;
 #pragma unroll
@@ -191,6 +194,61 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
+  if constexpr (SPLIT) {
+    // raw fp32 partials of this K slice -> splitk_work[slice][row][col] (a lane holds 4
+    // consecutive columns of one row per sub-tile, as in gemm_epilogue); the last workgroup of
+    // the tile to arrive sums the slices in slice order and runs the normal epilogue
+    const long mn = (long)d.M * d.N;
+    const bool v4 = (d.N & 3) == 0;
+    float* wk = d.splitk_work + (long)blockIdx.y * mn;
+#pragma unroll
+    for (int a = 0; a < RM; ++a) {
+      const int row = m0 + wr * (RM * 16) + a * 16 + fr;
+      if (row >= d.M) continue;
+#pragma unroll
+      for (int b = 0; b < RN; ++b) {
+        const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4;
+        if (v4 && col + 4 <= d.N) {
+          *reinterpret_cast<f32x4*>(wk + (long)row * d.N + col) = acc[a][b];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (col + j < d.N) wk[(long)row * d.N + col + j] = acc[a][b][j];
+        }
+      }
+    }
+    __shared__ int last;
+    __threadfence();                                  // partials visible device-wide (all XCDs)
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = atomicAdd(d.splitk_count + bid, 1);
+      last = prev == d.splitk - 1;
+      if (last) d.splitk_count[bid] = 0;              // leave the counter zero for the next launch
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();                                  // acquire: see the other slices' partials
+#pragma unroll
+    for (int a = 0; a < RM; ++a) {
+      const int row = min(m0 + wr * (RM * 16) + a * 16 + fr, d.M - 1);
+#pragma unroll
+      for (int b = 0; b < RN; ++b) {
+        const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4;
+        f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sl = 0; sl < d.splitk; ++sl) {
+          const float* p = d.splitk_work + sl * mn + (long)row * d.N + col;
+          if (v4 && col + 4 <= d.N) {
+            t += *reinterpret_cast<const f32x4*>(p);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (col + j < d.N) t[j] += p[j];
+          }
+        }
+        acc[a][b] = t;
+      }
+    }
+  }
   // ---- epilogue (shared with the register-staged kernel; acc holds transposed sub-tiles;
   //      LN_EPI: LayerNorm after the product)
   if constexpr (STAGED) {
@@ -433,6 +491,16 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   }
 }
 
+int launch_splitk(const hv_gemm_desc& d, hipStream_t s) {
+  const unsigned tiles = hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64);
+  hv_diag_count(HV_KF_GEMM_SPLITK);
+  const dim3 grid(tiles, d.splitk);
+  if (d.conv_k > 0) gemm_glds_kernel<64, 64, true, false, false, 4, true><<<grid, 256, 0, s>>>(d);
+  else gemm_glds_kernel<64, 64, false, false, false, 4, true><<<grid, 256, 0, s>>>(d);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
 std::atomic<int> g_staged_train{1};   // LDS-staged epilogue for the training modes (A/B knob)
 std::atomic<int> g_staged_epi{1};             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
 
@@ -513,6 +581,14 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
   if (d.ldb % 8) return HV_EUNSUPPORTED;
+  if (d.splitk > 1) {
+    // caller-requested split-K (small output grids, long K): inference epilogues only
+    if (d.conv_k > 0 && d.K % 64) return HV_EUNSUPPORTED;
+    if (d.epi_mode || !d.splitk_work || !d.splitk_count || d.splitk > 64 ||
+        (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64) > HV_SPLITK_MAX_TILES)
+      return HV_EINVAL;
+    return launch_splitk(d, s);
+  }
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   const long t256 = (long)hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
   switch (g_force_tile.load(std::memory_order_relaxed)) {

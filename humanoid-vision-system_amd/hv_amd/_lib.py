@@ -47,7 +47,8 @@ class GemmDesc(C.Structure):
                 ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
                 ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp),
                 ("aux", vp), ("ld_aux", i64), ("aux_dtype", i32), ("epi_mode", i32),
-                ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("pad1_", i32)]
+                ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("pad1_", i32),
+                ("splitk_work", vp), ("splitk_count", vp), ("splitk", i32), ("pad2_", i32)]
 
 
 class CopySegment(C.Structure):

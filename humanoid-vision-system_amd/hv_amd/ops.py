@@ -8,6 +8,7 @@ sequences are [rows, c].
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import torch
@@ -41,6 +42,47 @@ def _contig(t: Tensor, name: str) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- GEMM
+# Split-K is opt-in (HV_SPLITK=1): measured no gain (profiles/r02/splitk_ab.txt) -- with a
+# separate reduce launch the split GEMM + reduce (6.1 + 5.4 us) cost what the un-split kernel
+# does (10.1 us) at B=1; with the reduction fused into the last-arriving workgroup the
+# agent-scope release/acquire (L2 write-back + invalidate on every workgroup) made it 31 us.
+SPLITK_ON = os.environ.get("HV_SPLITK", "0") == "1"
+_SPLITK_COUNTERS: dict = {}
+SPLITK_MAX_TILES = 4096                                      # HV_SPLITK_MAX_TILES
+
+
+def _splitk_counters(device) -> Tensor:
+    """Per-(device, stream) tile arrival counters of the split-K kernel: zeroed once, and every
+    launch leaves them zero (its last workgroup per tile resets its counter); launches on one
+    stream are ordered, so they can share them."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    c = _SPLITK_COUNTERS.get(key)
+    if c is None:
+        c = torch.zeros(SPLITK_MAX_TILES, device=device, dtype=torch.int32)
+        _SPLITK_COUNTERS[key] = c
+    return c
+
+
+def _splitk(d, M: int, N: int, K: int, dtype: torch.dtype, device) -> Optional[Tensor]:
+    """Split-K for small output grids with long contractions (B=1 streaming: the ViT's 401-token
+    GEMMs, the coarse FPN / head convs; the 16-row final-fusion GEMMs at any batch): the bf16
+    LDS-DMA kernel has too few 64x64 output tiles to fill 256 CUs, so each tile's K-tiles are
+    split over `splitk` workgroups (>= 4 K-tiles each); the last workgroup of a tile to finish
+    sums the fp32 partials in slice order and runs the epilogue (deterministic).  Returns the workspace
+    (kept alive by the caller until the launch is enqueued) or None."""
+    if not SPLITK_ON or dtype != torch.bfloat16 or K % 64:
+        return None
+    tiles = -(-M // 64) * -(-N // 64)
+    if tiles >= 192:
+        return None
+    splits = min(K // 256, max(2, 384 // tiles), 64)
+    if splits < 2:
+        return None
+    work = torch.empty(splits * M * N, device=device, dtype=torch.float32)
+    d.splitk_work, d.splitk_count, d.splitk = work.data_ptr(), _splitk_counters(device).data_ptr(), splits
+    return work
+
+
 def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional[Tensor] = None,
          act: str = "none", alpha: float = 1.0, residual: Optional[Tensor] = None,
          a_mean: Optional[Tensor] = None, a_rstd: Optional[Tensor] = None,
@@ -83,6 +125,7 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
     if residual is not None:
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), residual.stride(0), dtype_code(residual.dtype)
         d.r_mod = residual_mod
+    work = _splitk(d, M, N, K, a.dtype, a.device)      # noqa: F841  (alive until enqueued)
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm M={M} N={N} K={K}")
     return out
 
@@ -114,6 +157,7 @@ def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, b
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), cout, dtype_code(residual.dtype)
     d.conv_n, d.conv_h, d.conv_w, d.conv_c = n, h, wd, c
     d.conv_k, d.conv_stride, d.conv_pad, d.conv_oh, d.conv_ow = k, stride, pad, oh, ow
+    work = _splitk(d, d.M, cout, d.K, x.dtype, x.device)   # noqa: F841  (alive until enqueued)
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(conv {c}->{cout} k{k} s{stride})")
     return out
 
@@ -853,7 +897,8 @@ def stability_stats(x_in: Tensor, x_out: Tensor, h: Tensor, history: Optional[Te
 
 # ---------------------------------------------------------------------------- diagnostics
 KERNEL_FAMILIES = ("gemm_pp256", "glds_128x128", "glds_64x128", "glds_128x64", "glds_64x64", "gemm_regstage",
-                   "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group", "attn_general", "gemm_smallk")
+                   "mhc_fused", "attn_mfma", "attn_scalar", "sinkhorn_group", "attn_general", "gemm_smallk",
+                   "gemm_splitk")
 
 
 def launch_counts(reset: bool = False) -> dict:

@@ -117,8 +117,20 @@ typedef struct hv_gemm_desc {
      input pixel (ih, iw) reads output pixel ((ih + pad - kh) / stride, ...) when divisible. */
   int conv_transposed;
   int pad1_;
+  /* split-K for small output grids (inference epilogues, epi_mode 0, bf16, LDS-DMA kernel):
+     splitk > 1 splits the K-tiles of every output tile over `splitk` workgroups, each writing
+     its fp32 partial product to splitk_work [splitk][M][N] and bumping the tile's arrival
+     counter; the LAST workgroup to arrive sums the partials in slice order (deterministic,
+     independent of arrival order) and runs the epilogue above.  0 or 1 = off.  The caller owns
+     the workspace (splitk * M * N floats) and the counters (HV_SPLITK_MAX_TILES ints, zero
+     before the first use; every launch leaves them zero again). */
+  float* splitk_work;
+  int* splitk_count;
+  int splitk;
+  int pad2_;
 } hv_gemm_desc;
 
+#define HV_SPLITK_MAX_TILES 4096
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

@@ -54,6 +54,7 @@ enum hv_kernel_family {
   HV_KF_SINKHORN_GROUP = 9,  /* one grouped Sinkhorn forward (all its passes) */
   HV_KF_ATTN_GENERAL = 10,   /* hv_attention_general (cross / masked / weights / CLS-row queries) */
   HV_KF_GEMM_SMALLK = 11,    /* gemm_sk_kernel (persistent small-K, register epilogue) */
+  HV_KF_GEMM_SPLITK = 12,    /* split-K LDS-DMA GEMM (64x64 tiles) + its reduce launch */
   HV_KF_COUNT = 16
 };
 /* copies the HV_KF_COUNT launch counters into out[] */

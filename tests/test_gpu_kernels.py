@@ -141,6 +141,59 @@ def test_gemm_ln_epilogue_equals_prologue(gpu_device, T, D, N):
     assert rel_err(pro, ref) < TOL["bf16"]
 
 
+@pytest.mark.parametrize("M,N,K,kind", [(401, 512, 1024, "plain"), (401, 1024, 256 + 768, "ln"),
+                                         (401, 256, 768, "cat"), (16, 1792, 1792, "plain"),
+                                         (16, 7168, 1792, "resmod"), (400, 1024, 2304, "conv")])
+def test_gemm_splitk_vs_unsplit(gpu_device, M, N, K, kind):
+    """Split-K (small output grids: ops._splitk engages for < 192 64x64 tiles, bf16) against the
+    register-staged un-split kernel and a CPU fp32 torch reference: same epilogue (LN after the
+    product, scale, bias, GELU, residual / row-modulo residual, concat-K, implicit-GEMM conv);
+    only the summation order differs.  Also checks the split actually engaged and that it is
+    deterministic (bitwise across runs)."""
+    ops = _ops()
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(M + N + K)
+    dev = gpu_device
+    kw = {}
+    if kind == "conv":
+        x = torch.randn(1, 20, 20, 256, generator=g).to(dt).to(dev)
+        w = (torch.randn(N, 2304, generator=g) / 48).to(dt).to(dev)
+        kw = dict(scale=(torch.rand(N, generator=g) + 0.5).to(dev), bias=torch.randn(N, generator=g).to(dev),
+                  act="silu")
+        run = lambda: ops.conv2d(x, w, 3, 1, 1, **kw)                      # noqa: E731
+    else:
+        a = (torch.randn(M, K if kind != "cat" else 256, generator=g) * (3 if kind == "ln" else 1) + 1).to(dt).to(dev)
+        b = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt).to(dev)
+        kw = dict(bias=torch.randn(N, generator=g).to(dev), act="gelu")
+        if kind == "ln":
+            mean, rstd = ops.row_stats(a, 1e-5)
+            kw.update(a_mean=mean, a_rstd=rstd, b_colsum=b.float().sum(1).contiguous())
+        if kind == "cat":
+            kw["a2"] = torch.randn(M, K - 256, generator=g).to(dt).to(dev)
+        if kind == "resmod":
+            kw.update(residual=torch.randn(4, N, generator=g).to(dt).to(dev), residual_mod=4)
+            kw.pop("act")
+        run = lambda: ops.gemm(a, b, **kw)                                   # noqa: E731
+    saved = ops.SPLITK_ON
+    ops.SPLITK_ON = True                                    # opt-in path (off by default)
+    try:
+        ops.launch_counts(reset=True)
+        out = run()
+        counts = ops.launch_counts(reset=True)
+        assert counts["gemm_splitk"] == 1, counts           # the split path ran
+        assert torch.equal(run(), out)                      # deterministic
+        ops.SPLITK_ON = False
+        ref = run()                                         # same LDS-DMA kernel family, un-split
+    finally:
+        ops.SPLITK_ON = saved
+    d = (out.float() - ref.float()).abs()
+    assert d.max().item() <= 2 ** -6 * max(1.0, ref.float().abs().max().item()), d.max().item()
+    assert rel_err(out.float(), ref.float()) < 4e-3
+    if kind == "plain":                                     # and vs CPU fp32 torch
+        cpu = F.gelu(a.float().cpu() @ b.float().cpu().T + kw["bias"].cpu())
+        assert rel_err(out.float().cpu(), cpu) < TOL["bf16"]
+
+
 def test_gemm_residual_mod(gpu_device):
     ops = _ops()
     a = torch.randn(6 * 10, 32)
