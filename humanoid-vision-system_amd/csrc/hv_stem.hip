@@ -10,6 +10,8 @@
 // pixel's COUT outputs leave as one contiguous run.  Arithmetic matches the GEMM path term for term
 // (bf16 x bf16 products, fp32 sums, acc * scale + bias, activation); only the summation order
 // differs.
+#include <type_traits>
+
 #include "hv_common.h"
 
 namespace {
@@ -216,9 +218,134 @@ int hv_conv3x3_c32(const hv_gemm_desc& d, hipStream_t s) {
   return HV_OK;
 }
 
+namespace {
+
+// bf16 stem on the matrix cores: the workgroup stages the input rows of a 2 x 64 output-pixel
+// tile ((2-1)*s+3 rows x (64-1)*s+3 columns x 3 channels, rounded to bf16) in LDS with
+// coalesced row loads, then each wave runs the whole 27(->32)-deep contraction of 16 pixels x
+// 16 channels as ONE 16x16x32 MFMA: the B fragment is the pixel's 8 taps k = 8g..8g+7 (k order
+// kh, kw, cin as the weights; k >= 27 zero) gathered from LDS through a per-lane offset table,
+// the A fragments (weights) stay in registers.  Same instruction, operands and k order as the
+// implicit-GEMM path's single K-step, so the outputs match it; the NHWC and NCHW inputs give
+// the same values.  Lane (pixel fr, group g) ends with 4 consecutive channels -> 8-B stores.
+constexpr int STM_TOH = 2, STM_TOW = 64;
+constexpr int STM_IH = (STM_TOH - 1) * 2 + 3, STM_IW = (STM_TOW - 1) * 2 + 3;   // stride <= 2
+
+template <int COUT, typename TI, bool NHWC>
+__global__ void __launch_bounds__(256) k_conv_stem_mfma(const TI* __restrict__ x, int n, int h, int w, int oh,
+                                                        int ow, int stride, int pad, const unsigned short* __restrict__ wt,
+                                                        int ldw, const float* scale, const float* bias, int act,
+                                                        unsigned short* __restrict__ y, int tiles_x, int tiles_y) {
+  constexpr int NT = COUT / 16;
+  __shared__ float xs[kStemCin][STM_IH][STM_IW];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * STM_TOH, ox0 = tx * STM_TOW;
+  const int iy0 = oy0 * stride - pad, ix0 = ox0 * stride - pad;
+  const int rows = (STM_TOH - 1) * stride + 3, cols = (STM_TOW - 1) * stride + 3;
+  // stage the input tile (rounded to bf16 exactly as the NHWC conversion pass stores it)
+  if constexpr (NHWC) {
+    for (int i = tid; i < rows * cols * kStemCin; i += 256) {
+      const int ci = i % kStemCin, rc = i / kStemCin, c = rc % cols, r = rc / cols;
+      const int iy = iy0 + r, ix = ix0 + c;
+      float v = 0.f;
+      if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = Elem<TI>::load(x, (((long)b * h + iy) * w + ix) * kStemCin + ci);
+      xs[ci][r][c] = v;
+    }
+  } else {
+    for (int i = tid; i < kStemCin * rows * cols; i += 256) {
+      const int c = i % cols, rr = i / cols, r = rr % rows, ci = rr / rows;
+      const int iy = iy0 + r, ix = ix0 + c;
+      float v = 0.f;
+      if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = bf2f(f2bf(x[(((long)b * kStemCin + ci) * h + iy) * w + ix]));
+      xs[ci][r][c] = v;
+    }
+  }
+  // weights (A operand): channel tile nt, row fr, k = 8g .. 8g+7
+  uint4 wf[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    unsigned short e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * g + j;
+      e[j] = k < kStemTaps ? wt[(long)(nt * 16 + fr) * ldw + k] : (unsigned short)0;
+    }
+    wf[nt] = make_uint4(e[0] | (unsigned)e[1] << 16, e[2] | (unsigned)e[3] << 16, e[4] | (unsigned)e[5] << 16,
+                        e[6] | (unsigned)e[7] << 16);
+  }
+  // this lane's 8 taps as LDS offsets relative to the pixel's window origin (-1: zero pad of k)
+  int off[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * g + j;
+    const int tap = k / kStemCin, ci = k % kStemCin;
+    off[j] = k < kStemTaps ? (ci * STM_IH + tap / 3) * STM_IW + tap % 3 : -1;
+  }
+  float sc[NT][4], bi[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = nt * 16 + 4 * g + j;
+      sc[nt][j] = scale ? scale[c] : 1.f;
+      bi[nt][j] = bias ? bias[c] : 0.f;
+    }
+  __syncthreads();
+  const float* xf = &xs[0][0][0];
+  // 128 pixels = 8 groups of 16; wave wv takes groups wv and wv + 4
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = (wv + 4 * q) * 16 + fr;             // pixel within the tile (B column = fr)
+    const int py = p / STM_TOW, px = p % STM_TOW;
+    const int base = py * stride * STM_IW + px * stride;
+    float v8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v8[j] = off[j] >= 0 ? xf[base + off[j]] : 0.f;
+    const uint4 xb = make_uint4(pack_bf16x2(v8[0], v8[1]), pack_bf16x2(v8[2], v8[3]), pack_bf16x2(v8[4], v8[5]),
+                                pack_bf16x2(v8[6], v8[7]));
+    const int oy = oy0 + py, ox = ox0 + px;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[nt]),
+                                                                __builtin_bit_cast(bf16x8, xb),
+                                                                f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if (oy < oh && ox < ow) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = hv_act(acc[j] * sc[nt][j] + bi[nt][j], act);
+        *reinterpret_cast<uint2*>(y + (((long)b * oh + oy) * ow + ox) * COUT + nt * 16 + 4 * g) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+}  // namespace
+
 template <typename T, int COUT>
 void launch_stem(const void* x, int x_nhwc, int n, int h, int w, int oh, int ow, int stride, int pad, const void* wt,
                  int ldw, const float* scale, const float* bias, int act, void* y, unsigned grid, hipStream_t s) {
+  if constexpr (std::is_same<T, unsigned short>::value) {
+    if (stride <= 2) {                                  // the MFMA kernel (bf16)
+      const int tiles_x = hv_cdiv(ow, STM_TOW), tiles_y = hv_cdiv(oh, STM_TOH);
+      const unsigned g2 = (unsigned)((long)n * tiles_x * tiles_y);
+      if (x_nhwc)
+        k_conv_stem_mfma<COUT, unsigned short, true><<<g2, 256, 0, s>>>(
+            (const unsigned short*)x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt, ldw, scale, bias, act,
+            (unsigned short*)y, tiles_x, tiles_y);
+      else
+        k_conv_stem_mfma<COUT, float, false><<<g2, 256, 0, s>>>(
+            (const float*)x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt, ldw, scale, bias, act,
+            (unsigned short*)y, tiles_x, tiles_y);
+      return;
+    }
+  }
   if (x_nhwc)
     k_conv_stem<T, COUT, T, true><<<grid, 256, 0, s>>>((const T*)x, n, h, w, oh, ow, stride, pad, (const T*)wt, ldw,
                                                       scale, bias, act, (T*)y);

@@ -17,11 +17,11 @@ from .layers import conv_prep, ctx_scope, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection
 from .runtime import current, require_cuda, resolve_dtype
 
-# Direct stem conv (hv_conv_stem) instead of NHWC conversion + implicit GEMM: opt-in.  Measured
-# in-model at B=16 640^2 (profiles/r02/stem_direct_ab.txt): 606 us vs 237 us for the pair it
-# replaces -- per-lane address math and the 8-lane redundant tap loads dominate; B=1: 48.8 vs
-# ~35 us.  Kept (parity-tested) for the A/B, off by default.
-_DIRECT_STEM = os.environ.get("HV_DIRECT_STEM", "0") == "1"
+# Direct stem conv (hv_conv_stem: bf16 = LDS-staged input tile + one MFMA k-step per 16 pixels)
+# instead of the NCHW->NHWC pass + implicit GEMM (237 us at B=16 640^2).  Same-box A/B
+# (profiles/r02/stem_direct_ab.txt): 759.5 vs 749.9 img/s, B=1 frozen p50 5.335 vs 5.363 ms.
+# HV_DIRECT_STEM=0 restores the GEMM path.
+_DIRECT_STEM = os.environ.get("HV_DIRECT_STEM", "1") == "1"
 
 
 class ConvMHCLayer(nn.Module):
