@@ -220,23 +220,24 @@ int hv_conv3x3_c32(const hv_gemm_desc& d, hipStream_t s) {
 
 namespace {
 
-// bf16 stem on the matrix cores: the workgroup stages the input rows of a 2 x 64 output-pixel
-// tile ((2-1)*s+3 rows x (64-1)*s+3 columns x 3 channels, rounded to bf16) in LDS with
+// bf16 stem on the matrix cores: the workgroup stages the input rows of a TOH x 64 output-pixel
+// tile ((TOH-1)*s+3 rows x (64-1)*s+3 columns x 3 channels, rounded to bf16) in LDS with
 // coalesced row loads, then each wave runs the whole 27(->32)-deep contraction of 16 pixels x
 // 16 channels as ONE 16x16x32 MFMA: the B fragment is the pixel's 8 taps k = 8g..8g+7 (k order
 // kh, kw, cin as the weights; k >= 27 zero) gathered from LDS through a per-lane offset table,
 // the A fragments (weights) stay in registers.  Same instruction, operands and k order as the
 // implicit-GEMM path's single K-step, so the outputs match it; the NHWC and NCHW inputs give
 // the same values.  Lane (pixel fr, group g) ends with 4 consecutive channels -> 8-B stores.
-constexpr int STM_TOH = 2, STM_TOW = 64;
-constexpr int STM_IH = (STM_TOH - 1) * 2 + 3, STM_IW = (STM_TOW - 1) * 2 + 3;   // stride <= 2
+// TOH output rows per workgroup: 8 for big batches (the stride-2 window re-reads 1/8 of its
+// rows instead of 1/2 at 2 rows), 2 when 8 would leave CUs idle (B=1: 200 workgroups)
+constexpr int STM_TOW = 64, STM_IW = (STM_TOW - 1) * 2 + 3;   // stride <= 2
 
-template <int COUT, typename TI, bool NHWC>
+template <int COUT, typename TI, bool NHWC, int STM_TOH>
 __global__ void __launch_bounds__(256) k_conv_stem_mfma(const TI* __restrict__ x, int n, int h, int w, int oh,
                                                         int ow, int stride, int pad, const unsigned short* __restrict__ wt,
                                                         int ldw, const float* scale, const float* bias, int act,
                                                         unsigned short* __restrict__ y, int tiles_x, int tiles_y) {
-  constexpr int NT = COUT / 16;
+  constexpr int NT = COUT / 16, STM_IH = (STM_TOH - 1) * 2 + 3;
   __shared__ float xs[kStemCin][STM_IH][STM_IW];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
@@ -298,9 +299,9 @@ __global__ void __launch_bounds__(256) k_conv_stem_mfma(const TI* __restrict__ x
     }
   __syncthreads();
   const float* xf = &xs[0][0][0];
-  // 128 pixels = 8 groups of 16; wave wv takes groups wv and wv + 4
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  // STM_TOH * 64 pixels = groups of 16; wave wv takes groups wv, wv + 4, ...
+#pragma unroll 2
+  for (int q = 0; q < STM_TOH * STM_TOW / 64; ++q) {
     const int p = (wv + 4 * q) * 16 + fr;             // pixel within the tile (B column = fr)
     const int py = p / STM_TOW, px = p % STM_TOW;
     const int base = py * stride * STM_IW + px * stride;
@@ -333,16 +334,21 @@ void launch_stem(const void* x, int x_nhwc, int n, int h, int w, int oh, int ow,
                  int ldw, const float* scale, const float* bias, int act, void* y, unsigned grid, hipStream_t s) {
   if constexpr (std::is_same<T, unsigned short>::value) {
     if (stride <= 2) {                                  // the MFMA kernel (bf16)
-      const int tiles_x = hv_cdiv(ow, STM_TOW), tiles_y = hv_cdiv(oh, STM_TOH);
+      const int tiles_x = hv_cdiv(ow, STM_TOW);
+      const bool tall = (long)n * tiles_x * hv_cdiv(oh, 8) >= 1024;
+      const int tiles_y = hv_cdiv(oh, tall ? 8 : 2);
       const unsigned g2 = (unsigned)((long)n * tiles_x * tiles_y);
-      if (x_nhwc)
-        k_conv_stem_mfma<COUT, unsigned short, true><<<g2, 256, 0, s>>>(
-            (const unsigned short*)x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt, ldw, scale, bias, act,
-            (unsigned short*)y, tiles_x, tiles_y);
-      else
-        k_conv_stem_mfma<COUT, float, false><<<g2, 256, 0, s>>>(
-            (const float*)x, n, h, w, oh, ow, stride, pad, (const unsigned short*)wt, ldw, scale, bias, act,
-            (unsigned short*)y, tiles_x, tiles_y);
+      auto us = (const unsigned short*)wt;
+      auto yo = (unsigned short*)y;
+      if (x_nhwc) {
+        auto xi = (const unsigned short*)x;
+        if (tall) k_conv_stem_mfma<COUT, unsigned short, true, 8><<<g2, 256, 0, s>>>(xi, n, h, w, oh, ow, stride, pad, us, ldw, scale, bias, act, yo, tiles_x, tiles_y);
+        else k_conv_stem_mfma<COUT, unsigned short, true, 2><<<g2, 256, 0, s>>>(xi, n, h, w, oh, ow, stride, pad, us, ldw, scale, bias, act, yo, tiles_x, tiles_y);
+      } else {
+        auto xi = (const float*)x;
+        if (tall) k_conv_stem_mfma<COUT, float, false, 8><<<g2, 256, 0, s>>>(xi, n, h, w, oh, ow, stride, pad, us, ldw, scale, bias, act, yo, tiles_x, tiles_y);
+        else k_conv_stem_mfma<COUT, float, false, 2><<<g2, 256, 0, s>>>(xi, n, h, w, oh, ow, stride, pad, us, ldw, scale, bias, act, yo, tiles_x, tiles_y);
+      }
       return;
     }
   }
