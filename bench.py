@@ -57,7 +57,7 @@ def parse():
                     help="time host-launched steps instead of HIP-graph replays")
     ap.add_argument("--train", dest="train", action="store_true", default=None,
                     help="also time the training step (config C: base 640, bf16, DDP over RCCL when N>1); "
-                         "default: on at N=1, off at N>1")
+                         "default: on (every N)")
     ap.add_argument("--no-train", dest="train", action="store_false")
     ap.add_argument("--train-batch", type=int, default=16)
     ap.add_argument("--train-steps", type=int, default=4)
@@ -299,10 +299,10 @@ def main():
         sys.exit(launch_ranks(a.gpus))
     if a.dry_run:
         return dry_run(a, world, rank)
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)                 # the device first: RCCL binds the rank to it
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
 
     from hv_amd import HybridVisionSystem, ops
     torch.manual_seed(0)
@@ -401,7 +401,7 @@ def main():
                                "workload": "hybrid_vision base 1024x1024 inference (hipGraph replay), 20 Sinkhorn iters"}}
 
     train = None
-    if a.train if a.train is not None else True:
+    if a.train is not False:
         train = train_bench(a, dev, world, rank, a.size, a.train_batch, a.train_steps,
                             2095.9 if a.size == 640 else None)
         if large is not None:

@@ -337,18 +337,6 @@ int launch_typed(const hv_gemm_desc& d, hipStream_t s) {
 
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s);   // hv_gemm_glds.hip
 
-static std::atomic<int> g_big_tile{1};   // 256x256 ping-pong LDS-DMA kernel: 0 off, 1 by shape (default), 2 always
-int hv_gemm_big_tile_mode() { return g_big_tile.load(std::memory_order_relaxed); }
-static std::atomic<int> g_small_tile{1}; // 64x64 LDS-DMA tiles for small grids: 1 on (default), 0 off (A/B tests)
-int hv_gemm_small_tile_mode() { return g_small_tile.load(std::memory_order_relaxed); }
-extern "C" void hv_gemm_set_small_tile(int mode) { g_small_tile = mode; }
-extern "C" void hv_gemm_set_big_tile(int mode) { g_big_tile = mode; }
-
-static std::atomic<int> g_force_regstage{0};
-static int hv_gemm_force_regstage() { return g_force_regstage.load(std::memory_order_relaxed); }
-// 1: route every GEMM through the register-staged kernel (A/B testing of the two paths)
-extern "C" void hv_gemm_set_path(int regstage_only) { g_force_regstage = regstage_only; }
-
 int hv_conv3x3_c32(const hv_gemm_desc& d, hipStream_t s);   // hv_stem.hip
 
 extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
@@ -368,7 +356,7 @@ extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (d.ldb % epc) return HV_EUNSUPPORTED;
   if (((uintptr_t)d.A | (uintptr_t)d.B) & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  if (!hv_gemm_force_regstage()) {
+  if (!(d.variant & HV_GV_REGSTAGE)) {
     if (d.conv_k == 3 && d.conv_c == 32) {               // halo-tiled 3x3 conv, Cin = 32 (hv_stem.hip)
       const int rc = hv_conv3x3_c32(d, s);
       if (rc != HV_EUNSUPPORTED) return rc;

@@ -501,8 +501,8 @@ int launch_splitk(const hv_gemm_desc& d, hipStream_t s) {
   return HV_OK;
 }
 
-std::atomic<int> g_staged_train{1};   // LDS-staged epilogue for the training modes (A/B knob)
-std::atomic<int> g_staged_epi{1};             // LDS-staged coalesced epilogue in the 64/128 tiles (A/B knob): +25-35 % at K <= 512
+// LDS-staged epilogues (inference: +25-35 % at K <= 512; training modes too) unless the call
+// asks for the fragment-layout one (HV_GV_FLAT_EPI / HV_GV_FLAT_TRAIN)
 
 int launch256(const hv_gemm_desc& d, hipStream_t s) {
   const unsigned grid = hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
@@ -519,7 +519,6 @@ int launch256(const hv_gemm_desc& d, hipStream_t s) {
 // with one tile in flight (64x64: 4 buffers = 64 KiB, 64x128 / 128x64: 3 = 72 KiB)
 template <int BM, int BN>
 constexpr int deep_stages() { return BM * BN <= 64 * 64 ? 4 : (BM * BN <= 128 * 64 ? 3 : 2); }
-std::atomic<int> g_deep{1};                   // deeper LDS-DMA rings for the small tiles (A/B knob)
 
 template <int BM, int BN, int NS>
 int launch_ns(const hv_gemm_desc& d, hipStream_t s) {
@@ -527,14 +526,14 @@ int launch_ns(const hv_gemm_desc& d, hipStream_t s) {
   hv_diag_count(BM == 128 && BN == 128 ? HV_KF_GEMM_GLDS_128x128 : BM == 64 && BN == 128 ? HV_KF_GEMM_GLDS_64x128
                 : BM == 128 ? HV_KF_GEMM_GLDS_128x64 : HV_KF_GEMM_GLDS_64x64);
   if (d.epi_mode) {
-    if (g_staged_train) {
+    if (!(d.variant & HV_GV_FLAT_TRAIN)) {
       if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, true, NS><<<grid, 256, 0, s>>>(d);
       else gemm_glds_kernel<BM, BN, false, true, true, NS><<<grid, 256, 0, s>>>(d);
     } else {
       if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, true, false, NS><<<grid, 256, 0, s>>>(d);
       else gemm_glds_kernel<BM, BN, false, true, false, NS><<<grid, 256, 0, s>>>(d);
     }
-  } else if (g_staged_epi) {
+  } else if (!(d.variant & HV_GV_FLAT_EPI)) {
     if (d.conv_k > 0) gemm_glds_kernel<BM, BN, true, false, true, NS><<<grid, 256, 0, s>>>(d);
     else gemm_glds_kernel<BM, BN, false, false, true, NS><<<grid, 256, 0, s>>>(d);
   } else {
@@ -551,32 +550,24 @@ int launch(const hv_gemm_desc& d, hipStream_t s) {
   if constexpr (NS > 2) {
     // inference epilogues only: with the training epilogues (more VGPRs, fewer resident
     // workgroups) the deeper ring measured slower (train step 183.7 vs 176.0 ms)
-    if (g_deep && !d.epi_mode) return launch_ns<BM, BN, NS>(d, s);
+    if (!(d.variant & HV_GV_SHALLOW) && !d.epi_mode) return launch_ns<BM, BN, NS>(d, s);
   }
   return launch_ns<BM, BN, 2>(d, s);
 }
 
 }  // namespace
 
-int hv_gemm_big_tile_mode();   // hv_gemm.hip
 int hv_gemm_smallk(const hv_gemm_desc& d, hipStream_t s, bool force);   // hv_gemm_sk.hip
-int hv_gemm_small_tile_mode();  // hv_gemm.hip
-std::atomic<int> g_train128{0};             // 128x128 tiles for the training epilogues: measured slower (199 vs 182 ms/step), off
-extern "C" void hv_gemm_set_train128(int on) { g_train128 = on; }
-extern "C" void hv_gemm_set_staged_epilogue(int on) { g_staged_epi = on; }
-extern "C" void hv_gemm_set_staged_train(int on) { g_staged_train = on; }
-extern "C" void hv_gemm_set_deep_ring(int on) { g_deep = on; }
-std::atomic<int> g_force_tile{0};         // A/B: 0 auto, 1 128x128, 2 64x128, 3 128x64, 4 64x64, 5 256x256, 6 small-K
-extern "C" void hv_gemm_set_force_tile(int code) { g_force_tile = code; }
-std::atomic<int> g_conv_ktail{0};            // LDS-DMA kernel for convs with K % 64 != 0: in-model A/B slower (23.73 vs 23.59 ms), off
-extern "C" void hv_gemm_set_conv_ktail(int on) { g_conv_ktail = on; }
+// Per-call variants (hv_gemm_desc.variant, HV_GV_*): measured-off choices stay selectable for the
+// A/B tools -- 128x128 training tiles (199 vs 182 ms/step), the LDS-DMA kernel for convs with
+// K % 64 != 0 (in-model 23.73 vs 23.59 ms).
 
 // Returns HV_EUNSUPPORTED when the shape/mode is not covered (caller falls back).
 int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // K % 64 != 0 only for convolutions (channels a multiple of 8): the last K-tile's tail reads the
   // zero line for both operands (e.g. 3x3 convs with 32 input channels, K = 288)
   if (d.dtype != HV_BF16 || d.conv_transposed) return HV_EUNSUPPORTED;
-  if (d.K % 64 && !(g_conv_ktail && d.conv_k > 0 && d.K % 8 == 0)) return HV_EUNSUPPORTED;
+  if (d.K % 64 && !((d.variant & HV_GV_CONV_KTAIL) && d.conv_k > 0 && d.K % 8 == 0)) return HV_EUNSUPPORTED;
   if (d.a_mean && (!d.b_colsum || d.A2 || d.conv_k > 0)) return HV_EUNSUPPORTED;
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
@@ -591,7 +582,7 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   }
   const long t128 = (long)hv_cdiv(d.M, 128) * hv_cdiv(d.N, 128);
   const long t256 = (long)hv_cdiv(d.M, 256) * hv_cdiv(d.N, 256);
-  switch (g_force_tile.load(std::memory_order_relaxed)) {
+  switch (d.variant & HV_GV_TILE_MASK) {
     case 1: return launch<128, 128>(d, s);
     case 2: return launch<64, 128>(d, s);
     case 3: return launch<128, 64>(d, s);
@@ -608,13 +599,13 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
   // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for
   // the implicit-im2col convolutions (+3..29 %); K = 256 loses everywhere (prologue-bound)
-  if (!d.epi_mode && d.K % 64 == 0 && (hv_gemm_big_tile_mode() == 2 ||
-                      (hv_gemm_big_tile_mode() == 1 && d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
+  if (!d.epi_mode && d.K % 64 == 0 && !(d.variant & HV_GV_NO_BIG) &&
+      ((d.variant & HV_GV_BIG_ALWAYS) || (d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
   // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs
   const long t64x128 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 128);
-  if (hv_gemm_small_tile_mode() && t64x128 < 320) return launch<64, 64>(d, s);
-  if (d.M <= 64 || t128 < 256 || (d.epi_mode && !g_train128)) return launch<64, 128>(d, s);
+  if (!(d.variant & HV_GV_NO_SMALL) && t64x128 < 320) return launch<64, 64>(d, s);
+  if (d.M <= 64 || t128 < 256 || (d.epi_mode && !(d.variant & HV_GV_TRAIN128))) return launch<64, 128>(d, s);
   return launch<128, 128>(d, s);
 }

@@ -50,7 +50,7 @@ __device__ __forceinline__ int sk_tile(int round, int ntiles) {
   return base + bid < ntiles ? (int)(base + bid) : -1;
 }
 
-// DIAG (hv_gemm_set_smallk 2 / 3, tools/k256_probe2.py only): 1 = skip the stores, 2 = skip the
+// DIAG (variant HV_GV_SK_DIAG1 / 2, tools/k256_probe2.py only): 1 = skip the stores, 2 = skip the
 // k-loop (DMA + MFMA) -- the two halves of a tile's time, measured apart.  0 in the product.
 template <bool LN, int DIAG = 0>
 __global__ void __launch_bounds__(256, 2) gemm_sk_kernel(const hv_gemm_desc d, int ntiles) {
@@ -267,17 +267,14 @@ __global__ void __launch_bounds__(256, 2) gemm_sk_kernel(const hv_gemm_desc d, i
   }
 }
 
-std::atomic<int> g_sk_on{1};     // persistent small-K kernel (A/B knob hv_gemm_set_smallk)
 std::atomic<int> g_cus{0};
 
 }  // namespace
 
-extern "C" void hv_gemm_set_smallk(int on) { g_sk_on = on; }
-
 // Returns HV_EUNSUPPORTED when the shape/mode is not this kernel's (the caller falls back).
-// force (hv_gemm_set_force_tile(6), tests): any supported shape, even below one round of tiles.
+// force (variant tile code 6, tests): any supported shape, even below one round of tiles.
 int hv_gemm_smallk(const hv_gemm_desc& d0, hipStream_t s, bool force) {
-  if (!force && !g_sk_on.load(std::memory_order_relaxed)) return HV_EUNSUPPORTED;
+  if (!force && (d0.variant & HV_GV_NO_SMALLK)) return HV_EUNSUPPORTED;
   hv_gemm_desc d = d0;
   // a 1x1 stride-1 unpadded convolution is the plain GEMM over the NHWC pixel rows
   if (d.conv_k == 1 && d.conv_stride == 1 && d.conv_pad == 0 && !d.conv_transposed) {
@@ -300,9 +297,8 @@ int hv_gemm_smallk(const hv_gemm_desc& d0, hipStream_t s, bool force) {
   if (!force && ntiles < 2L * cus) return HV_EUNSUPPORTED;   // under one persistent round: nothing to overlap
   const int grid = (int)(ntiles < 2L * cus ? ntiles : 2L * cus);
   hv_diag_count(HV_KF_GEMM_SMALLK);
-  const int mode = g_sk_on.load(std::memory_order_relaxed);
-  if (mode == 2) gemm_sk_kernel<false, 1><<<grid, 256, 0, s>>>(d, (int)ntiles);
-  else if (mode == 3) gemm_sk_kernel<false, 2><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  if (d.variant & HV_GV_SK_DIAG1) gemm_sk_kernel<false, 1><<<grid, 256, 0, s>>>(d, (int)ntiles);
+  else if (d.variant & HV_GV_SK_DIAG2) gemm_sk_kernel<false, 2><<<grid, 256, 0, s>>>(d, (int)ntiles);
   else if (d.a_mean) gemm_sk_kernel<true><<<grid, 256, 0, s>>>(d, (int)ntiles);
   else gemm_sk_kernel<false><<<grid, 256, 0, s>>>(d, (int)ntiles);
   HV_CHECK_LAUNCH();

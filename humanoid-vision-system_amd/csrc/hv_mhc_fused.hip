@@ -668,7 +668,6 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
   }
 }
 
-std::atomic<int> g_ablate2{0};   // diagnostic (tools/mhc_ab.py): 1 no weight DMA, 2 no GEMM2, 4 no GEMM1, 8 no GEMM3
 template <int D, int HD, int NG>
 int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
   using C = Cfg2<D, HD, NG>;
@@ -682,30 +681,23 @@ int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
   k<<<hv_cdiv(a->T, C::TOK), C::NT, C::LDS, s>>>(
       (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
       a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
-      (unsigned short*)a->out, g_ablate2.load(std::memory_order_relaxed));
+      (unsigned short*)a->out, a->variant >> HV_MV_ABLATE_SHIFT);   // diagnostics only (tools/mhc_ablate*.py)
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
-std::atomic<int> g_fused_wide{0};
-std::atomic<int> g_variant{0};
-
 }  // namespace
 
-extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype) {
+extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant) {
   if (dtype != HV_BF16) return 0;
   return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
-         (D == 256 && Hd == 512 && g_fused_wide);
+         (D == 256 && Hd == 512 && (variant & HV_MV_WIDE));
 }
-extern "C" void hv_mhc_fused_enable_wide(int on) { g_fused_wide = on; }
-extern "C" void hv_mhc_fused_set_ablate(int a) { g_ablate2 = a; }
-// tuning knob (tools/mhc_ab.py): 0 = default, 1 = three 4-wave groups per CU, 2 = one 8-wave group,
-// 5 = (D = 128) the per-wave 4-wave kernel instead of the split-hidden one
-extern "C" void hv_mhc_fused_set_variant(int v) { g_variant = v; }
 
 extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   if (!a || a->T <= 0) return HV_EINVAL;
-  if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype)) return HV_EUNSUPPORTED;
+  if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype, a->variant)) return HV_EUNSUPPORTED;
+  const int shape = a->variant & HV_MV_SHAPE_MASK;
   const uintptr_t al = (uintptr_t)a->x | (uintptr_t)a->a1t | (uintptr_t)a->w2 | (uintptr_t)a->wct |
                        (uintptr_t)a->out | (uintptr_t)a->c1 | (uintptr_t)a->b2 | (uintptr_t)a->g_post |
                        (uintptr_t)a->b_post | (uintptr_t)a->residual;
@@ -718,25 +710,25 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   // groups per CU (register cap 170): 2x slower.  Also measured slower: 1.5x tokens per wave
   // (TB 6 / 3, 35-60%) and 2-wave groups (4x) -- all register spills.
   if (a->D == 32) {
-    if (g_variant == 1) return launch<32, 128, 4, 3, 4>(a, s);
-    if (g_variant == 2) return launch<32, 128, 4, 1>(a, s);
+    if (shape == 1) return launch<32, 128, 4, 3, 4>(a, s);
+    if (shape == 2) return launch<32, 128, 4, 1>(a, s);
     return launch<32, 128, 4, 2, 4>(a, s);
   }
   if (a->D == 64) {
-    if (g_variant == 1) return launch<64, 256, 2, 3, 4>(a, s);
-    if (g_variant == 2) return launch<64, 256, 2, 1>(a, s);
+    if (shape == 1) return launch<64, 256, 2, 3, 4>(a, s);
+    if (shape == 2) return launch<64, 256, 2, 1>(a, s);
     return launch<64, 256, 2, 2, 4>(a, s);
   }
   if (a->D == 128) {
     // default: the split-hidden kernel (hidden dimension across 4 waves, 2 token groups per
     // workgroup) -- tools/mhc_ab.py: 0.306 vs 0.329 ms at T = 102400, 0.073 vs 0.088 at 25600;
     // variant 5 = the per-wave 4-wave kernel, 2 = per-wave 8-wave
-    if (g_variant == 2) return launch<128, 512, 1, 1>(a, s);
-    if (g_variant == 5) return launch<128, 512, 1, 2, 4>(a, s);
+    if (shape == 2) return launch<128, 512, 1, 1>(a, s);
+    if (shape == 5) return launch<128, 512, 1, 2, 4>(a, s);
     return launch2<128, 512, 2>(a, s);
   }
   // D=256 (ViT, off by default): at T=6416 / 25600 the unfused chain wins (65 / 150 us vs
   // 94 / 139 us fused, tools/mhc_ab.py); 8-wave groups here, variant 1 = 4-wave
-  if (g_variant == 1) return launch<256, 512, 1, 1, 4>(a, s);
+  if (shape == 1) return launch<256, 512, 1, 1, 4>(a, s);
   return launch<256, 512, 1, 1>(a, s);
 }

@@ -13,6 +13,12 @@ import threading
 import torch  # noqa: F401  (must be loaded first: HIP runtime shared by soname)
 
 HV_F32, HV_BF16 = 0, 1
+# per-call kernel variants (include/hv_kernels.h HV_GV_* / HV_MV_*): 0 = automatic
+GV_TILE_128x128, GV_TILE_64x128, GV_TILE_128x64, GV_TILE_64x64, GV_TILE_256, GV_TILE_SMALLK = 1, 2, 3, 4, 5, 6
+GV_REGSTAGE, GV_NO_BIG, GV_BIG_ALWAYS, GV_NO_SMALL = 0x8, 0x10, 0x20, 0x40
+GV_TRAIN128, GV_FLAT_EPI, GV_FLAT_TRAIN, GV_SHALLOW = 0x80, 0x100, 0x200, 0x400
+GV_CONV_KTAIL, GV_NO_SMALLK, GV_SK_DIAG1, GV_SK_DIAG2 = 0x800, 0x1000, 0x2000, 0x4000
+MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_SHIFT = 1, 2, 5, 6, 0x100, 16
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
 _LIB = None
@@ -47,7 +53,7 @@ class GemmDesc(C.Structure):
                 ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
                 ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp),
                 ("aux", vp), ("ld_aux", i64), ("aux_dtype", i32), ("epi_mode", i32),
-                ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("pad1_", i32),
+                ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("variant", i32),
                 ("splitk_work", vp), ("splitk_count", vp), ("splitk", i32), ("pad2_", i32)]
 
 
@@ -80,7 +86,7 @@ class ParamEntry(C.Structure):
 class MhcFusedArgs(C.Structure):
     _fields_ = [("dtype", i32), ("D", i32), ("Hd", i32), ("T", i32),
                 ("x", vp), ("a1t", vp), ("c1", vp), ("w2", vp), ("b2", vp), ("wct", vp),
-                ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp)]
+                ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp), ("variant", i32), ("pad_", i32)]
 
 
 class SymeigEntry(C.Structure):
@@ -106,10 +112,8 @@ _SIGS = {
     "hv_mhc_prep_group": ([vp, i32, i32, vp, vp], i32),
     "hv_wprep_blocks": ([i32, i64, i32, i32], i32),
     "hv_wprep_group": ([vp, i32, i32, vp], i32),
-    "hv_mhc_fused_supported": ([i32, i32, i32], i32),
+    "hv_mhc_fused_supported": ([i32, i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
-    "hv_mhc_fused_enable_wide": ([i32], None),
-    "hv_mhc_fused_set_variant": ([i32], None),
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),
@@ -122,16 +126,6 @@ _SIGS = {
     "hv_sinkhorn_group_forward": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "hv_sinkhorn_group_forward_part": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
     "hv_gemm": ([vp, vp], i32),
-    "hv_gemm_set_path": ([i32], None),
-    "hv_gemm_set_big_tile": ([i32], None),
-    "hv_gemm_set_small_tile": ([i32], None),
-    "hv_gemm_set_train128": ([i32], None),
-    "hv_gemm_set_staged_epilogue": ([i32], None),
-    "hv_gemm_set_deep_ring": ([i32], None),
-    "hv_gemm_set_conv_ktail": ([i32], None),
-    "hv_gemm_set_smallk": ([i32], None),
-    "hv_gemm_set_force_tile": ([i32], None),
-    "hv_gemm_set_staged_train": ([i32], None),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),
     "hv_layernorm": ([i32, vp, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp], i32),
     "hv_rmsnorm": ([i32, vp, i32, i32, f32, vp, vp, vp], i32),

@@ -6,7 +6,6 @@ matrix the mHC layer consumes, so the reference's permute/reshape round trips
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -15,13 +14,12 @@ import torch.nn as nn
 from . import ops
 from .layers import conv_prep, ctx_scope, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection
-from .runtime import current, require_cuda, resolve_dtype
+from .runtime import current, options, require_cuda, resolve_dtype
 
 # Direct stem conv (hv_conv_stem: bf16 = LDS-staged input tile + one MFMA k-step per 16 pixels)
 # instead of the NCHW->NHWC pass + implicit GEMM (237 us at B=16 640^2).  Same-box A/B
 # (profiles/r02/stem_direct_ab.txt): 759.5 vs 749.9 img/s, B=1 frozen p50 5.335 vs 5.363 ms.
-# HV_DIRECT_STEM=0 restores the GEMM path.
-_DIRECT_STEM = os.environ.get("HV_DIRECT_STEM", "1") == "1"
+# HVOptions(direct_stem=False) restores the GEMM path.
 
 
 class ConvMHCLayer(nn.Module):
@@ -187,7 +185,7 @@ class HybridVisionBackbone(nn.Module):
         stem kernel (falls back to the NHWC conversion + implicit GEMM when not applicable)."""
         layers = list(self.stem)[:3]
         dt = current().dtype
-        if image is not None and not _DIRECT_STEM:
+        if image is not None and not options().direct_stem:
             x, image = to_nhwc(image, dt), None
         if image is not None:
             y = layers[0].forward_image(image, dt)
@@ -197,7 +195,7 @@ class HybridVisionBackbone(nn.Module):
         else:
             # NHWC input (the engine's preprocessed frame): the same direct stem kernel, so both
             # input layouts give identical results
-            y = layers[0].forward_image(x, dt, nhwc=True) if x.shape[-1] == 3 and _DIRECT_STEM else None
+            y = layers[0].forward_image(x, dt, nhwc=True) if x.shape[-1] == 3 and options().direct_stem else None
             if y is not None:
                 x, layers = y, layers[1:]
         for i, lyr in enumerate(layers):

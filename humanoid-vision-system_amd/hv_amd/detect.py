@@ -3,7 +3,6 @@
 from __future__ import annotations
 
 import math
-import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -14,12 +13,11 @@ from . import ops
 from .backbone import HybridVisionBackbone
 from .layers import ctx_scope, linear_prep, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection, prepare_plans
-from .runtime import RunCtx, VersionWatch, current, require_cuda, use_ctx, PRECISIONS
+from .runtime import HVOptions, RunCtx, VersionWatch, current, module_options, require_cuda, use_ctx, PRECISIONS
 from .vit import HybridVisionEncoder
 
-# side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HV_PREP_OVERLAP=1); on one
-# box, interleaved runs measured it 0.1 ms/step SLOWER in graph and eager mode
-_PREP_OVERLAP = os.environ.get("HV_PREP_OVERLAP", "0") == "1"
+# side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HVOptions.prep_overlap); on
+# one box, interleaved runs measured it 0.1 ms/step SLOWER in graph and eager mode
 
 # outputs['detections'] keys: the per-scale names DetectionPostprocessor (postprocessing.py:
 # 234-244, 270-281) and MHCYOLOLoss (loss_functions.py:86) look up
@@ -295,12 +293,13 @@ class GraphRunner:
     HIP runtime).  Every kernel of the step -- grouped Sinkhorn, coefficient folds, the token
     path, decode -- is recorded once and replayed with no host launch overhead.
 
-    Staleness: the graph bakes in parameter storage (and, with the model frozen, the prepared
-    coefficients).  Every call snapshots the parameters' / input buffers' storage pointers and
-    version counters (runtime.VersionWatch) AFTER enqueueing the replay -- the ~0.4 ms host
-    check overlaps the GPU step -- and when anything changed (an optimizer step,
-    load_state_dict, a `.data` swap) it re-captures and replays again before returning, so a
-    result never comes from stale weights.
+    Staleness: the graph bakes in parameter storage, the storage of the buffers it writes
+    (Sinkhorn histories) and, with the model frozen, the prepared coefficients.  Every call
+    snapshots the parameters' / buffers' storage pointers and version counters
+    (runtime.VersionWatch) BEFORE enqueueing the replay -- a replay after a `.data` swap or a
+    buffer rebind would read or write freed storage -- and when anything changed (an optimizer
+    step, load_state_dict, a `.data` swap, `.to()`, HVTrainer's flat buffers) it re-captures
+    first.  In a replay loop the ~0.4 ms host check still overlaps the previous step on the GPU.
 
     Ownership: replay() returns the captured static outputs, overwritten by the next replay;
     __call__(x, owned=True) returns fresh copies (one segmented-copy launch)."""
@@ -329,11 +328,10 @@ class GraphRunner:
         self.version = model._watch.snapshot()
 
     def replay(self) -> Dict[str, Any]:
-        self.graph.replay()
         if self.model._watch.snapshot() != self.version:
             self.recaptures += 1
             self._capture()
-            self.graph.replay()
+        self.graph.replay()
         return self.static_out
 
     def __call__(self, x: torch.Tensor, owned: bool = False) -> Dict[str, Any]:
@@ -408,6 +406,16 @@ class HybridVisionSystem(nn.Module):
         self._frozen = None
         return self
 
+    def set_options(self, options: Optional[HVOptions] = None, **kw) -> "HybridVisionSystem":
+        """Per-model execution options (runtime.HVOptions: kernel variants, exact restructurings);
+        e.g. ``model.set_options(use_fused_mhc=False)``.  Prepared / frozen state is rebuilt; a
+        captured GraphRunner keeps the options it was captured with."""
+        base = options if options is not None else module_options(self)
+        self.hv_options = base.replace(**kw) if kw else base
+        self._frozen = None if self._frozen is None else (None, None)
+        self._sk_cache = {}
+        return self
+
     def freeze(self, enabled: bool = True) -> "HybridVisionSystem":
         """Eval/streaming: keep the prepared coefficients (Sinkhorn, folds, BN folds, casts)
         across forwards until any parameter changes (version counters are checked)."""
@@ -415,9 +423,10 @@ class HybridVisionSystem(nn.Module):
         return self
 
     def _make_ctx(self) -> RunCtx:
-        ctx = RunCtx(dtype=PRECISIONS[self.hv_precision])
+        opts = module_options(self)
+        ctx = RunCtx(dtype=PRECISIONS[self.hv_precision], opts=opts)
         key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=_PREP_OVERLAP, groups=self._qkv_groups)
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=opts.prep_overlap, groups=self._qkv_groups)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":

@@ -377,14 +377,12 @@ class StreamingPipeline:
         """uint8 HWC BGR frame -> {'boxes' [k, 4] xyxy normalised, 'scores' [k], 'labels' [k]}."""
         if frame.shape != (*self.frame_hw, 3) or frame.dtype != np.uint8:
             raise ValueError(f"expected a uint8 {self.frame_hw + (3,)} frame")
+        if self.model._watch.snapshot() != self.version:   # before any replay: no stale storage
+            self.recaptures += 1
+            self._capture()
         self.staging[0].numpy()[...] = frame
         self.frame.copy_(self.staging, non_blocking=True)
         self.graph.replay()
-        if self.model._watch.snapshot() != self.version:
-            self.recaptures += 1
-            self._capture()
-            self.frame.copy_(self.staging, non_blocking=True)
-            self.graph.replay()
         self.nms_graph.replay()
         boxes, scores, labels, count = self.dets
         self.host["count"].copy_(count, non_blocking=True)

@@ -7,7 +7,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .runtime import RunCtx, current, resolve_dtype
+from .runtime import RunCtx, current, module_options, resolve_dtype
 
 
 def conv_prep(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], dtype: torch.dtype, owner: nn.Module):
@@ -88,7 +88,7 @@ class ctx_scope:
         c = current()
         if c is not None:
             return c
-        self.own = use_ctx(RunCtx(dtype=resolve_dtype(self.module)))
+        self.own = use_ctx(RunCtx(dtype=resolve_dtype(self.module), opts=module_options(self.module)))
         return self.own.__enter__()
 
     def __exit__(self, *exc):

@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .runtime import RunCtx, current, require_cuda, resolve_dtype, use_ctx
+from .runtime import RunCtx, current, module_options, options, require_cuda, resolve_dtype, use_ctx
 
 
 # ================================================================== stability monitor queue
@@ -98,8 +98,8 @@ class SinkhornKnoppProjection(nn.Module):
 
 
 # ================================================================== mHC plan
-FOLD_MAX_D = 1024   # fold H_pre into W1 for every site but the D=1792 final fusion
-USE_FUSED = True    # one-launch kernel for the small-D sites (hv_mhc_fused); False = unfused chain
+# HVOptions.fold_max_d (default 1024): fold H_pre into W1 for every site but the D=1792 final
+# fusion; HVOptions.use_fused_mhc: one-launch kernel for the small-D sites (hv_mhc_fused)
 
 
 @dataclass
@@ -120,11 +120,12 @@ class MhcPlan:
     cs: Optional[torch.Tensor] = None   # row sums of b1 as stored: LayerNorm applied after GEMM1
 
 
-def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.dtype) -> MhcPlan:
+def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.dtype,
+               fold_max_d: int = 1024) -> MhcPlan:
     """Per-site coefficient prep (about ten launches per site).  The forward uses the grouped
     prep.PrepProgram; this path is kept as its independent cross-check (tests/test_gpu_prep.py)."""
     D, Hd = m.input_dim, m.hidden_dim
-    fold = D <= FOLD_MAX_D and Hd % 32 == 0
+    fold = D <= fold_max_d and Hd % 32 == 0
     gc, u, wct = ops.mhc_prep(m.H_pre_raw, m.H_post_raw, h_res, m.norm_pre.weight, m.norm_pre.bias,
                               gc_transposed=not fold)
     w1 = ops.f32(m.mlp[0].weight)
@@ -144,7 +145,7 @@ def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.d
 
 def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token chain on x2 [T, D] (compute dtype).  Returns LN_post(...) (+ residual) [T, D]."""
-    if (USE_FUSED and p.fold and x2.is_contiguous() and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)
+    if (options().use_fused_mhc and p.fold and x2.is_contiguous() and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)
             and (residual is None or residual.dtype == x2.dtype)):
         return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post, residual)
     mean, rstd = ops.row_stats(x2, 1e-5)
@@ -168,12 +169,13 @@ def prepare_plans(mods, ctx: RunCtx, cache: Optional[dict] = None, key=None, ove
     if not mods:
         return
     prog = None
-    if cache is not None and cache.get("key") == (key, ctx.dtype, FOLD_MAX_D):
+    fmd = ctx.opts.fold_max_d
+    if cache is not None and cache.get("key") == (key, ctx.dtype, fmd):
         prog = cache["program"]
     if prog is None:
-        prog = PrepProgram(mods, ctx.dtype, mods[0].H_res_raw.device, FOLD_MAX_D, groups)
+        prog = PrepProgram(mods, ctx.dtype, mods[0].H_res_raw.device, fmd, groups)
         if cache is not None:
-            cache["key"], cache["program"] = (key, ctx.dtype, FOLD_MAX_D), prog
+            cache["key"], cache["program"] = (key, ctx.dtype, fmd), prog
     ctx.program = prog
     prog.run(ctx, overlap)
 
@@ -235,7 +237,7 @@ class ManifoldHyperConnection(nn.Module):
                 prepare_plans([self], ctx)
                 p = ctx.plans[id(self)]
             return p
-        own = RunCtx(dtype=resolve_dtype(self))
+        own = RunCtx(dtype=resolve_dtype(self), opts=module_options(self))
         prepare_plans([self], own)
         return own.plans[id(self)]
 
@@ -305,8 +307,8 @@ class ManifoldHyperConnection(nn.Module):
 
 
 # ================================================================== attention / norms
-PARALLEL_QKV = False  # q / k / v on three streams: measured slower (22.30 vs 21.77 ms, tools/ab_vit.py)
-GROUP_QKV = True      # q / k / v GEMM1 as one N = 3*2Hd GEMM (shared LN statistics)
+# HVOptions.parallel_qkv: q / k / v on three streams -- measured slower (22.30 vs 21.77 ms,
+# tools/ab_vit.py); HVOptions.group_qkv: q / k / v GEMM1 as one N = 3*2Hd GEMM (shared LN stats)
 
 
 class MultiHeadManifoldAttention(nn.Module):
@@ -333,16 +335,17 @@ class MultiHeadManifoldAttention(nn.Module):
     def forward_tokens(self, x: torch.Tensor, n: int) -> torch.Tensor:
         """Self-attention on x [n*L, D] (compute dtype); returns out_proj(attn) [n*L, D].
         The q / k / v projections are independent mHC chains of small-M GEMMs (M = n*L, K =
-        256): with PARALLEL_QKV they run on three streams (three branches of a captured
+        256): with HVOptions.parallel_qkv they run on three streams (three branches of a captured
         graph), so their latency-bound launches overlap."""
         L = x.shape[0] // n
         ctx = current()
-        grp = ctx.plans.get(("group", id(self))) if (ctx is not None and GROUP_QKV) else None
+        opts = options()
+        grp = ctx.plans.get(("group", id(self))) if (ctx is not None and opts.group_qkv) else None
         if grp is not None and not self.training:
             q, k, v = (t.view(n, L, -1) for t in self._qkv_grouped(x, grp))
             o = ops.attention(q, k, v, self.num_heads)
             return self.out_proj.forward_tokens(o.view(n * L, -1))
-        if PARALLEL_QKV:
+        if opts.parallel_qkv:
             main = torch.cuda.current_stream()
             if self._side is None:
                 self._side = (torch.cuda.Stream(device=x.device), torch.cuda.Stream(device=x.device))

@@ -8,13 +8,13 @@ sequences are [rows, c].
 from __future__ import annotations
 
 import ctypes as C
-import os
 from typing import Optional
 
 import torch
 
 from . import _lib as L
 from ._lib import check, dtype_code, ptr, stream_ptr
+from .runtime import options
 
 Tensor = torch.Tensor
 
@@ -42,11 +42,10 @@ def _contig(t: Tensor, name: str) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- GEMM
-# Split-K is opt-in (HV_SPLITK=1): measured no gain (profiles/r02/splitk_ab.txt) -- with a
+# Split-K is opt-in (HVOptions.splitk): measured no gain (profiles/r02/splitk_ab.txt) -- with a
 # separate reduce launch the split GEMM + reduce (6.1 + 5.4 us) cost what the un-split kernel
 # does (10.1 us) at B=1; with the reduction fused into the last-arriving workgroup the
 # agent-scope release/acquire (L2 write-back + invalidate on every workgroup) made it 31 us.
-SPLITK_ON = os.environ.get("HV_SPLITK", "0") == "1"
 _SPLITK_COUNTERS: dict = {}
 SPLITK_MAX_TILES = 4096                                      # HV_SPLITK_MAX_TILES
 
@@ -70,7 +69,7 @@ def _splitk(d, M: int, N: int, K: int, dtype: torch.dtype, device) -> Optional[T
     split over `splitk` workgroups (>= 4 K-tiles each); the last workgroup of a tile to finish
     sums the fp32 partials in slice order and runs the epilogue (deterministic).  Returns the workspace
     (kept alive by the caller until the launch is enqueued) or None."""
-    if not SPLITK_ON or dtype != torch.bfloat16 or K % 64:
+    if not options().splitk or dtype != torch.bfloat16 or K % 64:
         return None
     tiles = -(-M // 64) * -(-N // 64)
     if tiles >= 192:
@@ -87,12 +86,15 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
          act: str = "none", alpha: float = 1.0, residual: Optional[Tensor] = None,
          a_mean: Optional[Tensor] = None, a_rstd: Optional[Tensor] = None,
          a2: Optional[Tensor] = None, out_dtype: Optional[torch.dtype] = None,
-         out: Optional[Tensor] = None, residual_mod: int = 0, b_colsum: Optional[Tensor] = None) -> Tensor:
+         out: Optional[Tensor] = None, residual_mod: int = 0, b_colsum: Optional[Tensor] = None,
+         variant: Optional[int] = None) -> Tensor:
     """C = act((a' @ b^T) * alpha * scale + bias) + residual.
 
     a: [M, K1] (row stride may exceed K1), b: [N, K] with K = K1 (+ K2 if a2 [M, K2] given).
     a_mean/a_rstd: per-row LayerNorm statistics of a (applied on load, or -- given
     b_colsum = b.sum(1) in fp32 -- after the product as rstd * (acc - mean * b_colsum)).
+    variant: kernel selection for this launch (HV_GV_* bits, _lib.GV_*); None = the forward's
+    HVOptions.gemm_variant (0 = automatic).
     """
     _cuda(a, b)
     if a.dim() != 2 or b.dim() != 2 or a.stride(1) != 1 or b.stride(1) != 1:
@@ -125,6 +127,7 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
     if residual is not None:
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), residual.stride(0), dtype_code(residual.dtype)
         d.r_mod = residual_mod
+    d.variant = options().gemm_variant if variant is None else variant
     work = _splitk(d, M, N, K, a.dtype, a.device)      # noqa: F841  (alive until enqueued)
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm M={M} N={N} K={K}")
     return out
@@ -132,7 +135,7 @@ def gemm(a: Tensor, b: Tensor, *, bias: Optional[Tensor] = None, scale: Optional
 
 def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, bias=None,
            act: str = "none", residual: Optional[Tensor] = None,
-           out_dtype: Optional[torch.dtype] = None) -> Tensor:
+           out_dtype: Optional[torch.dtype] = None, variant: Optional[int] = None) -> Tensor:
     """Implicit-GEMM convolution. x: NHWC [n, h, w, c]; w: [cout, k*k*c] (from conv_weight_prep)."""
     _cuda(x, w)
     _contig(x, "conv input")
@@ -157,6 +160,7 @@ def conv2d(x: Tensor, w: Tensor, k: int, stride: int, pad: int, *, scale=None, b
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), cout, dtype_code(residual.dtype)
     d.conv_n, d.conv_h, d.conv_w, d.conv_c = n, h, wd, c
     d.conv_k, d.conv_stride, d.conv_pad, d.conv_oh, d.conv_ow = k, stride, pad, oh, ow
+    d.variant = options().gemm_variant if variant is None else variant
     work = _splitk(d, d.M, cout, d.K, x.dtype, x.device)   # noqa: F841  (alive until enqueued)
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(conv {c}->{cout} k{k} s{stride})")
     return out
@@ -243,12 +247,15 @@ def f32(t: Optional[Tensor]) -> Optional[Tensor]:
     return None if t is None else t.detach().float().contiguous()
 
 
-def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype) -> bool:
-    return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype)))
+def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype, variant: Optional[int] = None) -> bool:
+    v = options().mhc_variant if variant is None else variant
+    return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype), v))
 
 
-def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optional[Tensor] = None) -> Tensor:
-    """One-launch mHC token chain (bf16) for x [T, D]; see hv_mhc_fused in hv_kernels.h."""
+def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optional[Tensor] = None,
+              variant: Optional[int] = None) -> Tensor:
+    """One-launch mHC token chain (bf16) for x [T, D]; see hv_mhc_fused in hv_kernels.h.
+    variant: HV_MV_* bits for this launch (None = the forward's HVOptions.mhc_variant)."""
     _contig(x, "x")
     T, D = x.shape
     Hd = w2.shape[0]
@@ -261,7 +268,7 @@ def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optiona
     out = torch.empty_like(x)
     a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
                        b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), ptr(residual),
-                       out.data_ptr())
+                       out.data_ptr(), options().mhc_variant if variant is None else variant, 0)
     check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
     return out
 

@@ -14,6 +14,7 @@ import torch
 from . import _lib as L
 from ._lib import check, dtype_code, ptr, stream_ptr
 from .ops import _contig, _cuda, f32
+from .runtime import options
 
 Tensor = torch.Tensor
 
@@ -61,6 +62,7 @@ def gemm_train(a: Tensor, b: Tensor, *, mode: int, act: str = "none", aux: Optio
     if residual is not None:
         _contig(residual, "residual")
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), N, dtype_code(residual.dtype)
+    d.variant = options().gemm_variant
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(train mode {mode}) M={M} N={N} K={K}")
     return out
 
@@ -97,6 +99,7 @@ def conv_dgrad(dy: Tensor, wt: Tensor, k: int, stride: int, pad: int, in_hw, *, 
         d.conv_h, d.conv_w, d.conv_c = oh, ow, cout
         d.conv_stride, d.conv_pad, d.conv_oh, d.conv_ow = stride, pad, h, w
         d.conv_transposed = 1
+    d.variant = options().gemm_variant
     check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(conv dgrad {cout}->{cin} k{k} s{stride})")
     return out
 

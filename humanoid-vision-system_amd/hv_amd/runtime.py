@@ -11,6 +11,7 @@ parameter's version counter changes.
 from __future__ import annotations
 
 import contextvars
+import dataclasses
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -21,9 +22,40 @@ _CTX: contextvars.ContextVar = contextvars.ContextVar("hv_runtime_ctx", default=
 PRECISIONS = {"bf16": torch.bfloat16, "fp32": torch.float32}
 
 
+@dataclass(frozen=True)
+class HVOptions:
+    """Per-model execution options: kernel selection and the exact restructurings of the
+    inference path.  A model (or a standalone layer) carries one in ``hv_options``; every forward
+    copies it into its RunCtx, so the options are per model and per call -- there is no
+    process-global switch, and concurrent forwards (AsyncInferenceEngine's workers, other
+    streams) never see each other's choice.  The defaults are the product configuration."""
+    use_fused_mhc: bool = True        # one-launch mHC kernel for D <= 128 (hv_mhc_fused)
+    fold_max_d: int = 1024            # fold H_pre into W1 for D <= this (DESIGN.md §2)
+    cls_only_last_block: bool = True  # last ViT block on the CLS query only (exact)
+    group_qkv: bool = True            # q / k / v GEMM1 as one N = 3*2Hd GEMM (exact)
+    parallel_qkv: bool = False        # q / k / v on three streams: measured slower (tools/ab_vit.py)
+    prep_overlap: bool = False        # Sinkhorn + mHC prep on a side stream: measured no gain
+    direct_stem: bool = True          # MFMA stem conv straight from the NCHW image (hv_conv_stem)
+    splitk: bool = False              # split-K for small output grids: measured no gain
+    gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic
+    mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
+
+    def replace(self, **kw) -> "HVOptions":
+        return dataclasses.replace(self, **kw)
+
+
+DEFAULT_OPTIONS = HVOptions()
+
+
+def module_options(module: torch.nn.Module) -> HVOptions:
+    o = getattr(module, "hv_options", None)
+    return o if isinstance(o, HVOptions) else DEFAULT_OPTIONS
+
+
 @dataclass
 class RunCtx:
     dtype: torch.dtype
+    opts: HVOptions = DEFAULT_OPTIONS
     plans: Dict[int, object] = field(default_factory=dict)
     program: Optional[object] = None      # prep.PrepProgram that produced `plans` (grouped prep)
     prep_event: Optional[object] = None   # side-stream prep not yet joined (PrepProgram.run overlap)
@@ -38,6 +70,12 @@ class RunCtx:
 
 def current() -> Optional[RunCtx]:
     return _CTX.get()
+
+
+def options() -> HVOptions:
+    """The options of the forward in progress (the defaults outside any forward)."""
+    ctx = _CTX.get()
+    return ctx.opts if ctx is not None else DEFAULT_OPTIONS
 
 
 class use_ctx:
@@ -93,18 +131,34 @@ _OUTPUT_BUFFERS = ("convergence_history", "eigenvalues", "signal_ratio_history",
 class VersionWatch:
     """Cheap change detector for everything a prepared / captured forward baked in: the
     storage pointer and in-place version counter of every parameter and input buffer (BN
-    statistics, anchors, ...) of `module`.  In-place updates (optimizer steps, load_state_dict
-    copies), `.data` swaps and `.to()` moves all change the snapshot."""
+    statistics, anchors, ...) of `module`, and the storage pointer of every buffer the forward
+    WRITES (Sinkhorn histories, monitor buffers: a captured graph keeps writing into the
+    storage it saw at capture).  In-place updates (optimizer steps, load_state_dict copies),
+    `.data` swaps, buffer rebinding (`module.buf = t`, `_buffers[...] = t` as `.to()` does,
+    HVTrainer's flat-buffer views) and `.to()` moves all change the snapshot.
+
+    Buffers are looked up by (module, name) on every call -- `.to()` / `.float()` replace the
+    buffer tensor objects without a registration hook, so holding the tensors would miss them."""
 
     def __init__(self, module: torch.nn.Module):
         self.module = module
         self._gen = -1
-        self._ts = []
+        self._params = []
+        self._ins = []
+        self._outs = []
 
     def snapshot(self):
         if self._gen != _REG_GEN[0]:
-            self._ts = list(self.module.parameters()) + [
-                b for n, b in self.module.named_buffers() if not n.endswith(_OUTPUT_BUFFERS)]
+            self._params = list(self.module.parameters())
+            self._ins, self._outs = [], []
+            for mname, mod in self.module.named_modules():
+                for bname in mod._buffers:
+                    (self._outs if bname in _OUTPUT_BUFFERS else self._ins).append((mod._buffers, bname))
             self._gen = _REG_GEN[0]
-        ts = self._ts
-        return tuple([t._version for t in ts]), tuple([t.data_ptr() for t in ts])
+        ps = self._params
+        ins = [d.get(n) for d, n in self._ins]
+        ins = [b for b in ins if b is not None]
+        outs = [d.get(n) for d, n in self._outs]
+        return (tuple([t._version for t in ps]), tuple([t.data_ptr() for t in ps]),
+                tuple([t._version for t in ins]), tuple([t.data_ptr() for t in ins]),
+                tuple([0 if t is None else t.data_ptr() for t in outs]))

@@ -7,7 +7,7 @@ import torch.nn as nn
 from . import ops
 from .layers import conv_prep, ctx_scope, linear_prep, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection, MultiHeadManifoldAttention, RMSNorm
-from .runtime import current, require_cuda
+from .runtime import current, options, require_cuda
 
 
 def _positions(pe: torch.Tensor, tokens: int) -> torch.Tensor:
@@ -24,8 +24,8 @@ def _positions(pe: torch.Tensor, tokens: int) -> torch.Tensor:
     return t
 
 
-# run the encoder's last block on the CLS rows only (TransformerEncoderBlock.forward_tokens_cls)
-CLS_ONLY_LAST_BLOCK = True
+# HVOptions.cls_only_last_block: run the encoder's last block on the CLS rows only
+# (TransformerEncoderBlock.forward_tokens_cls)
 
 
 class PatchEmbedding(nn.Module):
@@ -157,7 +157,7 @@ class VisionTransformerEncoder(nn.Module):
         t = t.view(n * L, D)
         nb = len(self.blocks)
         for i, blk in enumerate(self.blocks):
-            if i == nb - 1 and features is None and CLS_ONLY_LAST_BLOCK:
+            if i == nb - 1 and features is None and options().cls_only_last_block:
                 cls = blk.forward_tokens_cls(t, n)          # only the CLS rows survive (exact)
                 break
             t = blk.forward_tokens(t, n)

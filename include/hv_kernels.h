@@ -116,7 +116,10 @@ typedef struct hv_gemm_desc {
      forward INPUT [conv_n, conv_oh, conv_ow]; B = W^T [cin, kh, kw, cout]; tap (kh, kw) of
      input pixel (ih, iw) reads output pixel ((ih + pad - kh) / stride, ...) when divisible. */
   int conv_transposed;
-  int pad1_;
+  /* per-call kernel selection, 0 = automatic (the product default).  Bit fields HV_GV_* below;
+     tests and A/B tools pin a kernel variant per launch -- there is no process-global switch,
+     so concurrent callers (engine worker threads, streams) never see each other's choice. */
+  int variant;
   /* split-K for small output grids (inference epilogues, epi_mode 0, bf16, LDS-DMA kernel):
      splitk > 1 splits the K-tiles of every output tile over `splitk` workgroups, each writing
      its fp32 partial product to splitk_work [splitk][M][N] and bumping the tile's arrival
@@ -131,6 +134,21 @@ typedef struct hv_gemm_desc {
 } hv_gemm_desc;
 
 #define HV_SPLITK_MAX_TILES 4096
+#define HV_GV_TILE_MASK    0x7     /* force: 1 128x128, 2 64x128, 3 128x64, 4 64x64 (LDS-DMA ring),
+                                      5 256x256 ping-pong, 6 persistent small-K */
+#define HV_GV_REGSTAGE     0x8     /* register-staged kernel only (no LDS-DMA path) */
+#define HV_GV_NO_BIG       0x10    /* never the 256x256 ping-pong kernel */
+#define HV_GV_BIG_ALWAYS   0x20    /* the 256x256 kernel whenever eligible */
+#define HV_GV_NO_SMALL     0x40    /* no 64x64 tiles for small grids */
+#define HV_GV_TRAIN128     0x80    /* 128x128 tiles for the training epilogues */
+#define HV_GV_FLAT_EPI     0x100   /* fragment-layout (not LDS-staged) inference epilogue */
+#define HV_GV_FLAT_TRAIN   0x200   /* fragment-layout training epilogue */
+#define HV_GV_SHALLOW      0x400   /* 2-buffer rings for the 64x64 / 64x128 / 128x64 tiles */
+#define HV_GV_CONV_KTAIL   0x800   /* convolutions with K % 64 != 0 on the LDS-DMA kernel */
+#define HV_GV_NO_SMALLK    0x1000  /* no persistent small-K kernel */
+#define HV_GV_SK_DIAG1     0x2000  /* small-K kernel diagnostics (tools/k256_probe2.py; outputs
+                                      garbage): skip the stores */
+#define HV_GV_SK_DIAG2     0x4000  /* ... skip the k-loop */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
@@ -186,8 +204,16 @@ typedef struct hv_mhc_fused_args {
   const float* b_post;  /* [D] */
   const void* residual; /* optional [T, D], added after LN_post (transformer residual stream) */
   void* out;            /* [T, D] */
+  int variant;          /* per-call kernel selection, 0 = automatic; HV_MV_* below */
+  int pad_;
 } hv_mhc_fused_args;
-int hv_mhc_fused_supported(int D, int Hd, int dtype);
+#define HV_MV_SHAPE_MASK  0xff   /* workgroup shape: 1 three 4-wave groups per CU, 2 one 8-wave group,
+                                    5 (D = 128) the per-wave 4-wave kernel instead of split-hidden,
+                                    6 (D = 64) the per-wave 4-wave kernel instead of split-hidden */
+#define HV_MV_WIDE        0x100  /* also run (256, 512) fused (slower than the GEMM chain; tests) */
+#define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
+/* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
+int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant);
 int hv_mhc_fused(const hv_mhc_fused_args* args, hv_stream_t stream);
 
 /* y[N] = W[N, K] x[K] + b  (fp32; folded mHC bias c1 = W1 u + b1) */

@@ -49,5 +49,18 @@ def formula_state_dict(tag: str, fam: str):
     return sd
 
 
+def run_options(dtype=None, **kw):
+    """Context manager: run the enclosed HIP ops under per-call options (runtime.HVOptions --
+    kernel variants, restructurings) instead of the defaults; nothing process-global changes."""
+    import torch
+    from hv_amd.runtime import HVOptions, RunCtx, use_ctx
+    return use_ctx(RunCtx(dtype=dtype or torch.bfloat16, opts=HVOptions(**kw)))
+
+
+def gemm_variant(v: int):
+    """Pin the GEMM kernel variant (HV_GV_* bits, hv_amd._lib.GV_*) of the enclosed launches."""
+    return run_options(gemm_variant=v)
+
+
 MODEL_CFG = {"tiny": dict(num_blocks=[1, 1, 1, 1], vit_depth=1, sk_iters=5, verbose=False),
              "base": dict(verbose=False)}

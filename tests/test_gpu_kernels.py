@@ -5,7 +5,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import golden
+from conftest import gemm_variant, golden, run_options
 from oracle import cases
 
 pytestmark = pytest.mark.gpu
@@ -174,18 +174,13 @@ def test_gemm_splitk_vs_unsplit(gpu_device, M, N, K, kind):
             kw.update(residual=torch.randn(4, N, generator=g).to(dt).to(dev), residual_mod=4)
             kw.pop("act")
         run = lambda: ops.gemm(a, b, **kw)                                   # noqa: E731
-    saved = ops.SPLITK_ON
-    ops.SPLITK_ON = True                                    # opt-in path (off by default)
-    try:
+    with run_options(splitk=True):                          # opt-in path (off by default)
         ops.launch_counts(reset=True)
         out = run()
         counts = ops.launch_counts(reset=True)
         assert counts["gemm_splitk"] == 1, counts           # the split path ran
         assert torch.equal(run(), out)                      # deterministic
-        ops.SPLITK_ON = False
-        ref = run()                                         # same LDS-DMA kernel family, un-split
-    finally:
-        ops.SPLITK_ON = saved
+    ref = run()                                             # same LDS-DMA kernel family, un-split
     d = (out.float() - ref.float()).abs()
     assert d.max().item() <= 2 ** -6 * max(1.0, ref.float().abs().max().item()), d.max().item()
     assert rel_err(out.float(), ref.float()) < 4e-3
@@ -226,11 +221,8 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
         run = lambda: ops.gemm(a, b, bias=bias, act="relu", out_dtype=torch.float32)  # noqa: E731
         ref = F.relu(a.float().cpu() @ b.float().cpu().T + bias.cpu())
     fast = run()
-    _lib.lib().hv_gemm_set_path(1)
-    try:
+    with gemm_variant(_lib.GV_REGSTAGE):
         slow = run()
-    finally:
-        _lib.lib().hv_gemm_set_path(0)
     assert rel_err(fast, slow) < 1e-5
     assert rel_err(fast, ref) < 1e-4
 
@@ -282,16 +274,12 @@ def test_gemm_smallk_equals_ring(gpu_device, kind, M, N, K):
         x = a.view(2, hw, hw, K)
         run = lambda: ops.conv2d(x, b, 1, 1, 0, out_dtype=torch.float32)  # noqa: E731
         ref = af @ bfl.T
-    lib = _lib.lib()
-    try:
-        lib.hv_gemm_set_force_tile(6)
+    with gemm_variant(_lib.GV_TILE_SMALLK):
         ops.launch_counts(reset=True)
         fast = run()
         assert ops.launch_counts()["gemm_smallk"] == 1
-        lib.hv_gemm_set_force_tile(1)
+    with gemm_variant(_lib.GV_TILE_128x128):
         ring = run()
-    finally:
-        lib.hv_gemm_set_force_tile(0)
     if M * N >= 8192 * 1024:
         ops.launch_counts(reset=True)
         auto = run()
@@ -312,7 +300,7 @@ PP256_CASES = [  # (kind, M, N, K): ragged M/N, 1-3 K-tiles (prologue/tail vmcnt
 
 @pytest.mark.parametrize("kind,M,N,K", PP256_CASES)
 def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
-    """The 256x256 ping-pong LDS-DMA kernel (hv_gemm_set_big_tile(2) forces it) against the
+    """The 256x256 ping-pong LDS-DMA kernel (variant GV_BIG_ALWAYS forces it) against the
     default tiles: same per-element k order, so bit-identical outputs; plus a CPU fp32 check."""
     ops = _ops()
     from hv_amd import _lib
@@ -350,21 +338,14 @@ def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
             a1, a2 = a[:, :k1].contiguous(), a[:, k1:].contiguous()
             run = lambda: ops.gemm(a1, b, a2=a2, out_dtype=torch.float32)  # noqa: E731
             ref = af @ bfl.T
-    lib = _lib.lib()
     outs = {}
-    try:
-        for staged in (1, 0):                   # LDS-staged coalesced epilogue vs fragment-layout stores
-            lib.hv_gemm_set_staged_epilogue(staged)
-            for deep in (1, 0):                 # 3/4-buffer LDS-DMA rings vs 2 buffers
-                lib.hv_gemm_set_deep_ring(deep)
-                lib.hv_gemm_set_big_tile(0)
+    for staged in (1, 0):                       # LDS-staged coalesced epilogue vs fragment-layout stores
+        flat = 0 if staged else _lib.GV_FLAT_EPI
+        for deep in (1, 0):                     # 3/4-buffer LDS-DMA rings vs 2 buffers
+            with gemm_variant(flat | _lib.GV_NO_BIG | (0 if deep else _lib.GV_SHALLOW)):
                 outs["base", staged, deep] = run()
-            lib.hv_gemm_set_big_tile(2)
+        with gemm_variant(flat | _lib.GV_BIG_ALWAYS):
             outs["pp", staged] = run()
-    finally:
-        lib.hv_gemm_set_big_tile(1)
-        lib.hv_gemm_set_staged_epilogue(1)
-        lib.hv_gemm_set_deep_ring(1)
     torch.cuda.synchronize()
     pp, base = outs["pp", 1], outs["base", 0, 0]
     for key, o in outs.items():
@@ -383,14 +364,9 @@ def test_conv_ktail_lds_dma_vs_register_path(gpu_device, cin, cout, s, hw):
     w = (torch.randn(cout, 9 * cin, generator=g) / (9 * cin) ** 0.5).to(torch.bfloat16).to(gpu_device)
     bias = torch.randn(cout, generator=g).to(gpu_device)
     run = lambda: ops.conv2d(x, w, 3, s, 1, bias=bias, act="silu", out_dtype=torch.float32)  # noqa: E731
-    lib = _lib.lib()
-    try:
-        lib.hv_gemm_set_conv_ktail(1)
+    with gemm_variant(_lib.GV_CONV_KTAIL):
         fast = run()
-        lib.hv_gemm_set_conv_ktail(0)
-        slow = run()
-    finally:
-        lib.hv_gemm_set_conv_ktail(0)
+    slow = run()
     ref = F.silu(F.conv2d(x.float().cpu().permute(0, 3, 1, 2), w.float().cpu().view(cout, 3, 3, cin).permute(0, 3, 1, 2),
                           bias.cpu(), s, 1)).permute(0, 2, 3, 1)
     assert rel_err(fast, slow) < 1e-5
@@ -479,11 +455,8 @@ def test_conv3x3_c32_halo_kernel_vs_torch_and_regstage(gpu_device, cout, h, w):
     wd = ops.conv_weight_prep(wt.to(gpu_device), dt)
     kw = dict(scale=sc.to(gpu_device), bias=bi.to(gpu_device), act="silu")
     out = ops.conv2d(xd, wd, 3, 1, 1, **kw)
-    _lib.lib().hv_gemm_set_path(1)
-    try:
+    with gemm_variant(_lib.GV_REGSTAGE):
         reg = ops.conv2d(xd, wd, 3, 1, 1, **kw)
-    finally:
-        _lib.lib().hv_gemm_set_path(0)
     d = (out.float() - reg.float()).abs()
     assert d.max().item() <= 2 ** -7 * max(1.0, reg.float().abs().max().item())
     assert (d > 0).float().mean().item() < 0.02            # equal up to rare 1-ulp roundings

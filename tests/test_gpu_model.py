@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import MODEL_CFG, formula_state_dict, golden
+from conftest import MODEL_CFG, formula_state_dict, golden, run_options
 from oracle import cases
 from oracle import weights as W
 
@@ -28,19 +28,15 @@ def rel_l2(a, b):
 @pytest.mark.parametrize("D,e", cases.MHC_CASES)
 def test_mhc_fp32_matches_reference(gpu_device, fam, D, e):
     from hv_amd import ManifoldHyperConnection
-    from hv_amd import manifold as MF
+    from hv_amd.runtime import HVOptions
     g = golden(f"mhc_{fam}_D{D}_e{e}")
     m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=False)
     W.load_formula_weights(m, fam)
     m = m.to(gpu_device).eval()
     x = cases.mhc_input(D, e).to(gpu_device)
     for fold in (True, False):
-        old = MF.FOLD_MAX_D
-        MF.FOLD_MAX_D = 4096 if fold else 0
-        try:
-            y = m(x).cpu().numpy()
-        finally:
-            MF.FOLD_MAX_D = old
+        m.hv_options = HVOptions(fold_max_d=4096 if fold else 0)     # per-layer option
+        y = m(x).cpu().numpy()
         np.testing.assert_allclose(y, g["y64"], rtol=0, atol=1e-3)
         np.testing.assert_allclose(y, g["y"], rtol=0, atol=1e-3)
 
@@ -62,26 +58,18 @@ def test_mhc_bf16_agreement(gpu_device, D, e):
                                              (256, 2, 130, True)])
 def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, e, T, with_res):
     """hv_mhc_fused (one launch, on-chip intermediates) vs the six-launch chain, both bf16."""
-    from hv_amd import ManifoldHyperConnection
-    from hv_amd import manifold as MF
-    from hv_amd.runtime import RunCtx, use_ctx
+    from hv_amd import ManifoldHyperConnection, _lib
     m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
     W.load_formula_weights(m, "wc")
     m = m.to(gpu_device).eval()
     g = torch.Generator().manual_seed(T)
     x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
     res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
-    from hv_amd import _lib
-    _lib.lib().hv_mhc_fused_enable_wide(1)
-    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
-        MF.USE_FUSED = True
-        y1 = m.forward_tokens(x, residual=res).float().cpu().numpy()
-        MF.USE_FUSED = False
-        try:
+    with torch.no_grad():
+        with run_options(mhc_variant=_lib.MV_WIDE):
+            y1 = m.forward_tokens(x, residual=res).float().cpu().numpy()
+        with run_options(use_fused_mhc=False):
             y0 = m.forward_tokens(x, residual=res).float().cpu().numpy()
-        finally:
-            MF.USE_FUSED = True
-            _lib.lib().hv_mhc_fused_enable_wide(0)
     assert rel_l2(y1, y0) < 1e-2
     assert np.abs(y1 - y0).max() < 0.1
 
@@ -301,23 +289,17 @@ def test_model_deterministic_and_frozen_cache(gpu_device):
 def test_mhc_fused_workgroup_shapes_bitwise_equal(gpu_device, D, T):
     """The 4-wave (default) and 8-wave workgroup shapes of hv_mhc_fused give identical bits:
     every wave computes its own tokens end to end, only the barrier grouping differs."""
-    import ctypes
     from hv_amd import ManifoldHyperConnection, _lib
-    from hv_amd.runtime import RunCtx, use_ctx
-    lib = _lib.lib()
-    lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
     m = ManifoldHyperConnection(D, expansion_rate=4, use_mixed_precision=True)
     W.load_formula_weights(m, "wc")
     m = m.to(gpu_device).eval()
     x = torch.randn(T, D, generator=torch.Generator().manual_seed(T)).to(torch.bfloat16).to(gpu_device)
-    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
-        try:
-            lib.hv_mhc_fused_set_variant(2)
+    with torch.no_grad():
+        with run_options(mhc_variant=_lib.MV_ONE_GROUP8):
             y8 = m.forward_tokens(x).cpu()
-            lib.hv_mhc_fused_set_variant(5)          # D=128: the per-wave 4-wave kernel (default is split-hidden)
+        # D=128: the per-wave 4-wave kernel (default is split-hidden)
+        with run_options(mhc_variant=_lib.MV_PERWAVE128 if D == 128 else 0):
             y4 = m.forward_tokens(x).cpu()
-        finally:
-            lib.hv_mhc_fused_set_variant(0)
     assert torch.equal(y4, y8)
 
 
@@ -326,30 +308,21 @@ def test_mhc_fused_split_hidden_matches_unfused(gpu_device, T, with_res):
     """The split-hidden D=128 kernel (the default: hidden dimension across 4 waves, split-K
     GEMM3 reduced in LDS) vs the unfused six-launch chain and the per-wave fused kernel (bf16),
     ragged T, residual; deterministic (two runs bitwise equal)."""
-    import ctypes
     from hv_amd import ManifoldHyperConnection, _lib
-    from hv_amd import manifold as MF
-    from hv_amd.runtime import RunCtx, use_ctx
-    lib = _lib.lib()
-    lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
     m = ManifoldHyperConnection(128, expansion_rate=4, use_mixed_precision=True)
     W.load_formula_weights(m, "wc")
     m = m.to(gpu_device).eval()
     g = torch.Generator().manual_seed(T)
     x = torch.randn(T, 128, generator=g).to(torch.bfloat16).to(gpu_device)
     res = torch.randn(T, 128, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
-    with torch.no_grad(), use_ctx(RunCtx(dtype=torch.bfloat16)):
-        try:
-            lib.hv_mhc_fused_set_variant(0)
+    with torch.no_grad():
+        with run_options():
             y3 = m.forward_tokens(x, residual=res).float().cpu()
             y3b = m.forward_tokens(x, residual=res).float().cpu()
-            lib.hv_mhc_fused_set_variant(2)
+        with run_options(mhc_variant=_lib.MV_ONE_GROUP8):
             y2 = m.forward_tokens(x, residual=res).float().cpu()
-            MF.USE_FUSED = False
+        with run_options(use_fused_mhc=False):
             y0 = m.forward_tokens(x, residual=res).float().cpu()
-        finally:
-            MF.USE_FUSED = True
-            lib.hv_mhc_fused_set_variant(0)
     assert torch.equal(y3, y3b)
     assert rel_l2(y3.numpy(), y0.numpy()) < 1e-2 and (y3 - y0).abs().max() < 0.1
     assert rel_l2(y3.numpy(), y2.numpy()) < 1e-2
@@ -497,20 +470,15 @@ def test_vit_shortcuts_match_plain_path(gpu_device, precision):
     (only the CLS row survives, vit_encoder_decoder.py:308-311), the q/k/v projections on
     three streams and the grouped q/k/v GEMM1 give the plain path's vit features (fp32: 1e-5; bf16: same GEMM kernels on
     fewer rows -> rounding-level)."""
-    from hv_amd import manifold as MF
-    from hv_amd import vit as VT
     m = _build("base", "wc", precision, gpu_device)
     x = cases.model_input(2, 224).to(gpu_device)
     outs = {}
     for cls_only, par, grp in ((True, True, False), (False, False, False), (True, False, False),
                                (True, False, True)):
-        VT.CLS_ONLY_LAST_BLOCK, MF.PARALLEL_QKV, MF.GROUP_QKV = cls_only, par, grp
-        try:
-            with torch.no_grad():
-                o = m(x)
-            outs[(cls_only, par, grp)] = (o["vit_features"].float().cpu(), o["predictions"]["scale_2"].cpu())
-        finally:
-            VT.CLS_ONLY_LAST_BLOCK, MF.PARALLEL_QKV, MF.GROUP_QKV = True, False, True
+        m.set_options(cls_only_last_block=cls_only, parallel_qkv=par, group_qkv=grp)   # per model
+        with torch.no_grad():
+            o = m(x)
+        outs[(cls_only, par, grp)] = (o["vit_features"].float().cpu(), o["predictions"]["scale_2"].cpu())
     ref_v, ref_p = outs[(False, False, False)]
     tol = 1e-5 if precision == "fp32" else 2e-2
     for key, (v, p) in outs.items():

@@ -33,11 +33,7 @@ def test_mhc_prep_group_matches_per_site(gpu_device, dtype):
         p = ctx.plans[id(m)]
         h, hist = ops.sinkhorn(m.H_res_raw, m.sinkhorn.num_iterations)
         assert torch.equal(m.sinkhorn.convergence_history, hist)
-        MF.FOLD_MAX_D, old = 1024, MF.FOLD_MAX_D
-        try:
-            q = MF.build_plan(m, h, dtype)
-        finally:
-            MF.FOLD_MAX_D = old
+        q = MF.build_plan(m, h, dtype, fold_max_d=1024)
         assert p.fold == q.fold == (m.input_dim <= 1024)
         assert rel(p.b1, q.b1) < tol, (m.input_dim, rel(p.b1, q.b1))
         assert rel(p.c1, q.c1) < 1e-5

@@ -708,13 +708,12 @@ def test_module_level_training_api(gpu_device):
 @pytest.mark.parametrize("M,N,K,act,ln", [(300, 136, 128, "gelu", False), (1000, 256, 256, "silu", True),
                                           (777, 96, 64, "leaky", False)])
 def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
-    """The LDS-staged training epilogue (hv_gemm_set_staged_train, the default) writes exactly the
+    """The LDS-staged training epilogue (the default; variant GV_FLAT_TRAIN = fragment layout) writes exactly the
     bits of the fragment-layout one: pre-activation, dropout(act) output (mode 1) and the
     gradient through act + dropout with a residual (mode 2), incl. the LayerNorm-after-product
     variant and ragged M / N."""
     from hv_amd import _lib, ops
     T = OT()
-    lib = _lib.lib()
     g = torch.Generator().manual_seed(M + N)
     a = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu_device)
     b = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(gpu_device)
@@ -725,14 +724,12 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
         mean, rstd = ops.row_stats(a, 1e-5)
         kw = dict(a_mean=mean, a_rstd=rstd, b_colsum=b.float().sum(1))
     outs = {}
+    from conftest import gemm_variant
     for staged in (1, 0):
-        lib.hv_gemm_set_staged_train(staged)
-        try:
+        with gemm_variant(0 if staged else _lib.GV_FLAT_TRAIN):
             pre = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
             y = T.gemm_train(a, b, mode=1, act=act, aux=pre, bias=bias, drop_p=0.2, seed=5, **kw)
             dpre = T.gemm_train(a, b, mode=2, act=act, aux=pre, drop_p=0.2, seed=5, residual=res)
             outs[staged] = (pre, y, dpre)
-        finally:
-            lib.hv_gemm_set_staged_train(1)
     for x0, x1 in zip(outs[1], outs[0]):
         assert torch.equal(x0, x1)

@@ -16,10 +16,9 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 640
 P = sys.argv[3] if len(sys.argv) > 3 else "bf16"
 
-if os.environ.get("HV_GEMM_BIG") is not None:       # A/B knob for the 256x256 kernel
-    from hv_amd import _lib
-    _lib.lib().hv_gemm_set_big_tile(int(os.environ["HV_GEMM_BIG"]))
 m = HybridVisionSystem({"precision": P, "verbose": False}).cuda().eval()
+if os.environ.get("HV_GEMM_VARIANT"):               # per-model GEMM variant (HV_GV_* bits) for A/Bs
+    m.set_options(gemm_variant=int(os.environ["HV_GEMM_VARIANT"], 0))
 x = torch.randn(B, 3, S, S, device="cuda")
 with torch.no_grad():
     m(x)

@@ -10,6 +10,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
 from hv_amd import ManifoldHyperConnection, ops  # noqa: E402
 from hv_amd import manifold as MF  # noqa: E402
+from hv_amd.runtime import HVOptions, RunCtx, use_ctx  # noqa: E402
 
 
 def timeit(fn, iters=20, warm=3):
@@ -36,11 +37,10 @@ def mhc_bench():
         for fused in (True, False):
             if fused and not ops.mhc_fused_supported(D, Hd, torch.bfloat16):
                 continue
-            MF.USE_FUSED = fused
-            ms = timeit(lambda: MF.mhc_apply(x, p))
+            with use_ctx(RunCtx(dtype=torch.bfloat16, opts=HVOptions(use_fused_mhc=fused))):
+                ms = timeit(lambda: MF.mhc_apply(x, p))
             print(f"mhc D={D:4d} Hd={Hd:4d} T={T:8d} {'fused  ' if fused else 'unfused'} {ms:8.3f} ms "
                   f"{fl / ms / 1e9:8.1f} TF/s (executed)")
-        MF.USE_FUSED = True
 
 
 def gemm_bench():

@@ -1,5 +1,5 @@
-"""A/B the fused mHC kernel variants against the unfused GEMM chain at in-model shapes (B=16)."""
-import ctypes
+"""A/B the fused mHC kernel variants (per-call HV_MV_* shapes) against the unfused GEMM chain at
+in-model shapes (B=16).  usage: python tools/mhc_ab.py [D:T[:expansion] ...]"""
 import os
 import sys
 
@@ -8,13 +8,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
 from hv_amd import ManifoldHyperConnection, _lib  # noqa: E402
 from hv_amd import manifold as MF  # noqa: E402
+from hv_amd.runtime import HVOptions, RunCtx, use_ctx  # noqa: E402
 
-lib = _lib.lib()
-lib.hv_mhc_fused_set_variant.argtypes = [ctypes.c_int]
-# argv: D:T[:expansion] ...
 shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[1:]] or \
     [(32, 1638400), (64, 409600), (128, 102400), (128, 25600)]
-lib.hv_mhc_fused_enable_wide(1)
 
 
 def timed(fn, n=5):
@@ -28,6 +25,11 @@ def timed(fn, n=5):
     return s.elapsed_time(e) / n
 
 
+W = _lib.MV_WIDE
+CASES = {"unfused": HVOptions(use_fused_mhc=False), "fused_v0": HVOptions(mhc_variant=W),
+         "fused_v1": HVOptions(mhc_variant=W | 1), "fused_v2": HVOptions(mhc_variant=W | 2),
+         "fused_v5": HVOptions(mhc_variant=W | 5), "fused_v6": HVOptions(mhc_variant=W | 6)}
+
 for shp in shapes:
     D, T, ex = shp if len(shp) == 3 else (*shp, 4)
     m = ManifoldHyperConnection(D, expansion_rate=ex).cuda().eval()
@@ -35,22 +37,18 @@ for shp in shapes:
     p = m.plan()
     Hd = ex * D
     fl = 2.0 * T * (D * 2 * Hd + 2 * Hd * Hd + (Hd + D) * D)
-    cases = {"unfused": (False, 0), "fused_v0": (True, 0), "fused_v1": (True, 1), "fused_v2": (True, 2),
-             "fused_v5": (True, 5)}
-    res = {k: [] for k in cases}
+    res = {k: [] for k in CASES}
     with torch.no_grad():
-        MF.USE_FUSED = False
-        ref = MF.mhc_apply(x, p).float()
+        with use_ctx(RunCtx(dtype=torch.bfloat16, opts=CASES["unfused"])):
+            ref = MF.mhc_apply(x, p).float()
         for rep in range(5):
-            for k, (fu, v) in cases.items():
-                MF.USE_FUSED = fu
-                lib.hv_mhc_fused_set_variant(v)
-                if rep == 0:
-                    y = MF.mhc_apply(x, p).float()
-                    print(f"D={D} T={T} {k}: rel err vs unfused {((y - ref).norm() / ref.norm()).item():.2e}", flush=True)
-                res[k].append(timed(lambda: MF.mhc_apply(x, p)))
-    MF.USE_FUSED = True
-    lib.hv_mhc_fused_set_variant(0)
+            for k, o in CASES.items():
+                with use_ctx(RunCtx(dtype=torch.bfloat16, opts=o)):
+                    if rep == 0:
+                        y = MF.mhc_apply(x, p).float()
+                        print(f"D={D} T={T} {k}: rel err vs unfused {((y - ref).norm() / ref.norm()).item():.2e}",
+                              flush=True)
+                    res[k].append(timed(lambda: MF.mhc_apply(x, p)))
     for k, ts in res.items():
         t = sorted(ts)[len(ts) // 2]
         print(f"mhc D={D:4d} T={T:8d} {k:9s}: {t:.3f} ms {fl / t / 1e9:7.1f} TF/s", flush=True)

@@ -1,9 +1,10 @@
-"""In-model A/B of a GEMM knob: base 640 bf16 B=16 forward as a hipGraph captured under each
-setting (kernel choice is fixed at capture), replays timed in interleaved rounds.
+"""In-model A/B of execution options: base 640 bf16 forward as a hipGraph captured under each
+option set (runtime.HVOptions: kernel variants are per call and fixed at capture), replays timed
+in interleaved rounds.
 
-usage: python tools/model_ab.py <knob> <v0> <v1> [batch]
-  knob: deep | staged | big | small | train128 | ktail (hv_gemm_set_*),
-        mhc (hv_mhc_fused_set_variant), wide (hv_mhc_fused_enable_wide)
+usage: python tools/model_ab.py <spec0> <spec1> [batch]
+  spec: comma-separated HVOptions fields, e.g. "gemm_variant=16" (HV_GV_NO_BIG),
+        "mhc_variant=2", "use_fused_mhc=0,group_qkv=0", or "default"
 """
 import os
 import sys
@@ -12,37 +13,42 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
-from hv_amd import HybridVisionSystem, _lib  # noqa: E402
+from hv_amd import HybridVisionSystem  # noqa: E402
+from hv_amd.runtime import HVOptions  # noqa: E402
 
-lib = _lib.lib()
-knob, v0, v1 = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-B = int(sys.argv[4]) if len(sys.argv) > 4 else 16
-setter = {"deep": lib.hv_gemm_set_deep_ring, "staged": lib.hv_gemm_set_staged_epilogue,
-          "big": lib.hv_gemm_set_big_tile, "small": lib.hv_gemm_set_small_tile,
-          "train128": lib.hv_gemm_set_train128, "ktail": lib.hv_gemm_set_conv_ktail,
-          "mhc": lib.hv_mhc_fused_set_variant, "wide": lib.hv_mhc_fused_enable_wide}[knob]
+
+def parse(spec: str) -> HVOptions:
+    kw = {}
+    if spec != "default":
+        for item in spec.split(","):
+            k, v = item.split("=")
+            kw[k] = int(v, 0)
+    return HVOptions(**kw)
+
+
+specs = sys.argv[1:3]
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 16
 torch.manual_seed(0)
 m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False}).cuda().eval()
 x = torch.randn(B, 3, 640, 640, device="cuda")
 runners = {}
 with torch.no_grad():
     m(x)
-    for v in (v0, v1):
-        setter(v)
-        runners[v] = m.capture(x)
-    setter(v0)
-    res = {v0: [], v1: []}
+    for sp in specs:
+        m.set_options(parse(sp))
+        runners[sp] = m.capture(x)
+    res = {sp: [] for sp in specs}
     for rnd in range(5):
-        for v in (v0, v1):
-            r = runners[v]
+        for sp in specs:
+            r = runners[sp]
             for _ in range(2):
-                r.replay()
+                r.graph.replay()
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(10):
-                r.replay()
+                r.graph.replay()
             torch.cuda.synchronize()
-            res[v].append((time.perf_counter() - t) / 10 * 1e3)
-for v in (v0, v1):
-    ts = sorted(res[v])
-    print(f"{knob}={v}: median {ts[len(ts) // 2]:.3f} ms/step  min {ts[0]:.3f}  ({B / ts[len(ts) // 2] * 1e3:.1f} img/s)")
+            res[sp].append((time.perf_counter() - t) / 10 * 1e3)
+for sp in specs:
+    ts = sorted(res[sp])
+    print(f"{sp}: median {ts[len(ts) // 2]:.3f} ms/step  min {ts[0]:.3f}  ({B / ts[len(ts) // 2] * 1e3:.1f} img/s)")

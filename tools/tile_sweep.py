@@ -1,4 +1,4 @@
-"""Per-shape sweep of the LDS-DMA GEMM tiles (hv_gemm_set_force_tile) on the bench's weak GEMM
+"""Per-shape sweep of the LDS-DMA GEMM tiles (per-call variant HV_GV_TILE_MASK) on the bench's weak GEMM
 shapes, with their real epilogues (LN-after-product + GELU, K-concat, conv).  HIP events, us.
 usage: python tools/tile_sweep.py"""
 import os
@@ -7,9 +7,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "humanoid-vision-system_amd")]
 import torch  # noqa: E402
-from hv_amd import ops, _lib  # noqa: E402
+from hv_amd import ops  # noqa: E402
+from hv_amd.runtime import HVOptions, RunCtx, use_ctx  # noqa: E402
 
-lib = _lib.lib()
 
 
 def timeit(fn, iters=20, warm=3):
@@ -75,11 +75,10 @@ for name, mk in CASES:
     fn, flop = mk()
     row = []
     for code in range(6):
-        lib.hv_gemm_set_force_tile(code)
-        try:
-            row.append(timeit(fn))
-        except RuntimeError:
-            row.append(float("nan"))
-    lib.hv_gemm_set_force_tile(0)
+        with use_ctx(RunCtx(dtype=torch.bfloat16, opts=HVOptions(gemm_variant=code))):   # per-call tile
+            try:
+                row.append(timeit(fn))
+            except RuntimeError:
+                row.append(float("nan"))
     best = min(v for v in row if v == v)
     print(f"{name:28s} " + " ".join(f"{v:9.1f}" for v in row) + f"   best {flop / best / 1e6:7.1f} TF/s", flush=True)

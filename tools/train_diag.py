@@ -54,11 +54,6 @@ if what in ("grads", "all"):
     print("median rel", sorted(r[0] for r in rows)[len(rows) // 2])
 
 if what in ("time", "all"):
-    from hv_amd import _lib
-    if len(sys.argv) > 4:                      # A/B knob: 128x128 training-epilogue tiles on/off
-        _lib.lib().hv_gemm_set_train128(int(sys.argv[4]))
-    if os.environ.get("HV_GEMM_DEEP") is not None:   # A/B knob: deep LDS-DMA rings
-        _lib.lib().hv_gemm_set_deep_ring(int(os.environ["HV_GEMM_DEEP"]))
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 640
     torch.manual_seed(0)
