@@ -842,10 +842,16 @@ __global__ void __launch_bounds__(256) k_grad_norm_final(int nblk, const float* 
 }
 
 __global__ void __launch_bounds__(256) k_adamw(const hv_param_entry* tab, int count, const float* coefs, float lr,
-                                               float b1, float b2, float eps, float wd, float bc1, float bc2s) {
+                                               float b1, float b2, float eps, float wd, float bc1, float bc2s,
+                                               const int* __restrict__ steps) {
   const int ei = find_param(tab, count, blockIdx.x);
   const hv_param_entry e = tab[ei];
   if (!e.grad) return;
+  if (steps) {                                  // per-parameter bias correction (torch state['step'])
+    const float t = (float)max(steps[ei], 1);
+    bc1 = 1.f - powf(b1, t);
+    bc2s = sqrtf(1.f - powf(b2, t));
+  }
   const long b0 = (long)(blockIdx.x - e.blk) * PB_ELEMS;
   const float cf = coefs ? coefs[e.group] : 1.f;
   const float step = lr / bc1;
@@ -1214,12 +1220,13 @@ extern "C" int hv_grad_norms(const hv_param_entry* tab, int count, int total_blo
 }
 
 extern "C" int hv_adamw(const hv_param_entry* tab, int count, int total_blocks, const float* coefs, float lr,
-                        float beta1, float beta2, float eps, float weight_decay, int step, hv_stream_t stream) {
-  if (!tab || count <= 0 || total_blocks <= 0 || step < 1) return HV_EINVAL;
-  const float bc1 = 1.f - powf(beta1, (float)step);
-  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+                        float beta1, float beta2, float eps, float weight_decay, int step, const int* steps,
+                        hv_stream_t stream) {
+  if (!tab || count <= 0 || total_blocks <= 0 || (step < 1 && !steps)) return HV_EINVAL;
+  const float bc1 = 1.f - powf(beta1, (float)max(step, 1));
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)max(step, 1)));
   k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, lr, beta1, beta2, eps, weight_decay, bc1,
-                                                         bc2s);
+                                                         bc2s, steps);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

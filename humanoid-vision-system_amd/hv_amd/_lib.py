@@ -203,7 +203,7 @@ _SIGS = {
     "hv_yolo_loss": ([i32, vp, vp, i32, i32, i32, i32, i32, f32, f32, f32, f32, vp, i32, vp, vp, vp], i32),
     "hv_param_blocks": ([i64], i32),
     "hv_grad_norms": ([vp, i32, i32, i32, vp, vp, vp, vp, vp], i32),
-    "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp], i32),
+    "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp, vp], i32),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -10,6 +10,7 @@ import ctypes as C
 from typing import Optional
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib as L
 from ._lib import check, dtype_code, ptr, stream_ptr
@@ -204,6 +205,11 @@ def bn_stats(x: Tensor, eps: float, momentum: float, running_mean: Optional[Tens
     check(L.lib().hv_bn_stats(dtype_code(x.dtype), x.data_ptr(), rows, c, eps, momentum, mean.data_ptr(),
                               rstd.data_ptr(), ptr(running_mean), ptr(running_var), work.data_ptr(), stream_ptr()),
           "hv_bn_stats")
+    # running statistics were updated by the kernel: bump their versions like torch's in-place
+    # update (VersionWatch: eval-mode frozen coefficients / captured graphs refold the BN)
+    ran = [t for t in (running_mean, running_var) if t is not None]
+    if ran:
+        increment_version(ran)
     return mean, rstd
 
 

@@ -26,6 +26,7 @@ import math
 from typing import Dict, List, Optional, Sequence
 
 import torch
+from torch.autograd.graph import increment_version
 import torch.distributed as dist
 
 from . import _lib as L
@@ -193,6 +194,9 @@ class FusedAdamW:
         self.exp_avg_sq = [torch.zeros_like(p) for _, p in self.named]
         self.step_count = 0
         self.param_steps = [0] * len(self.named)   # per-parameter steps (reference state['step'])
+        # the same counts on the device, for the per-parameter bias correction of hv_adamw
+        self._steps_dev = torch.zeros(len(self.named), device=self.named[0][1].device, dtype=torch.int32)
+        self._active_dev = None
         self.norms = torch.zeros(len(self.max_norms), device=dev, dtype=torch.float32)
         self.coefs = torch.ones(len(self.max_norms), device=dev, dtype=torch.float32)
         self._table = None
@@ -227,10 +231,12 @@ class FusedAdamW:
         if key != self._key:
             self._build(active)
             self._key = key
+            self._active_dev = torch.tensor([int(a) for a in active], dtype=torch.int32).to(self.device)
         lib = L.lib()
         self.step_count += 1
         for i, a in enumerate(active):
             self.param_steps[i] += int(a)
+        self._steps_dev.add_(self._active_dev)
         coefs = None
         if clip:
             mx = (C.c_float * len(self.max_norms))(*self.max_norms)
@@ -240,7 +246,11 @@ class FusedAdamW:
             coefs = self.coefs.data_ptr()
         b1, b2 = self.betas
         check(lib.hv_adamw(self._table.data_ptr(), len(self.named), self._blocks, coefs, self.lr, b1, b2, self.eps,
-                           self.wd, self.step_count, stream_ptr()), "hv_adamw")
+                           self.wd, self.step_count, self._steps_dev.data_ptr(), stream_ptr()), "hv_adamw")
+        # the kernel wrote the parameters behind autograd's back: bump their version counters as
+        # an in-place torch update would, so frozen coefficients / captured graphs (VersionWatch)
+        # see the new weights
+        increment_version([p for (_, p), a in zip(self.named, active) if a])
 
     # ---- torch.optim-compatible state (checkpoints load into / from torch.optim.AdamW)
     def state_dict(self) -> Dict:
@@ -273,6 +283,7 @@ class FusedAdamW:
             steps.append(self.param_steps[i])
         if steps:
             self.step_count = max(steps)
+        self._steps_dev.copy_(torch.tensor(self.param_steps, dtype=torch.int32))
 
     def total_norm(self) -> Tensor:
         """sqrt(sum of squared group norms) (mhc_trainer.py:383), a device scalar."""

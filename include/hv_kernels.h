@@ -601,10 +601,13 @@ int hv_param_blocks(long n);
 int hv_grad_norms(const hv_param_entry* dev_table, int count, int total_blocks, int groups,
                   const float* max_norm /* host [groups] */, float* norms, float* coefs, float* work,
                   hv_stream_t stream);
-/* AdamW step with the clip coefficient of each parameter's group (coefs may be NULL) */
+/* AdamW step with the clip coefficient of each parameter's group (coefs may be NULL).  Bias
+   correction 1 - beta^t uses each parameter's own step count steps[i] (device [count], the
+   torch.optim.AdamW per-parameter state['step']; a parameter that skipped steps keeps its own
+   count) or, with steps == NULL, `step` for every parameter. */
 int hv_adamw(const hv_param_entry* dev_table, int count, int total_blocks, const float* coefs,
              float lr, float beta1, float beta2, float eps, float weight_decay, int step,
-             hv_stream_t stream);
+             const int* steps, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Stability monitor (ManifoldHyperConnection._monitor_stability, reference

@@ -49,6 +49,21 @@ def formula_state_dict(tag: str, fam: str):
     return sd
 
 
+def record_parity(name: str, values: dict) -> None:
+    """Persist a parity test's measured agreement (rel-L2, class agreement, ...) as
+    gpurun_out/parity/<name>.json -- the GPU box merges gpurun_out/ back, and the round's
+    records are copied to profiles/ -- so the numbers behind each tolerance stay on file."""
+    import json
+    d = os.path.join(ROOT, "gpurun_out", "parity")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as f:
+            json.dump(values, f, indent=1, sort_keys=True)
+    except OSError:
+        pass
+    print(f"parity record {name}: {values}")
+
+
 def run_options(dtype=None, **kw):
     """Context manager: run the enclosed HIP ops under per-call options (runtime.HVOptions --
     kernel variants, restructurings) instead of the defaults; nothing process-global changes."""

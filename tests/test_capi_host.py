@@ -96,3 +96,60 @@ def test_pil_resample_tables_match_oracle():
             np.testing.assert_array_equal(t[o:o + arr.size], arr.reshape(-1))
             o += arr.size
         assert o == n
+
+
+def test_no_process_global_kernel_switches():
+    """Kernel-variant selection is per call (hv_gemm_desc.variant / hv_mhc_fused_args.variant,
+    runtime.HVOptions per model): the library exports no global setters and the package keeps no
+    module-level switches."""
+    from hv_amd import _lib, manifold, vit, ops, detect, backbone
+    lib = _lib.lib()
+    for name in ("hv_gemm_set_path", "hv_gemm_set_big_tile", "hv_gemm_set_force_tile", "hv_gemm_set_smallk",
+                 "hv_mhc_fused_set_variant", "hv_mhc_fused_enable_wide"):
+        assert not hasattr(lib, name), name
+    for mod, names in ((manifold, ("FOLD_MAX_D", "USE_FUSED", "PARALLEL_QKV", "GROUP_QKV")),
+                       (vit, ("CLS_ONLY_LAST_BLOCK",)), (ops, ("SPLITK_ON",)),
+                       (detect, ("_PREP_OVERLAP",)), (backbone, ("_DIRECT_STEM",))):
+        for n in names:
+            assert not hasattr(mod, n), (mod.__name__, n)
+
+
+def test_version_watch_sees_every_storage_change():
+    """runtime.VersionWatch (the graph / frozen-coefficient staleness check): in-place updates,
+    `.data` swaps, buffer re-registration, `_buffers[...]` rebinding (what `.to()` does, no hook)
+    and a rebound OUTPUT buffer (one the forward writes, e.g. a Sinkhorn history) all change the
+    snapshot; writing into an output buffer in place does not."""
+    import torch.nn as nn
+    from hv_amd.runtime import VersionWatch
+
+    class Leaf(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = nn.Parameter(torch.randn(4))
+            self.register_buffer("running_mean", torch.zeros(4))
+            self.register_buffer("convergence_history", torch.zeros(3))
+
+    root = nn.Sequential(Leaf(), Leaf())
+    vw = VersionWatch(root)
+    s0 = vw.snapshot()
+    assert vw.snapshot() == s0
+    root[1].convergence_history.add_(1.0)               # the forward writes its history: no change
+    assert vw.snapshot() == s0
+    def inplace():
+        with torch.no_grad():
+            root[0].w.mul_(2.0)
+    steps = [inplace,                                                             # optimizer-style in place
+             lambda: setattr(root[0].w, "data", root[0].w.data.clone()),          # .data swap
+             lambda: root[1].running_mean.add_(1.0),                              # input buffer in place
+             lambda: setattr(root[1], "running_mean", torch.ones(4)),             # re-registration
+             lambda: root[0]._buffers.__setitem__("running_mean", torch.ones(4)), # .to()-style rebind
+             lambda: setattr(root[1], "convergence_history", torch.zeros(3)),     # output buffer rebound
+             lambda: root[0]._buffers.__setitem__("convergence_history", torch.zeros(3))]
+    prev = s0
+    keep = []
+    for i, step in enumerate(steps):
+        keep.append([b for m in root for b in m._buffers.values()])   # old storage stays alive: fresh pointers
+        step()
+        cur = vw.snapshot()
+        assert cur != prev, f"step {i} not detected"
+        prev = cur

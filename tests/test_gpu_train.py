@@ -600,6 +600,89 @@ def test_base_train_step_matches_reference_fixture(gpu_device):
     assert not bad, bad[:10]
 
 
+def _group_norms(named_norms):
+    """Gradient norm per (top-level module, clip group): sqrt of the summed squared per-parameter
+    norms; the clip groups are the trainer's (mhc_trainer.py:342-383: mHC parameters / others)."""
+    from hv_amd.trainer import mhc_group
+    acc = {}
+    for n, v in named_norms:
+        key = f"{n.split('.')[0]}/{'mhc' if mhc_group(n) == 0 else 'other'}"
+        acc[key] = acc.get(key, 0.0) + float(v) ** 2
+    return {k: v ** 0.5 for k, v in acc.items()}
+
+
+def _base_train_step(gpu_device, precision, B, S, seed_x, target_seed):
+    from conftest import formula_state_dict
+    from hv_amd import HybridVisionSystem
+    from hv_amd.targets import synthetic_targets
+    m = HybridVisionSystem(dict(verbose=False, precision=precision))
+    m.load_state_dict(formula_state_dict("base", "wc"))
+    m = m.to(gpu_device).train()
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            mod.p = 0.0
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(seed_x)).to(gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=target_seed)]
+    out = m(x, targets=tg, compute_loss=True)
+    out["loss"]["total_loss"].backward()
+    torch.cuda.synchronize()
+    loss = {k: float(v) for k, v in out["loss"].items() if torch.is_tensor(v) and v.numel() == 1}
+    preds = {k: v.detach().float().cpu().numpy() for k, v in out["predictions"].items()}
+    norms, finite = [], True
+    for n, p in m.named_parameters():
+        if p.grad is not None:
+            finite &= bool(torch.isfinite(p.grad).all())
+            norms.append((n, p.grad.detach().double().norm().item()))
+    del out, m
+    torch.cuda.empty_cache()
+    return loss, preds, dict(norms), finite
+
+
+def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
+    """Config C's object in its own precision: the base model's bf16 training step (bf16
+    activations / GEMMs, fp32 parameters, coefficients and reductions -- the reference's autocast
+    contract, manifold_layers.py:186,248; loss yolo_head.py:374-465) at
+      (1) 224x224 B=2 against the reference fixture train_base_224_b2 (its fp64 run): total loss,
+          and the gradient norm of every (top-level module, clip group) -- the quantities the
+          trainer's per-group clipping (mhc_trainer.py:342-383) acts on;
+      (2) 640x640 B=2 (config C's resolution) against the fp32 HIP step on the same batch:
+          loss components, per-group gradient norms, finiteness of every gradient.
+    Bounds: this forward is ill-conditioned in train mode (the reference's OWN fp32 run is 9%
+    rel-L2 from fp64 on the head logits); bf16 rounding is 2^16x fp32's, so the bounds are set
+    from the measured bf16 step (2x the measured worst, recorded in
+    gpurun_out/parity/train_bf16_base.json): loss within 5%, group norms within 15%."""
+    import json
+    import os
+    from conftest import GOLDEN, golden, record_parity
+    g = golden("train_base_224_b2")
+    names = json.load(open(os.path.join(GOLDEN, "train_base_param_names.json")))
+    B, S = int(g["B"]), int(g["S"])
+    loss16, _, n16, fin16 = _base_train_step(gpu_device, "bf16", B, S, 1, int(g["target_seed"]))
+    assert fin16
+    ref_groups = _group_norms([(n, v) for n, v in zip(names, g["grad_norm_f64"]) if v >= 0])
+    my_groups = _group_norms(n16.items())
+    l64 = float(g["total_loss_f64"])
+    rec = {"224_b2_vs_ref_f64": {"loss_rel": abs(loss16["total_loss"] / l64 - 1),
+                                 "group_norm_rel": {k: abs(my_groups.get(k, 0.0) / v - 1) for k, v in ref_groups.items()
+                                                    if v > 0}}}
+    # (2) config C's resolution: bf16 vs fp32 HIP on the same batch
+    loss32, p32, n32, fin32 = _base_train_step(gpu_device, "fp32", 2, 640, 7, 11)
+    loss16b, p16b, n16b, fin16b = _base_train_step(gpu_device, "bf16", 2, 640, 7, 11)
+    assert fin32 and fin16b
+    g32, g16 = _group_norms(n32.items()), _group_norms(n16b.items())
+    rec["640_b2_bf16_vs_fp32"] = {
+        "loss_rel": {k: abs(loss16b[k] / loss32[k] - 1) for k in loss32 if abs(loss32[k]) > 1e-6},
+        "group_norm_rel": {k: abs(g16.get(k, 0.0) / v - 1) for k, v in g32.items() if v > 0},
+        "logits_rel_l2": {k: float(np.linalg.norm(p16b[k] - p32[k]) / np.linalg.norm(p32[k])) for k in p32}}
+    record_parity("train_bf16_base", rec)
+    r1, r2 = rec["224_b2_vs_ref_f64"], rec["640_b2_bf16_vs_fp32"]
+    assert r1["loss_rel"] < 0.05, r1
+    assert max(r1["group_norm_rel"].values()) < 0.15, r1
+    assert r2["loss_rel"]["total_loss"] < 0.05, r2
+    assert max(r2["group_norm_rel"].values()) < 0.15, r2
+    assert set(g16) == set(g32)
+
+
 def test_tiny_train_step_bf16_runs_and_agrees(gpu_device):
     """bf16 activations through the whole training step.  The model's gradient at init is so
     ill-conditioned that the oracle's own fp32 gradients are ~1% (median) away from fp64
@@ -620,6 +703,33 @@ def test_tiny_train_step_bf16_runs_and_agrees(gpu_device):
     for p in m16.parameters():
         if p.grad is not None:
             assert torch.isfinite(p.grad).all()
+
+
+def test_fused_adamw_per_parameter_steps_match_torch(gpu_device):
+    """A parameter without gradient for the first steps keeps its own step count: its AdamW
+    bias correction 1 - beta^t uses that count (torch.optim.AdamW state['step']), not the
+    optimizer's global step; the state_dict reports the same counts as torch."""
+    from hv_amd.trainer import FusedAdamW
+    torch.manual_seed(1)
+    named = [("a.conv.weight", torch.randn(300)), ("b.bias", torch.randn(7)), ("c.mhc.H_res_raw", torch.randn(5, 5))]
+    mine = [(n, t.clone().to(gpu_device).requires_grad_(True)) for n, t in named]
+    ref = [(n, t.clone().requires_grad_(True)) for n, t in named]
+    opt = FusedAdamW(mine, lr=1e-2, weight_decay=1e-2)
+    topt = torch.optim.AdamW([p for _, p in ref], lr=1e-2, weight_decay=1e-2, eps=1e-8)
+    for step in range(5):
+        active = (True, step >= 2, step % 2 == 0)
+        for i, ((_, p), (_, q)) in enumerate(zip(mine, ref)):
+            gr = torch.randn_like(q)
+            p.grad = gr.clone().to(gpu_device)
+            q.grad = gr.clone() if active[i] else None
+        opt.step(clip=False, active=active)
+        topt.step()
+    for (n, a), (_, b) in zip(mine, ref):
+        assert rel(a.detach(), b.detach()) < 1e-5, n
+    tsd, msd = topt.state_dict()["state"], opt.state_dict()["state"]
+    assert set(tsd) == set(msd)
+    for i in tsd:
+        assert float(tsd[i]["step"]) == float(msd[i]["step"]), i
 
 
 def test_trainer_step_reduces_loss(gpu_device):
