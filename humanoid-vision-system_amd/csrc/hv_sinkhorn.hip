@@ -417,9 +417,13 @@ extern "C" size_t hv_sinkhorn_work_floats(int batch, int n, int m, int iters) {
 }
 
 namespace {
-int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipStream_t s) {
+size_t sk_small_lds(int max_iters) {
   // the small entries: one workgroup each, every iteration inside (LDS: a, b, partials, history)
-  const size_t lds = (size_t)(512 + SKG * 256 + (max_iters > 0 ? max_iters : 1) * 256) * sizeof(float);
+  return (size_t)(512 + SKG * 256 + (max_iters > 0 ? max_iters : 1) * 256) * sizeof(float);
+}
+
+int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipStream_t s) {
+  const size_t lds = sk_small_lds(max_iters);
   if (lds > 160 * 1024) return HV_EUNSUPPORTED;
   static std::once_flag attr;
   std::call_once(attr, [] {
@@ -430,9 +434,9 @@ int sk_launch_small(const hv_sinkhorn_entry* tab, int count, int max_iters, hipS
   return HV_OK;
 }
 
+// sm: entries up to sm x sm (batch 1) are the single-workgroup kernel's and skipped here; 0 = none
 int sk_launch_large(const hv_sinkhorn_entry* tab, int count, int total_rows, int total_row_blocks, int total_cols,
-                    int max_iters, hipStream_t s) {
-  const int sm = 256;
+                    int max_iters, hipStream_t s, int sm = 256) {
   sk_init<<<hv_cdiv(total_rows, 4), 256, 0, s>>>(tab, count, total_rows, sm);
   sk_init_cols<<<hv_cdiv(total_cols, 256), 256, 0, s>>>(tab, count, total_cols, sm);
   HV_CHECK_LAUNCH();
@@ -459,12 +463,23 @@ extern "C" int hv_sinkhorn_group_forward_part(const hv_sinkhorn_entry* tab, int 
   if (!tab || count <= 0 || total_rows <= 0 || max_iters < 0 || part < 0 || part > 2) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hv_diag_count(HV_KF_SINKHORN_GROUP);
+  // more iterations than the single-workgroup kernel's LDS history holds: part 0 runs every
+  // entry through the grouped passes instead; part 1 (small entries alone) cannot
+  const bool small_fits = sk_small_lds(max_iters) <= 160 * 1024;
+  if (part == 0 && !small_fits)
+    return sk_launch_large(tab, count, total_rows, total_row_blocks, total_cols, max_iters, s, 0);
   if (part != 2) {
     const int rc = sk_launch_small(tab, count, max_iters, s);
     if (rc != HV_OK) return rc;
   }
   if (part != 1) return sk_launch_large(tab, count, total_rows, total_row_blocks, total_cols, max_iters, s);
   return HV_OK;
+}
+
+extern "C" int hv_sinkhorn_small_max_iters(void) {
+  int it = 1;
+  while (sk_small_lds(it + 1) <= 160 * 1024) ++it;
+  return it;
 }
 
 

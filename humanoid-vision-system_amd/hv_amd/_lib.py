@@ -125,6 +125,7 @@ _SIGS = {
     "hv_sinkhorn_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_forward": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "hv_sinkhorn_group_forward_part": ([vp, i32, i32, i32, i32, i32, i32, vp], i32),
+    "hv_sinkhorn_small_max_iters": ([], i32),
     "hv_gemm": ([vp, vp], i32),
     "hv_row_stats": ([i32, vp, i64, i32, i32, f32, vp, vp, vp], i32),
     "hv_layernorm": ([i32, vp, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp], i32),

@@ -215,6 +215,9 @@ class ManifoldHyperConnection(nn.Module):
         for lyr in (self.mlp[0], self.mlp[3]):                         # :199-203
             nn.init.xavier_uniform_(lyr.weight, gain=math.sqrt(2))
             nn.init.zeros_(lyr.bias)
+        # the eigenvalue solves queued by monitor_stability land before anyone reads the
+        # buffers through state_dict() / checkpoints (the reference writes them every forward)
+        self.register_state_dict_pre_hook(lambda *_a, **_k: flush_stability())
 
     @property
     def dtype(self):

@@ -321,9 +321,6 @@ def rmsnorm(x: Tensor, scale: Tensor, eps: float = 1e-8) -> Tensor:
 
 
 # ---------------------------------------------------------------------------- sinkhorn
-SINKHORN_SPLIT = False  # small / large entries on two streams (graph branches): measured 0.1 ms slower
-
-
 class SinkhornGroup:
     """A device table of Sinkhorn problems launched together (hv_sinkhorn_group_forward).
 
@@ -377,7 +374,6 @@ class SinkhornGroup:
             rbs_l += el.batch * ((el.n + 15) // 16)
             cs_l += el.batch * el.m
         self.totals_large = (rs_l, rbs_l, cs_l)
-        self._side = None
         self.table = None
         self.table_large = None
         self._raw_ptrs = None
@@ -398,32 +394,21 @@ class SinkhornGroup:
         lib = L.lib()
         mx = max(self.iters)
 
-        def small():
+        if self.has_small and mx > lib.hv_sinkhorn_small_max_iters():
+            # too many iterations for the single-workgroup kernel's LDS history: every entry
+            # through the grouped passes (part 0 on the full table)
+            rs, rbs, cs = self.totals
+            check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs, mx, 0,
+                                                     stream_ptr()), "hv_sinkhorn_group_forward")
+            return self.outs
+        if self.has_small:          # small matrices: one workgroup each, all iterations in one launch
             rs, rbs, cs = self.totals
             check(lib.hv_sinkhorn_group_forward_part(self.table.data_ptr(), len(self.entries), rs, rbs, cs, mx, 1,
                                                      stream_ptr()), "hv_sinkhorn_group_forward_part")
-
-        def large():
+        if self.has_large:          # the grouped row / column passes over the large entries' table
             rs, rbs, cs = self.totals_large
             check(lib.hv_sinkhorn_group_forward_part(self.table_large.data_ptr(), len(self._large_idx), rs, rbs,
                                                      cs, mx, 2, stream_ptr()), "hv_sinkhorn_group_forward_part")
-
-        if SINKHORN_SPLIT and self.has_small and self.has_large:
-            # small matrices (one workgroup each) on a side stream beside the grouped passes of the
-            # large ones: two branches of a captured graph
-            main = torch.cuda.current_stream()
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self.device)
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                small()
-            large()
-            main.wait_stream(self._side)
-        else:
-            if self.has_small:
-                small()
-            if self.has_large:
-                large()
         return self.outs
 
 

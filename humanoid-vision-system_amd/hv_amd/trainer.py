@@ -87,6 +87,14 @@ class GradBuckets:
         self._pending: List = []
         self._ready = [set() for _ in self.buckets]
         self._flushed = [False] * len(self.buckets)
+        self._reduced = [False] * len(self.buckets)
+        # Collective order must be identical on every rank.  A bucket is reduced from the hooks
+        # (overlapping the backward) only if EVERY rank completed it through the hooks on the
+        # previous step (`agreed`, all-reduced MIN in finish()), and agreed buckets are issued in
+        # bucket order; finish() then issues the agreed buckets still open, then the others, each
+        # in bucket order.  Step 1 (nothing agreed yet) reduces everything in finish().
+        self.agreed = [False] * len(self.buckets)
+        self._next = 0
         # which parameters received a gradient this step: the optimizer skips the others like
         # torch.optim skips grad=None (optimizer.py:144)
         self.received = [False] * len(self.params)
@@ -137,11 +145,22 @@ class GradBuckets:
                 g.record_stream(torch.cuda.current_stream())
 
     def _reduce(self, i: int) -> None:
+        self._reduced[i] = True
         if self.world > 1:
             lo, hi = self._span(i)
             view = self.flat[lo:hi]
             view.div_(self.world)
             self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def _issue_agreed(self) -> None:
+        """Reduce the agreed buckets in bucket order, as far as they are flushed."""
+        while self._next < len(self.buckets):
+            i = self._next
+            if self.agreed[i]:
+                if not self._flushed[i]:
+                    return
+                self._reduce(i)
+            self._next += 1
 
     def _on_grad(self, p: Tensor):
         i = self.bucket_of[id(p)]
@@ -151,7 +170,7 @@ class GradBuckets:
             self._flushed[i] = True
             for q in self.buckets[i]:            # free the stored gradients now
                 q.grad = self.views[self._index[id(q)]]
-            self._reduce(i)
+            self._issue_agreed()
 
     def zero(self):
         """Start a step: flat buffer zeroed (one fill), every param.grad set to None so the
@@ -162,22 +181,41 @@ class GradBuckets:
         self.received = [False] * len(self.params)
         self._ready = [set() for _ in self.buckets]
         self._flushed = [False] * len(self.buckets)
+        self._reduced = [False] * len(self.buckets)
+        self._next = 0
         self._pending = []
 
     def finish(self):
-        """Flush and reduce the buckets not completed by the hooks (parameters that got no
-        gradient: every rank reduces the same spans, so ranks stay in lock-step), wait for the
-        all-reduces, and point every param.grad at its flat view."""
-        for i, b in enumerate(self.buckets):
-            if not self._flushed[i]:
-                self._flush(b)
-                self._flushed[i] = True
+        """Flush and reduce the buckets not reduced from the hooks -- the agreed ones still open
+        first, then the rest, each in bucket order, so every rank issues the same collectives in
+        the same order -- wait for the all-reduces, and point every param.grad at its flat view.
+        With world > 1 the received-gradient flags are OR-ed over ranks (one small all-reduce),
+        so every replica skips exactly the parameters no rank produced a gradient for, and the
+        buckets every rank completed through the hooks become next step's agreed set."""
+        hooked = [self._flushed[i] for i in range(len(self.buckets))]
+        for agreed_pass in (True, False):
+            for i, b in enumerate(self.buckets):
+                if self.agreed[i] != agreed_pass or self._reduced[i]:
+                    continue
+                if not self._flushed[i]:
+                    self._flush(b)
+                    self._flushed[i] = True
                 self._reduce(i)
         for w in self._pending:
             w.wait()
         self._pending = []
         for p, v in zip(self.params, self.views):
             p.grad = v
+        if self.world > 1:
+            flags = torch.tensor([int(r) for r in self.received] + [1 - int(h) for h in hooked],
+                                 dtype=torch.int32, device=self.flat.device)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+            f = flags.tolist()
+            n = len(self.params)
+            self.received = [bool(v) for v in f[:n]]
+            self.agreed = [v == 0 for v in f[n:]]
+        else:
+            self.agreed = hooked
 
 
 class FusedAdamW:
@@ -324,6 +362,7 @@ class HVTrainer:
                 if b is not None:
                     by_dtype.setdefault(b.dtype, []).append((mod, name, b))
         flats = []
+        self._buf_views = []
         for dt, entries in by_dtype.items():
             total = sum(b.numel() for _, _, b in entries)
             flat = torch.empty(total, device=entries[0][2].device, dtype=dt)
@@ -333,6 +372,7 @@ class HVTrainer:
                     v = flat[off:off + b.numel()].view_as(b)
                     v.copy_(b)
                     mod._buffers[name] = v
+                    self._buf_views.append((mod, name, v.data_ptr()))
                     off += b.numel()
             flats.append(flat)
         from .runtime import _bump_generation
@@ -353,8 +393,21 @@ class HVTrainer:
             if not t.is_floating_point():
                 dist.broadcast(t, 0, group=self.group)
 
+    def _buffers_still_flat(self) -> bool:
+        """True while every buffer is still the view of the flat tensor it was bound to
+        (model.to(), .float() or a buffer assignment rebinds buffers and would silently stop the
+        per-step broadcast from reaching them)."""
+        for mod, name, ptr in self._buf_views:
+            b = mod._buffers.get(name)
+            if b is None or b.data_ptr() != ptr:
+                return False
+        return True
+
     def step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
         self.model.train()
+        if self._buf_flats and not self._buffers_still_flat():
+            self._buf_flats = self._flatten_buffers()   # re-bind (the ranks do it in lock-step:
+            # every rank sees the same module tree changes)
         for flat in self._buf_flats:               # DDP broadcast_buffers: rank 0's buffers
             dist.broadcast(flat, 0, group=self.group)
         self.grads.zero()
@@ -363,6 +416,8 @@ class HVTrainer:
         loss["total_loss"].backward()
         self.grads.finish()
         self.opt.step(clip=True, active=self.grads.received)
+        from .manifold import flush_stability
+        flush_stability()                          # monitors' eigenvalue buffers current after every step
         return loss
 
 

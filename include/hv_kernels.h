@@ -69,6 +69,10 @@ int hv_sinkhorn_group_forward(const hv_sinkhorn_entry* dev_table, int count,
 int hv_sinkhorn_group_forward_part(const hv_sinkhorn_entry* tab, int count, int total_rows,
                                    int total_row_blocks, int total_cols, int max_iters, int part,
                                    hv_stream_t stream);
+/* The single-workgroup kernel keeps the per-iteration row-sum history in LDS: up to this many
+   iterations.  Beyond it part 0 runs every entry through the grouped passes (any iteration
+   count, as the reference accepts) and part 1 returns HV_EUNSUPPORTED. */
+int hv_sinkhorn_small_max_iters(void);
 
 /* ------------------------------------------------------------------------------------
  * MFMA GEMM with fused prologue/epilogue:  C[M,N] = epi( A'[M,K] . B[N,K]^T )

@@ -210,3 +210,90 @@ def test_hvtrainer_ddp_broadcast_and_average():
         assert len(calls) == 2
         for act in calls:
             assert dict(zip(names, act)) == {n: not n.startswith("unused.") for n in names}
+
+
+class DivNet(torch.nn.Module):
+    """A parameter whose use is data-dependent: `c` gets a gradient only on some ranks/steps."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 8)
+        self.c = torch.nn.Linear(32, 8)
+        self.d = torch.nn.Linear(8, 8)
+
+    def forward(self, x, use_c):
+        h = torch.relu(self.a(x))
+        y = self.b(h)
+        if use_c:
+            y = y + self.c(h)
+        return self.d(y)
+
+
+def _use_c(rank, step):
+    return (rank == 1 and step != 1) or step == 3
+
+
+def _div_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, PKG]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hv_amd.trainer import GradBuckets
+        torch.manual_seed(0)
+        net = DivNet()
+        gb = GradBuckets(list(net.named_parameters()), bucket_bytes=256)   # ~one bucket per parameter
+        res = []
+        for step in range(4):
+            gb.zero()
+            torch.manual_seed(100 + 10 * rank + step)
+            net(torch.randn(6, 16), _use_c(rank, step)).pow(2).sum().backward()
+            gb.finish()
+            res.append({"grads": {n: p.grad.detach().clone().numpy() for n, p in net.named_parameters()},
+                        "received": list(gb.received), "agreed": list(gb.agreed)})
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradbuckets_data_dependent_gradients_stay_in_lockstep():
+    """A parameter that gets a gradient on one rank only (data-dependent use): the bucketed
+    all-reduces are issued in the same order on every rank (hook-driven only for buckets every
+    rank completed through the hooks the step before, in bucket order), the averaged gradient is
+    exact, and the received-gradient flags are OR-ed over ranks so both replicas' optimizers
+    update (or skip) the same parameters."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_div_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    ref = DivNet()
+    names = [n for n, _ in ref.named_parameters()]
+    for step in range(4):
+        acc = {n: torch.zeros_like(p) for n, p in ref.named_parameters()}
+        used = False
+        for r in range(world):
+            ref.zero_grad()
+            torch.manual_seed(100 + 10 * r + step)
+            ref(torch.randn(6, 16), _use_c(r, step)).pow(2).sum().backward()
+            used |= _use_c(r, step)
+            for n, p in ref.named_parameters():
+                if p.grad is not None:
+                    acc[n] += p.grad
+        for r in range(world):
+            got = results[r][step]
+            for n in names:
+                torch.testing.assert_close(torch.from_numpy(got["grads"][n]), acc[n] / world, rtol=1e-5, atol=1e-6)
+            rec = dict(zip(names, got["received"]))
+            assert rec["c.weight"] == rec["c.bias"] == used
+            assert all(rec[n] for n in names if not n.startswith("c."))
+        assert results[0][step]["received"] == results[1][step]["received"]
+        assert results[0][step]["agreed"] == results[1][step]["agreed"]

@@ -65,6 +65,30 @@ def test_sinkhorn_grouped_equals_single(gpu_device):
         assert torch.equal(M, o[0])
 
 
+def test_sinkhorn_many_iterations_falls_back_to_grouped_passes(gpu_device):
+    """More iterations than the single-workgroup kernel's LDS history holds
+    (hv_sinkhorn_small_max_iters): the whole group runs through the grouped passes -- any
+    iteration count works, as in the reference -- and a small entry with few iterations in the
+    same group is unaffected; matrices and histories vs the oracle in fp64."""
+    import math
+    ops = _ops()
+    from hv_amd import _lib, SinkhornKnoppProjection
+    from oracle import hv_oracle as O
+    it = _lib.lib().hv_sinkhorn_small_max_iters() + 24
+    raws = [cases.sinkhorn_raw(D, 20, "wc") for D in (48, 64, 300)]
+    iters = [it, 5, it]
+    grp = ops.SinkhornGroup([r.to(gpu_device) for r in raws], iters, gpu_device)
+    outs = [o.clone().cpu() for o in grp.run()]
+    for r, n, o, h in zip(raws, iters, outs, grp.hists):
+        hist = torch.zeros(n, dtype=torch.float64)
+        ref = O.sinkhorn(r.double(), n, history=hist)
+        assert (o[0].double() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item()), n
+        np.testing.assert_allclose(h[:n].cpu().numpy(), hist.numpy(), rtol=1e-3, atol=2e-6)
+    sk = SinkhornKnoppProjection(num_iterations=150).to(gpu_device)       # module level, D=64
+    M = sk(cases.sinkhorn_raw(64, 20, "init").to(gpu_device)).cpu()
+    assert math.isclose(float(M.sum(0).mean()), 1.0, rel_tol=1e-4)
+
+
 def test_sinkhorn_reference_properties(gpu_device):
     """test_models.py:33-56 / :85-100: doubly stochastic within rtol 1e-4, deterministic."""
     from hv_amd import SinkhornKnoppProjection
