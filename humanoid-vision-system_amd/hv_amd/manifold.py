@@ -195,9 +195,11 @@ class ManifoldHyperConnection(nn.Module):
         self.use_mixed_precision = use_mixed_precision
         self.dropout_rate = dropout_rate
         D, Hd = input_dim, self.hidden_dim
-        self.H_pre_raw = nn.Parameter(torch.empty(D, Hd))
-        self.H_post_raw = nn.Parameter(torch.empty(Hd, D))
-        self.H_res_raw = nn.Parameter(torch.empty(D, D))
+        # torch.randn * alpha first (manifold_layers.py:149-157): the Xavier re-init below
+        # overwrites the values, but the draws keep a seeded model's RNG stream the reference's
+        self.H_pre_raw = nn.Parameter(torch.randn(D, Hd) * alpha)
+        self.H_post_raw = nn.Parameter(torch.randn(Hd, D) * alpha)
+        self.H_res_raw = nn.Parameter(torch.randn(D, D) * alpha)
         self.sinkhorn = SinkhornKnoppProjection(sk_iterations)
         self.mlp = nn.Sequential(nn.Linear(Hd, 2 * Hd), nn.GELU(), nn.Dropout(dropout_rate),
                                  nn.Linear(2 * Hd, Hd), nn.GELU(), nn.Dropout(dropout_rate))

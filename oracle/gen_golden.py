@@ -453,6 +453,8 @@ def main():
         gen_nms(yh)
     if "preproc" in parts:
         gen_preproc()
+    if "seeded" in parts:
+        gen_seeded_init(hv)
 
 
 
@@ -471,6 +473,37 @@ def gen_layout(hv):
         anchors = model.detection_head.anchor_generator.anchors
         np.save(os.path.join(OUT, "anchors.npy"), anchors.numpy())
         print(f"  wrote {path} ({len(lay)} entries)")
+
+
+def gen_seeded_init(hv):
+    """Parameter values of the reference model built right after torch.manual_seed(0)
+    (hybrid_vision.py:53-197 and every submodule constructor: the RNG draws of each
+    torch.randn / nn.Linear / nn.Conv2d default init before the explicit re-inits).  Per
+    state_dict entry (state_dict_<tag>.json order): the first 8 and last 4 flattened values and
+    the fp64 sum and sum of squares."""
+    import json
+    for tag, tiny in (("tiny", True), ("base", False)):
+        _TINY["on"] = tiny
+        torch.manual_seed(0)
+        model = hv.HybridVisionSystem({})
+        _TINY["on"] = False
+        names = [k for k, _, _ in json.load(open(os.path.join(OUT, f"state_dict_{tag}.json")))]
+        sd = model.state_dict()
+        P = len(names)
+        head = np.full((P, 8), np.nan, dtype=np.float32)
+        tail = np.full((P, 4), np.nan, dtype=np.float32)
+        s1 = np.zeros(P, dtype=np.float64)
+        s2 = np.zeros(P, dtype=np.float64)
+        for i, n in enumerate(names):
+            v = sd[n].detach().reshape(-1)
+            if not v.is_floating_point():
+                v = v.double()
+            v = v.double()
+            head[i, :min(8, v.numel())] = v[:8].float().numpy()
+            tail[i, :min(4, v.numel())] = v[-4:].float().numpy() if v.numel() else []
+            s1[i] = float(v.sum())
+            s2[i] = float((v * v).sum())
+        save(f"seeded_init_{tag}", head=head, tail=tail, s1=s1, s2=s2)
 
 
 if __name__ == "__main__":

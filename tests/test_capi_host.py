@@ -153,3 +153,33 @@ def test_version_watch_sees_every_storage_change():
         cur = vw.snapshot()
         assert cur != prev, f"step {i} not detected"
         prev = cur
+
+
+@pytest.mark.parametrize("tag", ["tiny", "base"])
+def test_seeded_construction_matches_reference(tag):
+    """torch.manual_seed(0); HybridVisionSystem({}) draws the same random numbers in the same
+    order as the reference constructors (torch.randn(...) * alpha for H_pre/H_post/H_res before
+    the Xavier re-init, manifold_layers.py:149-157,194-196; the default nn.Linear / nn.Conv2d
+    inits; hybrid_vision.py:183-197's re-inits), so a seeded fresh model equals the
+    reference's: fixture tests/golden/seeded_init_<tag>.npz (oracle/gen_golden.py --only seeded)
+    holds the first 8 / last 4 values and the fp64 sum / sum of squares of every entry."""
+    import numpy as np
+    from hv_amd import HybridVisionSystem
+    g = np.load(os.path.join(GOLDEN, f"seeded_init_{tag}.npz"))
+    names = [k for k, _, _ in json.load(open(os.path.join(GOLDEN, f"state_dict_{tag}.json")))]
+    torch.manual_seed(0)
+    m = HybridVisionSystem(dict(MODEL_CFG[tag]))
+    sd = m.state_dict()
+    bad = []
+    for i, n in enumerate(names):
+        v = sd[n].detach().reshape(-1).double()
+        k = min(8, v.numel())
+        head_ok = np.array_equal(v[:k].float().numpy(), g["head"][i, :k])
+        tail_ok = np.array_equal(v[-min(4, v.numel()):].float().numpy(), g["tail"][i, :min(4, v.numel())]) \
+            if v.numel() else True
+        s1, s2 = float(v.sum()), float((v * v).sum())
+        sums_ok = abs(s1 - g["s1"][i]) <= 1e-9 * max(1.0, abs(g["s2"][i]) ** 0.5 * v.numel() ** 0.5) and \
+            abs(s2 - g["s2"][i]) <= 1e-9 * max(1.0, abs(g["s2"][i]))
+        if not (head_ok and tail_ok and sums_ok):
+            bad.append(n)
+    assert not bad, (len(bad), bad[:10])
