@@ -11,5 +11,6 @@ from .vit import (HybridVisionEncoder, PatchEmbedding, TransformerEncoderBlock, 
                   VisionTransformerEncoder)
 from .detect import (FeaturePyramidNetwork, HybridVisionSystem, YOLOAnchorGenerator,  # noqa: F401
                      YOLODecoder, YOLODetectionHead, YOLOLoss, YOLOPredictionHead)
+from . import library  # noqa: F401,E402  (registers the torch.ops.hv.* dispatcher operators)
 
 __version__ = "0.1.0"

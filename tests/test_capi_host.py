@@ -183,3 +183,30 @@ def test_seeded_construction_matches_reference(tag):
         if not (head_ok and tail_ok and sums_ok):
             bad.append(n)
     assert not bad, (len(bad), bad[:10])
+
+
+def test_hv_dispatcher_ops_have_fake_kernels():
+    """torch.ops.hv.* (hv_amd/library.py) are registered with fake kernels: shape propagation
+    under FakeTensorMode works on a machine without a GPU (what torch.compile / torch.export
+    run before any kernel)."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    import hv_amd
+    assert set(hv_amd.library.OPS) <= set(dir(torch.ops.hv))
+    with FakeTensorMode():
+        f = lambda *s, dt=torch.float32: torch.empty(*s, device="cuda", dtype=dt)   # noqa: E731
+        D, Hd = 64, 256
+        x = f(100, D, dt=torch.bfloat16)
+        assert torch.ops.hv.mhc(x, f(D, Hd), f(Hd, D), f(D, D), f(D), f(D), f(2 * Hd, Hd), f(2 * Hd), f(Hd, 2 * Hd),
+                                f(Hd), f(D), f(D), 20).shape == (100, D)
+        M, h = torch.ops.hv.sinkhorn(f(3, 16, 16), 7, 1e-8, 1.0)
+        assert M.shape == (3, 16, 16) and h.shape == (7,)
+        assert torch.ops.hv.linear(x, f(96, D), None, "gelu").shape == (100, 96)
+        assert torch.ops.hv.conv_bn_act(f(2, 40, 40, 32, dt=torch.bfloat16), f(64, 32, 3, 3), None, f(64), f(64),
+                                        f(64), f(64), 2, 1, "silu", 1e-5).shape == (2, 20, 20, 64)
+        assert torch.ops.hv.attention(f(2, 9, 256), f(2, 9, 256), f(2, 9, 256), 8).shape == (2, 9, 256)
+        outs = torch.ops.hv.yolo_decode(f(2, 8, 8, 255), 3, 80, f(3, 2))
+        assert [tuple(t.shape) for t in outs] == [(2, 3, 8, 8, 85), (2, 3, 8, 8, 4), (2, 3, 8, 8, 80), (2, 3, 8, 8),
+                                                  (2, 3, 8, 8), (2, 3, 8, 8, 1)]
+        assert outs[4].dtype == torch.int64
+        b, s, l, c = torch.ops.hv.nms([f(2, 3, 8, 8, 4)], [f(2, 3, 8, 8)], [f(2, 3, 8, 8, dt=torch.int64)], 0.5, 0.5, 50)
+        assert b.shape == (2, 50, 4) and l.dtype == torch.int64 and c.shape == (2,)
