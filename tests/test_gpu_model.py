@@ -337,7 +337,7 @@ def test_streaming_640_b1_frozen_graph_and_pipeline(gpu_device):
                        "fp32_top_matched_by_bf16_box_iou_0.5": round(frac, 4),
                        "label_agreement_of_matched": round(same_label / max(matched_all, 1), 4)}
     record_parity("streaming_640_b1", rec)
-    assert n_all == 0 or frac >= 0.6, rec["pipeline"]
+    assert n_all == 0 or frac >= 0.7, rec["pipeline"]     # measured 0.86 (label agreement 0.95)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
