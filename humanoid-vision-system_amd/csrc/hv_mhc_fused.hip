@@ -61,11 +61,26 @@ struct Cfg {
 // 64-byte rows (W2 / Wc^T chunks): 16-B chunk c of row r lives at c ^ ((r >> 2) & 3), which
 // makes the permuted 8-byte fragment reads (ds_read_b64, 32-lane groups) conflict-free.
 __device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+// An 8-byte fragment read kept a ds_read_b64.  Left to itself the compiler pairs the reads of
+// rows r and r + 16 (1 KiB apart) into ds_read2st64_b64, whose bank map is (a/4) mod 32 in
+// 16-lane groups: there this pattern is 2-way conflicted (rocprofv3 SQ_LDS_BANK_CONFLICT: 45% of
+// the LDS cycles of the D = 32 / 64 kernels).  A volatile access is never merged.
+template <bool NOMERGE>
+__device__ __forceinline__ uint2 lds_b64(const unsigned char* p) {
+  if constexpr (NOMERGE) {
+    typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
+    const unsigned long long v = *(lds_u64*)(p);
+    return make_uint2((unsigned)v, (unsigned)(v >> 32));
+  } else {
+    return *reinterpret_cast<const uint2*>(p);
+  }
+}
 // A1^T rows (2D bytes, CPA chunks): chunk c of row r at c ^ (r & (CPA - 1)).
 template <int CPA>
 __device__ __forceinline__ int swzA(int r, int c) { return c ^ (r & (CPA - 1)); }
 
-template <int D, int HD, int TB_, int MINB, int NW_ = 8>
+template <int D, int HD, int TB_, int MINB, int NW_ = 8, bool NOMERGE = false>
 __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_kernel(
     const unsigned short* __restrict__ x, int T,
     const unsigned short* __restrict__ a1t,   // [2HD, D]
@@ -204,8 +219,8 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_kernel(
 #pragma unroll
     for (int h = 0; h < C::HT; ++h) {
       const int r = h * 16 + fr;
-      const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
-      const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+      const uint2 lo = lds_b64<NOMERGE>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+      const uint2 hi = lds_b64<NOMERGE>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
       const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
       for (int tb = 0; tb < TB; ++tb) acc2[h][tb] = mfma(af, hb[tb], acc2[h][tb]);
@@ -255,8 +270,8 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_kernel(
 #pragma unroll
         for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, xg[tb], acc3[dt][tb]);
       } else {                                         // h2 part: permuted k order
-        const uint2 lo = *reinterpret_cast<const uint2*>(sb + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
-        const uint2 hi = *reinterpret_cast<const uint2*>(sb + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        const uint2 lo = lds_b64<NOMERGE>(sb + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = lds_b64<NOMERGE>(sb + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
         const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
         for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, h2f[tb], acc3[dt][tb]);
@@ -304,10 +319,10 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_kernel(
   }
 }
 
-template <int D, int HD, int TB, int MINB, int NW = 8>
+template <int D, int HD, int TB, int MINB, int NW = 8, bool NOMERGE = false>
 int launch(const hv_mhc_fused_args* a, hipStream_t s) {
   using C = Cfg<D, HD, TB, NW>;
-  auto k = mhc_fused_kernel<D, HD, TB, MINB, NW>;
+  auto k = mhc_fused_kernel<D, HD, TB, MINB, NW, NOMERGE>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -710,11 +725,13 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   // groups per CU (register cap 170): 2x slower.  Also measured slower: 1.5x tokens per wave
   // (TB 6 / 3, 35-60%) and 2-wave groups (4x) -- all register spills.
   if (a->D == 32) {
+    if (shape == 7) return launch<32, 128, 4, 2, 4, true>(a, s);
     if (shape == 1) return launch<32, 128, 4, 3, 4>(a, s);
     if (shape == 2) return launch<32, 128, 4, 1>(a, s);
     return launch<32, 128, 4, 2, 4>(a, s);
   }
   if (a->D == 64) {
+    if (shape == 7) return launch<64, 256, 2, 2, 4, true>(a, s);
     if (shape == 1) return launch<64, 256, 2, 3, 4>(a, s);
     if (shape == 2) return launch<64, 256, 2, 1>(a, s);
     return launch<64, 256, 2, 2, 4>(a, s);

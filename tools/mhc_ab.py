@@ -26,9 +26,9 @@ def timed(fn, n=5):
 
 
 W = _lib.MV_WIDE
-CASES = {"unfused": HVOptions(use_fused_mhc=False), "fused_v0": HVOptions(mhc_variant=W),
-         "fused_v1": HVOptions(mhc_variant=W | 1), "fused_v2": HVOptions(mhc_variant=W | 2),
-         "fused_v5": HVOptions(mhc_variant=W | 5), "fused_v6": HVOptions(mhc_variant=W | 6)}
+VARIANTS = [int(v) for v in os.environ.get("HV_MHC_VARIANTS", "0,1,2,5,6").split(",")]
+CASES = {"unfused": HVOptions(use_fused_mhc=False)}
+CASES.update({f"fused_v{v}": HVOptions(mhc_variant=W | v) for v in VARIANTS})
 
 for shp in shapes:
     D, T, ex = shp if len(shp) == 3 else (*shp, 4)
