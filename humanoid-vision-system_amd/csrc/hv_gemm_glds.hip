@@ -40,6 +40,29 @@ __device__ __forceinline__ void glds16_asm(const void* src, unsigned lds_addr) {
 }
 #pragma clang diagnostic pop
 
+// Implicit-im2col K position of a 64-wide K-tile when conv_c % 64 == 0 (every conv this path
+// serves but the K-tail ones): the tile lies inside ONE tap, so its source offset
+// ((kh * W + kw) * C + ci) is wave-uniform.  Advanced by one K-tile per call instead of
+// recomputed with per-lane integer divisions (the old address path cost ~130 VALU per K-tile
+// per wave against 32 MFMAs, rocprofv3 + ISA, profiles/r03).
+struct ConvK {
+  int kh, kw, ci;
+  __device__ void init(const hv_gemm_desc& d, int kt) {
+    const int k = kt * 64, tap = k / d.conv_c;
+    ci = k - tap * d.conv_c;
+    kh = tap / d.conv_k;
+    kw = tap - kh * d.conv_k;
+  }
+  __device__ void advance(const hv_gemm_desc& d) {
+    ci += 64;
+    if (ci == d.conv_c) {
+      ci = 0;
+      if (++kw == d.conv_k) { kw = 0; ++kh; }
+    }
+  }
+  __device__ int offset(const hv_gemm_desc& d) const { return (kh * d.conv_w + kw) * d.conv_c + ci; }
+};
+
 template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2, bool SPLIT = false>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   static_assert(NS >= 2 && NS <= 4, "stages");
@@ -95,15 +118,40 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
     brow[i] = (const unsigned short*)d.B + (long)n * d.ldb;
   }
   const int lchunk = pchunk ^ (lrow & 7);   // logical chunk fetched by this lane (rows 8-aligned)
+  // conv fast path (conv_c % 64 == 0): per-lane element offset of the output pixel's (kh, kw) =
+  // (0, 0) input position; a K-tile adds the wave-uniform ConvK offset
+  const bool cfast = CONV && d.conv_c % 64 == 0;
+  int apix[AI];                              // (< 2^31 elements per image on every path)
+  ConvK ck;
+  if constexpr (CONV) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      apix[i] = (aih[i] * d.conv_w + aiw[i]) * d.conv_c + lchunk * 8;
+  }
 
   // DMA of K-tile kt into ring buffer buf (inline asm: the compiler does not track it, so it does
-  // not drain vmcnt before the ds_reads of the other buffers; the loop waits with counted vmcnt)
+  // not drain vmcnt before the ds_reads of the other buffers; the loop waits with counted vmcnt).
+  // Called for consecutive kt (the conv fast path advances ck once per call).
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
   const int wu = __builtin_amdgcn_readfirstlane(wid);
   auto stage = [&](int buf, int kt) {
     const unsigned la = lds0 + buf * STAGE_BYTES + wu * AI * 1024;
     const unsigned lb = lds0 + buf * STAGE_BYTES + BM * ROW + wu * BI * 1024;
     const int k = kt * 64 + lchunk * 8;
+    if (CONV && cfast) {
+      const int koff = ck.offset(d);
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int ih = aih[i] + ck.kh, iw = aiw[i] + ck.kw;
+        const void* src = ((unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
+                              ? (const void*)(arow[i] + apix[i] + koff) : (const void*)hv_glds_zero_line;
+        glds16_asm(src, la + i * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) glds16_asm(brow[i] + k, lb + i * 1024);
+      ck.advance(d);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const void* src;
@@ -146,6 +194,9 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
   // ring of NS buffers, NS-1 K-tiles in flight.  Iteration kt: wait for this wave's DMAs of tile
   // kt (the younger tiles stay in flight), barrier (every wave's tile kt landed, every wave's
   // reads of tile kt-1 retired), refill the buffer of tile kt-1 with tile kt+NS-1, compute kt.
+  if constexpr (CONV) {
+    if (cfast) ck.init(d, kb);
+  }
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) stage(t, kb + t);
@@ -362,6 +413,21 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   }
   const int lchunk = pchunk ^ (lrow & 7);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  // conv fast path (conv_c % 64 == 0): wave-uniform K-tile offsets (ConvK), per-lane pixel base;
+  // ckn = the position of the next K-tile whose A parts are staged (K-tiles are staged in order)
+  int apix[4];
+  ConvK ckn;
+  if constexpr (CONV) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) apix[i] = (aih[i] * d.conv_w + aiw[i]) * d.conv_c + lchunk * 8;
+    ckn.init(d, 0);
+  }
+  auto dma_a_fast = [&](int buf, const ConvK& c, int koff, int i) {
+    const int ih = aih[i] + c.kh, iw = aiw[i] + c.kw;
+    const void* src = ((unsigned)ih < (unsigned)d.conv_h && (unsigned)iw < (unsigned)d.conv_w)
+                          ? (const void*)(arow[i] + apix[i] + koff) : (const void*)hv_glds_zero_line;
+    glds16_asm(src, lds0 + buf * B256_STAGE + arow0[i] * ROW);
+  };
 
   auto dma_a = [&](int buf, int kt, int i) {
     const int k = kt * 64 + lchunk * 8;
@@ -386,9 +452,32 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   auto dma_b = [&](int buf, int kt, int i) {
     glds16_asm(brow[i] + kt * 64 + lchunk * 8, lds0 + buf * B256_STAGE + BM * ROW + brow0[i] * ROW);
   };
-  auto part_tl = [&](int buf, int kt) { dma_a(buf, kt, 0); dma_a(buf, kt, 1); dma_b(buf, kt, 0); dma_b(buf, kt, 1); };
+  // the A parts of K-tile kt: TL (rows 0, 1) then B (rows 2, 3); ckn is advanced after part B
+  // (this kernel only runs convs with K % 64 == 0, i.e. conv_c % 64 == 0: always the fast path)
+  auto part_tl = [&](int buf, int kt) {
+    if constexpr (CONV) {
+      const int koff = ckn.offset(d);
+      dma_a_fast(buf, ckn, koff, 0);
+      dma_a_fast(buf, ckn, koff, 1);
+    } else {
+      dma_a(buf, kt, 0);
+      dma_a(buf, kt, 1);
+    }
+    dma_b(buf, kt, 0);
+    dma_b(buf, kt, 1);
+  };
   auto part_r = [&](int buf, int kt) { dma_b(buf, kt, 2); dma_b(buf, kt, 3); };
-  auto part_b = [&](int buf, int kt) { dma_a(buf, kt, 2); dma_a(buf, kt, 3); };
+  auto part_b = [&](int buf, int kt) {
+    if constexpr (CONV) {
+      const int koff = ckn.offset(d);
+      dma_a_fast(buf, ckn, koff, 2);
+      dma_a_fast(buf, ckn, koff, 3);
+      ckn.advance(d);
+    } else {
+      dma_a(buf, kt, 2);
+      dma_a(buf, kt, 3);
+    }
+  };
 
   const int fr = lane & 15, fg = lane >> 4;
   // fragment reads: A rows wr*128 + half*64 + a*16 + fr, B cols wc*64 + half*32 + b*16 + fr;
@@ -587,7 +676,7 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
     case 2: return launch<64, 128>(d, s);
     case 3: return launch<128, 64>(d, s);
     case 4: return launch<64, 64>(d, s);
-    case 5: if (!d.epi_mode && d.K % 64 == 0) return launch256(d, s); break;
+    case 5: if (!d.epi_mode && d.K % 64 == 0 && d.conv_c % 64 == 0) return launch256(d, s); break;
     case 6: return hv_gemm_smallk(d, s, true);
     default: {
       const int rc = hv_gemm_smallk(d, s, false);             // persistent small-K kernel (hv_gemm_sk.hip)
@@ -599,7 +688,7 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
   // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for
   // the implicit-im2col convolutions (+3..29 %); K = 256 loses everywhere (prologue-bound)
-  if (!d.epi_mode && d.K % 64 == 0 && !(d.variant & HV_GV_NO_BIG) &&
+  if (!d.epi_mode && d.K % 64 == 0 && d.conv_c % 64 == 0 && !(d.variant & HV_GV_NO_BIG) &&
       ((d.variant & HV_GV_BIG_ALWAYS) || (d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);
