@@ -16,3 +16,5 @@ timeout -k 10 200 python tools/model_ab.py default mhc_variant=7 > $OUT/model_ab
 cat $OUT/model_ab.txt
 timeout -k 10 200 python tools/gemm_breakdown.py > $OUT/gemm_breakdown.txt 2>&1 || exit 1
 head -60 $OUT/gemm_breakdown.txt
+HV_SWEEP_ONLY=conv3x3 timeout -k 10 300 python tools/tile_sweep.py > $OUT/tile_sweep_conv.txt 2>&1 || exit 1
+cat $OUT/tile_sweep_conv.txt

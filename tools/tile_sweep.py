@@ -68,8 +68,15 @@ CASES = [
     ("cat 25600x256x(256+1024)", lambda: case_cat(25600, 256, 256, 1024)),
     ("conv1x1 16x40x256->256", lambda: case_conv(16, 40, 256, 256, 1, 1)),
     ("conv3x3 16x80x256->256", lambda: case_conv(16, 80, 256, 256, 3, 1)),
+    ("conv3x3 16x80x256->512", lambda: case_conv(16, 80, 256, 512, 3, 1)),
+    ("conv3x3 16x80x512->256", lambda: case_conv(16, 80, 512, 256, 3, 1)),
+    ("conv3x3 16x40x512->1024", lambda: case_conv(16, 40, 512, 1024, 3, 1)),
+    ("conv3x3 16x40x1024->512", lambda: case_conv(16, 40, 1024, 512, 3, 1)),
     ("conv3x3 16x20x1024->2048", lambda: case_conv(16, 20, 1024, 2048, 3, 1)),
+    ("conv3x3 16x20x2048->1024", lambda: case_conv(16, 20, 2048, 1024, 3, 1)),
 ]
+if os.environ.get("HV_SWEEP_ONLY"):
+    CASES = [c for c in CASES if os.environ["HV_SWEEP_ONLY"] in c[0]]
 print(f"{'case':28s} " + " ".join(f"{n:>9s}" for n in ("auto", "128x128", "64x128", "128x64", "64x64", "256pp")))
 for name, mk in CASES:
     fn, flop = mk()
