@@ -338,6 +338,304 @@ int launch(const hv_mhc_fused_args* a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Software-pipelined per-wave kernel (D = 32, 64).  Same work split and arithmetic as
+// mhc_fused_kernel (bitwise-equal outputs), restructured around what the ISA of that kernel showed:
+//  * its chunk loop waited vmcnt(0) right after issuing the next chunk's DMA (the c1 global loads
+//    in the loop make hipcc drain the whole counter before their first use), so every chunk's
+//    weight DMA was fully exposed;
+//  * GEMM1 -> GELU -> GEMM2 of one chunk is a dependency chain: the ~170 GELU VALU of a chunk
+//    had no MFMAs of the same wave beside them.
+// Here c1 lives in LDS, the DMAs are inline asm (untracked by the compiler, waited with an
+// explicit vmcnt one chunk later), the weight chunks stream through a 3-stage ring, and
+// iteration ch computes GEMM1 + GELU of chunk ch+1 beside GEMM2 of chunk ch (independent
+// instruction streams the scheduler interleaves: matrix pipe || VALU).  Wc^T goes to LDS whole
+// in the last two iterations (the two stages no chunk needs any more), so GEMM3 runs barrier-free.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void mhc_glds16(const void* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int D, int HD, int TB_, int MINB, int NW_, bool NOMERGE>
+__global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
+    const unsigned short* __restrict__ x, int T, const unsigned short* __restrict__ a1t, const float* __restrict__ c1,
+    const unsigned short* __restrict__ w2, const float* __restrict__ b2, const unsigned short* __restrict__ wct,
+    const float* __restrict__ g_post, const float* __restrict__ b_post, const unsigned short* __restrict__ res,
+    unsigned short* __restrict__ out) {
+  using C = Cfg<D, HD, TB_, NW_>;
+  constexpr int TB = C::TB, KC = C::KC, NCH = C::NCH;
+  constexpr int WPS = C::STAGE / C::WCB;                 // Wc^T k-chunks per stage
+  static_assert(NCH >= 3 && C::KS3 <= 2 * WPS, "Wc^T fits the two stages freed by the last chunks");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* const c1s = reinterpret_cast<float*>(smem + 3 * C::STAGE);   // 2HD (+KC pad) floats
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int fr = lane & 15, fg = lane >> 4;
+  const long tw = (long)blockIdx.x * C::BM + w * C::TPW;
+
+  auto issue_chunk = [&](int ch, int st) {
+    const unsigned sa = lds0 + st * C::STAGE, sw = sa + C::A1B;
+#pragma unroll
+    for (int p0 = 0; p0 < KC * C::CPA; p0 += C::NT) {
+      if (p0 + wu * 64 < KC * C::CPA) {
+        const int p = p0 + tid, r = p / C::CPA, pc = p % C::CPA;
+        mhc_glds16(a1t + (long)(ch * KC + r) * D + swzA<C::CPA>(r, pc) * 8, sa + (p0 + wu * 64) * 16);
+      }
+    }
+#pragma unroll
+    for (int p0 = 0; p0 < HD * 4; p0 += C::NT) {
+      if (p0 + wu * 64 < HD * 4) {
+        const int p = p0 + tid, r = p >> 2, pc = p & 3;
+        mhc_glds16(w2 + (long)r * (2 * HD) + ch * KC + swz64(r, pc) * 8, sw + (p0 + wu * 64) * 16);
+      }
+    }
+  };
+  constexpr int WST_A = NCH % 3, WST_B = (NCH + 1) % 3;  // stages chunks NCH, NCH+1 would use
+  auto wc_chunk = [&](int ks) -> int { return (ks < WPS ? WST_A : WST_B) * C::STAGE + (ks % WPS) * C::WCB; };
+  auto issue_wc = [&](int k0, int k1) {                  // Wc^T k-chunks [k0, k1)
+#pragma unroll
+    for (int ks = k0; ks < k1; ++ks) {
+#pragma unroll
+      for (int p0 = 0; p0 < D * 4; p0 += C::NT) {
+        if (p0 + wu * 64 < D * 4) {
+          const int p = p0 + tid, r = p >> 2, pc = p & 3;
+          mhc_glds16(wct + (long)r * (D + HD) + ks * 32 + swz64(r, pc) * 8, lds0 + wc_chunk(ks) + (p0 + wu * 64) * 16);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: x and c1 loaded (c1 -> LDS) before the first DMA, so the compiler's waits for
+  // them never cover a DMA; chunks 0 and 1 in flight under LN_pre -> z fragments
+  uint4 xin[TB][C::KS1];
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb)
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks)
+      xin[tb][ks] = *reinterpret_cast<const uint4*>(x + min(tw + tb * 16 + fr, (long)T - 1) * D + ks * 32 + fg * 8);
+  for (int i = tid; i < 2 * HD; i += C::NT) c1s[i] = c1[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_chunk(0, 0);
+  issue_chunk(1, 1);
+  uint4 zf[TB][C::KS1];
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb) {
+    uint4 xf[C::KS1];
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      xf[ks] = xin[tb][ks];
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += __uint_as_float(wv[e] << 16) + __uint_as_float(wv[e] & 0xffff0000u);
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = __uint_as_float(wv[e] << 16) - mu, b = __uint_as_float(wv[e] & 0xffff0000u) - mu;
+        q += a * a + b * b;
+      }
+    }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rs = rsqrtf(q * (1.0f / D) + 1e-5f);
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks) {
+      const uint32_t wv[4] = {xf[ks].x, xf[ks].y, xf[ks].z, xf[ks].w};
+      uint32_t zv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        zv[e] = pack_bf16x2((__uint_as_float(wv[e] << 16) - mu) * rs, (__uint_as_float(wv[e] & 0xffff0000u) - mu) * rs);
+      zf[tb][ks] = make_uint4(zv[0], zv[1], zv[2], zv[3]);
+    }
+  }
+
+  // GEMM1 (transposed) + GELU of chunk ch from stage ch % 3 -> B fragments of GEMM2 (permuted k)
+  auto gemm1 = [&](int ch, uint4 (&hb)[TB]) {
+    const unsigned char* sa = smem + (ch % 3) * C::STAGE;
+    const float4 cb0 = *reinterpret_cast<const float4*>(c1s + ch * KC + fg * 4);
+    const float4 cb1 = *reinterpret_cast<const float4*>(c1s + ch * KC + 16 + fg * 4);
+    f32x4 g1[2][TB];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const int r = ct * 16 + fr;
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) g1[ct][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < C::KS1; ++ks) {
+        const uint4 af = *reinterpret_cast<const uint4*>(sa + r * (2 * D) + swzA<C::CPA>(r, ks * 4 + fg) * 16);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) g1[ct][tb] = mfma(af, zf[tb][ks], g1[ct][tb]);
+      }
+    }
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb)
+      hb[tb] = make_uint4(pack_bf16x2(hv_gelu_fast(g1[0][tb][0] + cb0.x), hv_gelu_fast(g1[0][tb][1] + cb0.y)),
+                          pack_bf16x2(hv_gelu_fast(g1[0][tb][2] + cb0.z), hv_gelu_fast(g1[0][tb][3] + cb0.w)),
+                          pack_bf16x2(hv_gelu_fast(g1[1][tb][0] + cb1.x), hv_gelu_fast(g1[1][tb][1] + cb1.y)),
+                          pack_bf16x2(hv_gelu_fast(g1[1][tb][2] + cb1.z), hv_gelu_fast(g1[1][tb][3] + cb1.w)));
+  };
+
+  f32x4 acc2[C::HT][TB];
+#pragma unroll
+  for (int h = 0; h < C::HT; ++h)
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb) acc2[h][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                       // chunks 0, 1 and c1 in LDS
+  uint4 hb[TB];
+  gemm1(0, hb);
+
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch > 0) {
+      // this wave's DMAs of chunk ch+1 landed; every wave's reads of iteration ch-1 retired
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (ch + 2 < NCH) issue_chunk(ch + 2, (ch + 2) % 3);
+    else if (ch + 2 == NCH) issue_wc(0, WPS < C::KS3 ? WPS : C::KS3);   // stage NCH % 3
+    else if (WPS < C::KS3) issue_wc(WPS, C::KS3);                     // stage (NCH + 1) % 3
+    // GEMM1 + GELU of chunk ch+1 (the last iteration computes an unused chunk from the Wc stage:
+    // straight-line code, no branch between the two instruction streams)
+    uint4 hn[TB];
+    gemm1(ch + 1 < NCH ? ch + 1 : NCH, hn);
+    // GEMM2 (transposed) of chunk ch: acc2[h] += W2[h*16 + fr][perm k] . h1^T
+    const unsigned char* sw = smem + (ch % 3) * C::STAGE + C::A1B;
+#pragma unroll
+    for (int h = 0; h < C::HT; ++h) {
+      const int r = h * 16 + fr;
+      const uint2 lo = lds_b64<NOMERGE>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+      const uint2 hi = lds_b64<NOMERGE>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+      const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) acc2[h][tb] = mfma(af, hb[tb], acc2[h][tb]);
+    }
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb) hb[tb] = hn[tb];
+  }
+
+  // ---- GEMM3 (transposed): y^T = Wc^T . [x | h2]^T, every Wc^T k-chunk resident
+  uint4 xg[TB][C::KS1];
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb)
+#pragma unroll
+    for (int ks = 0; ks < C::KS1; ++ks)
+      xg[tb][ks] = *reinterpret_cast<const uint4*>(x + min(tw + tb * 16 + fr, (long)T - 1) * D + ks * 32 + fg * 8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  f32x4 acc3[C::DT][TB];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < C::KS3; ++ks) {
+    const unsigned char* sb = smem + wc_chunk(ks);
+    if (ks < C::KS1) {
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const int r = dt * 16 + fr;
+        const uint4 af = *reinterpret_cast<const uint4*>(sb + r * 64 + swz64(r, fg) * 16);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, xg[tb][ks], acc3[dt][tb]);
+      }
+    } else {
+      const int s2 = ks - C::KS1;
+      const float4 ba = *reinterpret_cast<const float4*>(b2 + s2 * 32 + fg * 4);
+      const float4 bb = *reinterpret_cast<const float4*>(b2 + s2 * 32 + 16 + fg * 4);
+      uint4 h2f[TB];
+#pragma unroll
+      for (int tb = 0; tb < TB; ++tb) {
+        const f32x4 p = acc2[2 * s2][tb], q = acc2[2 * s2 + 1][tb];
+        h2f[tb] = make_uint4(pack_bf16x2(hv_gelu_fast(p[0] + ba.x), hv_gelu_fast(p[1] + ba.y)),
+                             pack_bf16x2(hv_gelu_fast(p[2] + ba.z), hv_gelu_fast(p[3] + ba.w)),
+                             pack_bf16x2(hv_gelu_fast(q[0] + bb.x), hv_gelu_fast(q[1] + bb.y)),
+                             pack_bf16x2(hv_gelu_fast(q[2] + bb.z), hv_gelu_fast(q[3] + bb.w)));
+      }
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const int r = dt * 16 + fr;
+        const uint2 lo = lds_b64<NOMERGE>(sb + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = lds_b64<NOMERGE>(sb + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int tb = 0; tb < TB; ++tb) acc3[dt][tb] = mfma(af, h2f[tb], acc3[dt][tb]);
+      }
+    }
+  }
+
+  // ---- LN_post per token (lane: token tb*16 + fr, columns dt*16 + 4g + j) + residual
+#pragma unroll
+  for (int tb = 0; tb < TB; ++tb) {
+    float s = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) s += (acc3[dt][tb][0] + acc3[dt][tb][1]) + (acc3[dt][tb][2] + acc3[dt][tb][3]);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float dd = acc3[dt][tb][j] - mu; q += dd * dd; }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float inv = rsqrtf(q * (1.0f / D) + 1e-5f);
+    const long tok = tw + tb * 16 + fr;
+    if (tok >= T) continue;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      const int col = dt * 16 + fg * 4;
+      const float4 gp = *reinterpret_cast<const float4*>(g_post + col);
+      const float4 bp = *reinterpret_cast<const float4*>(b_post + col);
+      float v0 = (acc3[dt][tb][0] - mu) * inv * gp.x + bp.x;
+      float v1 = (acc3[dt][tb][1] - mu) * inv * gp.y + bp.y;
+      float v2 = (acc3[dt][tb][2] - mu) * inv * gp.z + bp.z;
+      float v3 = (acc3[dt][tb][3] - mu) * inv * gp.w + bp.w;
+      if (res) {
+        const uint2 r2 = *reinterpret_cast<const uint2*>(res + tok * D + col);
+        v0 += __uint_as_float(r2.x << 16);
+        v1 += __uint_as_float(r2.x & 0xffff0000u);
+        v2 += __uint_as_float(r2.y << 16);
+        v3 += __uint_as_float(r2.y & 0xffff0000u);
+      }
+      *reinterpret_cast<uint2*>(out + tok * D + col) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+    }
+  }
+}
+
+template <int D, int HD, int TB, int MINB, int NW, bool NOMERGE>
+int launch_pipe(const hv_mhc_fused_args* a, hipStream_t s) {
+  using C = Cfg<D, HD, TB, NW>;
+  constexpr int LDS = 3 * C::STAGE + (2 * HD + C::KC) * 4;
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  auto k = mhc_fused_pipe_kernel<D, HD, TB, MINB, NW, NOMERGE>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hv_diag_count(HV_KF_MHC_FUSED);
+  k<<<hv_cdiv(a->T, C::BM), C::NT, LDS, s>>>(
+      (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
+      a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
+      (unsigned short*)a->out);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split-hidden variant (D = 128, HD = 512).  The kernel above gives every wave 16 tokens end to
 // end, so each W2 fragment read from LDS (1 KB) feeds ONE MFMA: at D = 128 the loop is LDS- and
 // latency-bound (~400 TF/s).  Here a 4-wave workgroup owns TOK = 64 tokens and splits the HIDDEN
@@ -725,13 +1023,19 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
   // groups per CU (register cap 170): 2x slower.  Also measured slower: 1.5x tokens per wave
   // (TB 6 / 3, 35-60%) and 2-wave groups (4x) -- all register spills.
   if (a->D == 32) {
+    if (shape == 8) return launch_pipe<32, 128, 4, 2, 4, false>(a, s);
+    if (shape == 9) return launch_pipe<32, 128, 4, 2, 4, true>(a, s);
     if (shape == 7) return launch<32, 128, 4, 2, 4, true>(a, s);
+    if (shape == 10) return launch<32, 128, 4, 2, 4>(a, s);
     if (shape == 1) return launch<32, 128, 4, 3, 4>(a, s);
     if (shape == 2) return launch<32, 128, 4, 1>(a, s);
     return launch<32, 128, 4, 2, 4>(a, s);
   }
   if (a->D == 64) {
+    if (shape == 8) return launch_pipe<64, 256, 2, 2, 4, false>(a, s);
+    if (shape == 9) return launch_pipe<64, 256, 2, 2, 4, true>(a, s);
     if (shape == 7) return launch<64, 256, 2, 2, 4, true>(a, s);
+    if (shape == 10) return launch<64, 256, 2, 2, 4>(a, s);
     if (shape == 1) return launch<64, 256, 2, 3, 4>(a, s);
     if (shape == 2) return launch<64, 256, 2, 1>(a, s);
     return launch<64, 256, 2, 2, 4>(a, s);

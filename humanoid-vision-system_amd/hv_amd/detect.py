@@ -325,6 +325,10 @@ class GraphRunner:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_out = model(self.static_in, task=self.task)
+        # the graph reads buffers that live outside its memory pool (the grouped Sinkhorn /
+        # coefficient-prep program and its device tables, frozen plans): keep the capture's RunCtx
+        # alive, or a later set_options / set_precision / cache rebuild would free them under it
+        self.ctx = model._last_ctx
         self.version = model._watch.snapshot()
 
     def replay(self) -> Dict[str, Any]:
@@ -396,6 +400,7 @@ class HybridVisionSystem(nn.Module):
                             if isinstance(a, MultiHeadManifoldAttention)}
         self._frozen: Optional[Tuple[Any, RunCtx]] = None
         self._sk_cache: Dict[str, Any] = {}
+        self._last_ctx: Optional[RunCtx] = None   # the RunCtx of the latest eval forward
         self._watch = VersionWatch(self)
 
     # ---- precision / caching controls
@@ -451,6 +456,7 @@ class HybridVisionSystem(nn.Module):
             from .train_model import system_forward
             return system_forward(self, x, targets, task, compute_loss)
         ctx = self._ctx()
+        self._last_ctx = ctx
         with torch.no_grad(), use_ctx(ctx):
             if x.dtype == torch.float32 and x.is_contiguous():
                 bb = self.backbone.forward_nhwc(None, image=x)     # direct stem conv from NCHW

@@ -366,6 +366,7 @@ class StreamingPipeline:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph), torch.no_grad():
             self.outputs = self._forward()
+        self.ctx = self.model._last_ctx           # buffers graph 1 reads outside its pool (detect.GraphRunner)
         self._nms = ops.NmsPlan(self.outputs["decoded"], *self.nms_args)
         torch.cuda.synchronize()
         self.nms_graph = torch.cuda.CUDAGraph()

@@ -213,7 +213,11 @@ typedef struct hv_mhc_fused_args {
 } hv_mhc_fused_args;
 #define HV_MV_SHAPE_MASK  0xff   /* workgroup shape: 1 three 4-wave groups per CU, 2 one 8-wave group,
                                     5 (D = 128) the per-wave 4-wave kernel instead of split-hidden,
-                                    6 (D = 64) the per-wave 4-wave kernel instead of split-hidden */
+                                    6 (D = 64) the per-wave 4-wave kernel instead of split-hidden,
+                                    7 (D = 32/64) per-wave kernel with unmerged fragment reads,
+                                    8 / 9 (D = 32/64) the software-pipelined per-wave kernel
+                                    (9: unmerged fragment reads), 10 (D = 32/64) the per-wave
+                                    kernel without pipelining */
 #define HV_MV_WIDE        0x100  /* also run (256, 512) fused (slower than the GEMM chain; tests) */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */

@@ -405,6 +405,70 @@ def test_mhc_fused_workgroup_shapes_bitwise_equal(gpu_device, D, T):
     assert torch.equal(y4, y8)
 
 
+@pytest.mark.parametrize("D,T,with_res", [(32, 1000, False), (32, 777, True), (64, 777, False), (64, 4097, True),
+                                           (64, 100, True)])
+def test_mhc_fused_pipelined_bitwise_equal(gpu_device, D, T, with_res):
+    """The software-pipelined per-wave kernel (3-stage weight ring, GEMM1+GELU of chunk c+1 beside
+    GEMM2 of chunk c, Wc^T resident for GEMM3) computes exactly the per-wave kernel's arithmetic:
+    bitwise equal to it, with and without the unmerged fragment reads, ragged T, residual."""
+    from hv_amd import ManifoldHyperConnection, _lib
+    m = ManifoldHyperConnection(D, expansion_rate=4, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    g = torch.Generator().manual_seed(T + D)
+    x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
+    res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
+    with torch.no_grad():
+        ys = {}
+        for v in (_lib.MV_PERWAVE, _lib.MV_PIPE, _lib.MV_PIPE_NOMERGE, 0):
+            with run_options(mhc_variant=v):
+                ys[v] = m.forward_tokens(x, residual=res).cpu()
+    for v in (_lib.MV_PIPE, _lib.MV_PIPE_NOMERGE, 0):
+        assert torch.equal(ys[v], ys[_lib.MV_PERWAVE]), v
+
+
+def test_graph_survives_option_change(gpu_device):
+    """A GraphRunner keeps the buffers its graph reads outside the graph pool (the grouped
+    Sinkhorn / coefficient-prep program of the capture's RunCtx): set_options() after a capture
+    rebuilds the model's caches, and the first runner must still replay correctly."""
+    from hv_amd import _lib
+    m = _build("tiny", "wc", "bf16", gpu_device)
+    x = torch.randn(2, 3, 128, 128, generator=torch.Generator().manual_seed(9)).to(gpu_device)
+    with torch.no_grad():
+        m.set_options(mhc_variant=_lib.MV_PERWAVE)
+        ref = {k: v.clone() for k, v in m(x)["predictions"].items()}
+        ra = m.capture(x)
+        m.set_options(mhc_variant=_lib.MV_PIPE)
+        rb = m.capture(x)
+        torch.cuda.empty_cache()
+        a = ra(x, owned=True)["predictions"]
+        b = rb(x, owned=True)["predictions"]
+        torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(a[k], ref[k]), k
+        assert torch.equal(b[k], ref[k]), k
+
+
+def test_model_pipelined_mhc_bitwise_equal(gpu_device):
+    """In the base model at 640^2 (stem / stage-1 fused sites at T = 409,600 / 102,400 tokens per
+    4 images): the pipelined per-wave fused mHC kernel leaves the whole forward bitwise unchanged,
+    eager and as a captured graph."""
+    from hv_amd import _lib
+    m = _build("base", "wc", "bf16", gpu_device)
+    x = torch.randn(4, 3, 640, 640, generator=torch.Generator().manual_seed(5)).to(gpu_device)
+    with torch.no_grad():
+        m.set_options(mhc_variant=_lib.MV_PERWAVE)
+        a = {k: v.clone() for k, v in m(x)["predictions"].items()}
+        m.set_options(mhc_variant=_lib.MV_PIPE_NOMERGE)
+        b = {k: v.clone() for k, v in m(x)["predictions"].items()}
+        runner = m.capture(x)
+        c = runner(x, owned=True)["predictions"]
+        torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+        assert torch.equal(a[k], c[k]), k
+
+
 @pytest.mark.parametrize("T,with_res", [(64, False), (200, True), (1000, False), (6417, True)])
 def test_mhc_fused_split_hidden_matches_unfused(gpu_device, T, with_res):
     """The split-hidden D=128 kernel (the default: hidden dimension across 4 waves, split-K
