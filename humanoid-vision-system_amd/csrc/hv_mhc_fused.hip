@@ -675,53 +675,54 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
     const unsigned short* __restrict__ x, int T, const unsigned short* __restrict__ a1t,
     const float* __restrict__ c1, const unsigned short* __restrict__ w2, const float* __restrict__ b2,
     const unsigned short* __restrict__ wct, const float* __restrict__ g_post, const float* __restrict__ b_post,
-    const unsigned short* __restrict__ res, unsigned short* __restrict__ out, int abl) {
+    const unsigned short* __restrict__ res, unsigned short* __restrict__ out) {
   using C = Cfg2<D, HD, NG>;
   constexpr int KC = C::KC, TT = C::TT, TBW = C::TBW, HQT = C::HQT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* const h1s = smem + 3 * C::STAGE;
   float* const c1s = reinterpret_cast<float*>(h1s + 2 * C::H1B);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
   const int gq = w >> 2, qq = w & 3;                   // token group, hidden quarter of this wave
   const int fr = lane & 15, fg = lane >> 4;
   const long t0 = (long)blockIdx.x * C::TOK;
   const long tg0 = t0 + gq * C::TOKG;                  // first token of this wave's group
   const long tw = t0 + w * C::TW1;                     // first GEMM1 token of this wave
 
+  // weight DMAs as inline asm (mhc_glds16): hipcc does not track them, so it no longer waits
+  // vmcnt(0) before every fragment read of the other stages (it cannot tell them apart from the
+  // stage being filled); every wait below is explicit
   auto issue_chunk = [&](int ch, int st) {
-    unsigned char* sa = smem + st * C::STAGE;
-    unsigned char* sw = sa + C::A1B;
+    const unsigned sa = lds0 + st * C::STAGE, sw = sa + C::A1B;
 #pragma unroll
     for (int p0 = 0; p0 < KC * C::CPA; p0 += C::NT) {
-      const int p = p0 + tid;
-      if (p0 + (tid & ~63) < KC * C::CPA) {
-        const int r = p / C::CPA, pc = p % C::CPA;
-        dma16(a1t + (long)(ch * KC + r) * D + swzA<C::CPA>(r, pc) * 8, sa + (p - lane) * 16);
+      if (p0 + wu * 64 < KC * C::CPA) {
+        const int p = p0 + tid, r = p / C::CPA, pc = p % C::CPA;
+        mhc_glds16(a1t + (long)(ch * KC + r) * D + swzA<C::CPA>(r, pc) * 8, sa + (p0 + wu * 64) * 16);
       }
     }
 #pragma unroll
     for (int p0 = 0; p0 < HD * 4; p0 += C::NT) {
-      const int p = p0 + tid;
-      if (p0 + (tid & ~63) < HD * 4) {
-        const int r = p >> 2, pc = p & 3;
-        dma16(w2 + (long)r * (2 * HD) + ch * KC + swz64(r, pc) * 8, sw + (p - lane) * 16);
+      if (p0 + wu * 64 < HD * 4) {
+        const int p = p0 + tid, r = p >> 2, pc = p & 3;
+        mhc_glds16(w2 + (long)r * (2 * HD) + ch * KC + swz64(r, pc) * 8, sw + (p0 + wu * 64) * 16);
       }
     }
   };
-
-  if (abl & 256) return;
   // c1 goes to LDS once: a global load inside the chunk loop would be younger than the chunk
   // DMA just issued, and vmcnt retires in order -- GEMM1 would wait for the whole DMA each chunk
   for (int i = tid; i < 2 * HD; i += C::NT) c1s[i] = c1[i];
   auto issue_wc = [&](int dp) {                        // Wc^T rows [dp*DP, +DP), all k -> stage (NCH+dp&1)%3
-    unsigned char* dst = smem + ((C::NCH + (dp & 1)) % 3) * C::STAGE;
+    const unsigned dst = lds0 + ((C::NCH + (dp & 1)) % 3) * C::STAGE;
 #pragma unroll
     for (int i = 0; i < C::WPT; ++i) {
       const int p = i * C::NT + tid;
       const int kc = p / (C::DP * 4), r = (p >> 2) % C::DP, pc = p & 3;
-      dma16(wct + (long)(dp * C::DP + r) * (D + HD) + kc * 32 + swz64(r, pc) * 8, dst + (p - lane) * 16);
+      mhc_glds16(wct + (long)(dp * C::DP + r) * (D + HD) + kc * 32 + swz64(r, pc) * 8, dst + (i * C::NT + wu * 64) * 16);
     }
   };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // c1 loads retired before the first DMA
   issue_chunk(0, 0);
   issue_chunk(1, 1);
 
@@ -766,12 +767,12 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
     }
   }
 
-  // GEMM1 of chunk ch for this wave's tokens -> h1 slot (ch & 1), in the GEMM2 B-fragment layout
-  auto gemm1 = [&](int ch) {
+  // GEMM1 of chunk ch for this wave's tokens -> h1 slot `par`, in the GEMM2 B-fragment layout
+  auto gemm1 = [&](int ch, int par) {
     const unsigned char* sa = smem + (ch % 3) * C::STAGE;
     const float4 cb0 = *reinterpret_cast<const float4*>(c1s + ch * KC + fg * 4);
     const float4 cb1 = *reinterpret_cast<const float4*>(c1s + ch * KC + 16 + fg * 4);
-    unsigned char* slot = h1s + (ch & 1) * C::H1B;
+    unsigned char* slot = h1s + par * C::H1B;
 #pragma unroll
     for (int tb = 0; tb < TBW; ++tb) {
       f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1v = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -799,46 +800,37 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                                     // chunks 0, 1 landed
-  gemm1(0);
+  gemm1(0, 0);
   __syncthreads();                                     // h1(0) visible
-  if (abl & 512) return;
 
   for (int ch = 0; ch < C::NCH; ++ch) {
-    if (ch + 2 < C::NCH) {
-      if (!(abl & 1)) issue_chunk(ch + 2, (ch + 2) % 3);
-    } else {
-      issue_wc(ch + 2 - C::NCH);                       // GEMM3's first two Wc parts ride the tail
-    }
-    if (ch + 1 < C::NCH && !(abl & 4)) gemm1(ch + 1);
+    if (ch + 2 < C::NCH) issue_chunk(ch + 2, (ch + 2) % 3);
+    else issue_wc(ch + 2 - C::NCH);                    // GEMM3's first two Wc parts ride the tail
     const unsigned char* sw = smem + (ch % 3) * C::STAGE + C::A1B;
     const unsigned char* slot = h1s + (ch & 1) * C::H1B + gq * TT * 1024;
     uint4 bf[TT];                                      // h1 chunk fragments of the group's tokens
 #pragma unroll
-    for (int t = 0; t < TT; ++t)
-      bf[t] = (abl & 32) ? make_uint4(t, lane, 1, 2) : *reinterpret_cast<const uint4*>(slot + (t * 64 + lane) * 16);
+    for (int t = 0; t < TT; ++t) bf[t] = *reinterpret_cast<const uint4*>(slot + (t * 64 + lane) * 16);
 #pragma unroll
     for (int hl = 0; hl < HQT; ++hl) {
       const int r = (qq * HQT + hl) * 16 + fr;
-      uint4 af = make_uint4(hl, r, 3, 4);
-      if (!(abl & 32)) {
-        const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
-        const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
-        af = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      }
-      if (!(abl & 2)) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+      const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
-        for (int t = 0; t < TT; ++t) acc2[hl][t] = mfma(af, bf[t], acc2[hl][t]);
-      } else {
-        acc2[hl][0][0] += __uint_as_float(af.x) + __uint_as_float(bf[0].y);
-      }
+      for (int t = 0; t < TT; ++t) acc2[hl][t] = mfma(af, bf[t], acc2[hl][t]);
     }
-    if (!(abl & 16)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    // GEMM1 of chunk ch+1 AFTER GEMM2 in program order: its h1 ds_write ends the iteration, so
+    // nothing keeps the scheduler from moving its fragment reads, MFMAs and GELU VALU up between
+    // GEMM2's MFMAs (in the other order GEMM2's reads could not pass the write).  The last
+    // iteration recomputes chunk NCH-1 into the idle h1 slot: straight-line code, no branch.
+    gemm1(ch + 1 < C::NCH ? ch + 1 : C::NCH - 1, (ch + 1) & 1);
+    // this wave's DMAs of chunk ch+2 (or the Wc part) landed; every wave's reads of this
+    // iteration retired and its h1(ch+1) writes visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
-
-  if ((abl & 1024) && acc2[0][0][0] != 12345.f) return;
   // ---- h2 = GELU(acc2 + b2) as GEMM3 B fragments (pairs of hidden tiles, permuted k order)
   uint4 h2f[HQT / 2][TT];
 #pragma unroll
@@ -865,7 +857,6 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
 
   // ---- GEMM3 (split-K over the 4 quarter waves of a group) + cross-wave reduce, NP column parts;
   // part dp+2's Wc DMA overlaps the reduce of part dp and the MFMAs of part dp+1
-  if ((abl & 2048) && __uint_as_float(h2f[0][0].x ^ xg[0].y) != 12345.f) return;
   float* const part = reinterpret_cast<float*>(gq == 0 ? smem + ((C::NCH + 2) % 3) * C::STAGE
                                                        : smem + 3 * C::STAGE);
   const int ltok = lane % C::RTW;                      // reduce / LN mapping: token, CPL columns
@@ -875,12 +866,8 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
   for (int dp = 0; dp < C::NP; ++dp) {
     if (dp + 1 < C::NP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::WPT) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                                   // Wc part dp visible; part dp-1 reduced
-    if (abl & 8) {
-#pragma unroll
-      for (int c = 0; c < C::CPL; ++c) y[dp][c] = __uint_as_float(h2f[0][0].x) + c;
-      continue;
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                      // Wc part dp visible; part dp-1 reduced
     const unsigned char* wcp = smem + ((C::NCH + (dp & 1)) % 3) * C::STAGE;
     f32x4 acc3[C::DT3][TT];
 #pragma unroll
@@ -930,7 +917,6 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
     }
   }
 
-  if ((abl & 4096) && y[0][0] + y[C::NP - 1][C::CPL - 1] != 12345.f) return;
   // ---- LN_post (+ residual) per token: lanes ltok, ltok + RTW, ... share a token
   float s = 0.f;
 #pragma unroll
@@ -994,7 +980,7 @@ int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
   k<<<hv_cdiv(a->T, C::TOK), C::NT, C::LDS, s>>>(
       (const unsigned short*)a->x, a->T, (const unsigned short*)a->a1t, a->c1, (const unsigned short*)a->w2,
       a->b2, (const unsigned short*)a->wct, a->g_post, a->b_post, (const unsigned short*)a->residual,
-      (unsigned short*)a->out, a->variant >> HV_MV_ABLATE_SHIFT);   // diagnostics only (tools/mhc_ablate*.py)
+      (unsigned short*)a->out);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -1016,6 +1002,9 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
                        (uintptr_t)a->b_post | (uintptr_t)a->residual;
   if (al & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+  // default for D = 32 / 64: the software-pipelined per-wave kernel with unmerged fragment reads
+  // (tools/mhc_ab.py, gpurun_out r3 mhcpipe3: D=64 T=1.6M 0.849 vs 0.979 ms, T=409,600 0.220 vs
+  // 0.265; D=32 T=1.6M 0.321 vs 0.346; in-model graph 19.94 vs 20.26 ms/step, bitwise equal).
   // measured (tools/mhc_variants.py): more tokens per wave wins while acc2 fits in registers;
   // (tools/mhc_ab.py) 4-wave workgroups, two per CU, beat one 8-wave workgroup by 16-20% at
   // every D (the two groups' chunk barriers no longer coincide, so one group's MFMAs cover the
@@ -1029,7 +1018,7 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
     if (shape == 10) return launch<32, 128, 4, 2, 4>(a, s);
     if (shape == 1) return launch<32, 128, 4, 3, 4>(a, s);
     if (shape == 2) return launch<32, 128, 4, 1>(a, s);
-    return launch<32, 128, 4, 2, 4>(a, s);
+    return launch_pipe<32, 128, 4, 2, 4, true>(a, s);
   }
   if (a->D == 64) {
     if (shape == 8) return launch_pipe<64, 256, 2, 2, 4, false>(a, s);
@@ -1038,7 +1027,7 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
     if (shape == 10) return launch<64, 256, 2, 2, 4>(a, s);
     if (shape == 1) return launch<64, 256, 2, 3, 4>(a, s);
     if (shape == 2) return launch<64, 256, 2, 1>(a, s);
-    return launch<64, 256, 2, 2, 4>(a, s);
+    return launch_pipe<64, 256, 2, 2, 4, true>(a, s);
   }
   if (a->D == 128) {
     // default: the split-hidden kernel (hidden dimension across 4 waves, 2 token groups per
