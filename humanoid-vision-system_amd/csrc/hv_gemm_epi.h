@@ -84,6 +84,54 @@ struct EpiCols {
   float sc[RN][4], bi[RN][4], cs[RN][4];
 };
 
+// Column (cbase + b*16 + j) constants as ONE batch of independent loads: clamped column indices,
+// a uniform branch per (possibly null) array, bounds applied afterwards.  Written per element as
+// `p && col < N ? p[col] : x`, hipcc branches around every load and waits vmcnt(0) inside each
+// branch -- 16-48 serialized round trips per epilogue (round-2 ISA of every GEMM kernel).
+template <int RN, bool LN_EPI>
+__device__ __forceinline__ void epi_load_cols(const hv_gemm_desc& d, EpiCols<RN>& k, int cbase) {
+  int cc[RN][4];
+#pragma unroll
+  for (int b = 0; b < RN; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cc[b][j] = min(cbase + b * 16 + j, d.N - 1);
+  if (d.scale) {
+#pragma unroll
+    for (int b = 0; b < RN; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k.sc[b][j] = d.scale[cc[b][j]];
+  } else {
+#pragma unroll
+    for (int b = 0; b < RN; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k.sc[b][j] = 1.f;
+  }
+  if (d.bias) {
+#pragma unroll
+    for (int b = 0; b < RN; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k.bi[b][j] = d.bias[cc[b][j]];
+  } else {
+#pragma unroll
+    for (int b = 0; b < RN; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k.bi[b][j] = 0.f;
+  }
+#pragma unroll
+  for (int b = 0; b < RN; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k.cs[b][j] = LN_EPI ? d.b_colsum[cc[b][j]] : 0.f;
+#pragma unroll
+  for (int b = 0; b < RN; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = cbase + b * 16 + j < d.N;
+      k.sc[b][j] = d.scale && ok ? k.sc[b][j] * d.alpha : d.alpha;
+      k.bi[b][j] = ok ? k.bi[b][j] : 0.f;
+      k.cs[b][j] = ok ? k.cs[b][j] : 0.f;
+    }
+}
+
 // One 16-row sub-tile row A of the wave's accumulators.  The row-tile index is a template
 // parameter (instantiated A = 0 .. RM-1 by epi_rows), so every acc[A][b] is a constant index:
 // a runtime-indexed row loop that the unroller declines (large RM x RN x body) would leave the
@@ -174,17 +222,7 @@ __device__ __forceinline__ void gemm_epilogue(const hv_gemm_desc& d, const f32x4
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wc = wid % WN;
   const int fg = lane >> 4;
   EpiCols<RN> k;
-#pragma unroll
-  for (int b = 0; b < RN; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4 + j;
-      const bool ok = col < d.N;
-      k.sc[b][j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
-      k.bi[b][j] = (d.bias && ok) ? d.bias[col] : 0.f;
-      k.cs[b][j] = 0.f;
-      if constexpr (LN_EPI) k.cs[b][j] = ok ? d.b_colsum[col] : 0.f;
-    }
+  epi_load_cols<RN, LN_EPI>(d, k, n0 + wc * (RN * 16) + fg * 4);
   epi_rows<0, LN_EPI, TRAIN, WN, RM, RN>(d, acc, k, m0, n0);
 }
 
@@ -250,7 +288,8 @@ __device__ __forceinline__ void epi_stage_rows(const hv_gemm_desc& d, const f32x
 // training write-out of 8 staged values (row, col .. col+7): mode 1 stores the pre-activation z
 // to aux (rounded like the fragment epilogue) and returns act(z) * keep; mode 2 reads aux and
 // returns z * keep * act'(aux).  keep(m, n) = hv_drop_scale(seed, m * N + n), as epi_train.
-__device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8], int row, int col, bool vec8) {
+__device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8], int row, int col, bool vec8,
+                                           const float* zpre = nullptr) {
   const bool aux_bf = d.aux_dtype == HV_BF16;
   const long ai = (long)row * d.ld_aux + col;
   const unsigned long long idx0 = (unsigned long long)row * d.N + col;
@@ -288,6 +327,9 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
+  } else if (zpre) {                         // mode 2 with the aux row preloaded by the caller
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(zpre[j], d.act);
   } else {
     if (av && aux_bf) {
       const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
@@ -312,14 +354,11 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
   }
 }
 
-template <int BN, int NT, int SLAB, bool TRAIN = false>
-__device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
+// Scalar write-out (C or residual not 16-B aligned / strided): element stores.
+template <int BN, int NT, int SLAB, bool TRAIN>
+__device__ __forceinline__ void epi_writeout_s(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
   const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
-  const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
-                   (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
-  // ---- coalesced write-out: thread -> (row, 8 columns)
-  constexpr int TPR = BN / 8;                 // threads per row
-  constexpr int RPP = NT / TPR;               // rows per pass
+  constexpr int TPR = BN / 8, RPP = NT / TPR;
 #pragma unroll
   for (int p = 0; p < SLAB / RPP; ++p) {
     const int lr = p * RPP + threadIdx.x / TPR;
@@ -328,24 +367,98 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
     if (row >= d.M || col >= d.N) continue;
     const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    if constexpr (TRAIN) epi_train8(d, v, row, col, col + 8 <= d.N);
+    if constexpr (TRAIN) epi_train8(d, v, row, col, false);
     const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
-    if (vec && col + 8 <= d.N) {
-      if (d.residual) {
-        if (r_bf) {
-          const uint4 r = *reinterpret_cast<const uint4*>((const unsigned short*)d.residual + rrow * d.ldr + col);
-          const unsigned rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (col + j >= d.N) break;
+      float x = v[j];
+      if (d.residual)
+        x += r_bf ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
+                  : ((const float*)d.residual)[rrow * d.ldr + col + j];
+      const long o = (long)row * d.ldc + col + j;
+      if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
+      else ((float*)d.C)[o] = x;
+    }
+  }
+}
+
+// RES: 0 no residual, 1 bf16 residual, 2 fp32 residual (vector path).  The residual rows of every
+// pass are loaded BEFORE the first store: a load issued after a store is waited for with vmcnt,
+// which counts in issue order, so interleaved it would also wait for every earlier store's write
+// (one store round trip per pass, round-2 ISA).
+template <int BN, int NT, int SLAB, bool TRAIN, int RES>
+__device__ __forceinline__ void epi_writeout_v(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
+  const bool c_bf = d.c_dtype == HV_BF16, r_bf = d.r_dtype == HV_BF16;
+  constexpr int TPR = BN / 8;                 // threads per row
+  constexpr int RPP = NT / TPR;               // rows per pass
+  constexpr int NP = SLAB / RPP;
+  const int c8 = (threadIdx.x % TPR) * 8;
+  const int col = n0 + c8;
+  const bool vcol = col + 8 <= d.N;           // whole 8-column vector (the vector path's condition)
+  uint4 rb[RES == 1 ? NP : 1];
+  float4 rf[RES == 2 ? NP : 1][2];
+  // training mode 2 (the activation backward) reads the stored pre-activation: preloaded too
+  float za[TRAIN ? NP : 1][8];
+  bool zok = false;
+  if constexpr (TRAIN) {
+    zok = d.epi_mode == 2 && vcol && (d.ld_aux & 7) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
+    if (zok) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int row = min(r0 + p * RPP + (int)threadIdx.x / TPR, d.M - 1);
+        const long ai = (long)row * d.ld_aux + col;
+        if (d.aux_dtype == HV_BF16) {
+          const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
+          const unsigned tw[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            v[2 * q] += __uint_as_float(rw[q] << 16);
-            v[2 * q + 1] += __uint_as_float(rw[q] & 0xffff0000u);
+            za[p][2 * q] = __uint_as_float(tw[q] << 16);
+            za[p][2 * q + 1] = __uint_as_float(tw[q] & 0xffff0000u);
           }
         } else {
-          const float4 r0 = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col);
-          const float4 r1 = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col + 4);
-          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
-          v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+          const float4 t0 = *reinterpret_cast<const float4*>((const float*)d.aux + ai);
+          const float4 t1 = *reinterpret_cast<const float4*>((const float*)d.aux + ai + 4);
+          za[p][0] = t0.x; za[p][1] = t0.y; za[p][2] = t0.z; za[p][3] = t0.w;
+          za[p][4] = t1.x; za[p][5] = t1.y; za[p][6] = t1.z; za[p][7] = t1.w;
         }
+      }
+    }
+  }
+  if constexpr (RES != 0) {
+    if (vcol) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int row = min(r0 + p * RPP + (int)threadIdx.x / TPR, d.M - 1);
+        const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
+        if constexpr (RES == 1) {
+          rb[p] = *reinterpret_cast<const uint4*>((const unsigned short*)d.residual + rrow * d.ldr + col);
+        } else {
+          rf[p][0] = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col);
+          rf[p][1] = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col + 4);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int lr = p * RPP + threadIdx.x / TPR;
+    const int row = r0 + lr;
+    if (row >= d.M || col >= d.N) continue;
+    const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if constexpr (TRAIN) epi_train8(d, v, row, col, vcol, zok ? za[p] : nullptr);
+    if (vcol) {
+      if constexpr (RES == 1) {
+        const unsigned rw[4] = {rb[p].x, rb[p].y, rb[p].z, rb[p].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] += __uint_as_float(rw[q] << 16);
+          v[2 * q + 1] += __uint_as_float(rw[q] & 0xffff0000u);
+        }
+      } else if constexpr (RES == 2) {
+        v[0] += rf[p][0].x; v[1] += rf[p][0].y; v[2] += rf[p][0].z; v[3] += rf[p][0].w;
+        v[4] += rf[p][1].x; v[5] += rf[p][1].y; v[6] += rf[p][1].z; v[7] += rf[p][1].w;
       }
       if (c_bf) {
         *reinterpret_cast<uint4*>((unsigned short*)d.C + (long)row * d.ldc + col) =
@@ -357,11 +470,12 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
         *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
       }
     } else {
+      const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (col + j >= d.N) break;
         float x = v[j];
-        if (d.residual)
+        if (RES != 0)
           x += r_bf ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
                     : ((const float*)d.residual)[rrow * d.ldr + col + j];
         const long o = (long)row * d.ldc + col + j;
@@ -372,6 +486,17 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
   }
 }
 
+template <int BN, int NT, int SLAB, bool TRAIN = false>
+__device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
+  const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
+                   (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
+  // coalesced write-out: thread -> (row, 8 columns); the vector path needs aligned C / residual
+  if (!vec) epi_writeout_s<BN, NT, SLAB, TRAIN>(d, r0, n0, smem);
+  else if (!d.residual) epi_writeout_v<BN, NT, SLAB, TRAIN, 0>(d, r0, n0, smem);
+  else if (d.r_dtype == HV_BF16) epi_writeout_v<BN, NT, SLAB, TRAIN, 1>(d, r0, n0, smem);
+  else epi_writeout_v<BN, NT, SLAB, TRAIN, 2>(d, r0, n0, smem);
+}
+
 template <int BM, int BN, bool LN_EPI, int WN, int RM, int RN, int NT, int SLAB, bool TRAIN = false>
 __device__ __forceinline__ void gemm_epilogue_staged(const hv_gemm_desc& d, const f32x4 (&acc)[RM][RN], int m0, int n0,
                                                      unsigned char* smem) {
@@ -379,17 +504,7 @@ __device__ __forceinline__ void gemm_epilogue_staged(const hv_gemm_desc& d, cons
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid / WN, wc = wid % WN;
   const int fg = lane >> 4;
   EpiCols<RN> k;
-#pragma unroll
-  for (int b = 0; b < RN; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * (RN * 16) + b * 16 + fg * 4 + j;
-      const bool ok = col < d.N;
-      k.sc[b][j] = (d.scale && ok) ? d.scale[col] * d.alpha : d.alpha;
-      k.bi[b][j] = (d.bias && ok) ? d.bias[col] : 0.f;
-      k.cs[b][j] = 0.f;
-      if constexpr (LN_EPI) k.cs[b][j] = ok ? d.b_colsum[col] : 0.f;
-    }
+  epi_load_cols<RN, LN_EPI>(d, k, n0 + wc * (RN * 16) + fg * 4);
   const int wrow0 = wr * (RM * 16);
   if constexpr (BM == SLAB) {
     epi_stage_rows<0, LN_EPI, RM, RN, BN / 4, TRAIN>(d, acc, k, m0 + wrow0, wrow0, wc * (RN * 16), smem);

@@ -369,6 +369,11 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
   static_assert(NCH >= 3 && C::KS3 <= 2 * WPS, "Wc^T fits the two stages freed by the last chunks");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* const c1s = reinterpret_cast<float*>(smem + 3 * C::STAGE);   // 2HD (+KC pad) floats
+  // b2 [HD], g_post [D], b_post [D] in LDS too: read from global inside the GEMM3 / LN_post
+  // loops, each load was waited for on its own (and, once stores had been issued, behind them)
+  float* const b2s = c1s + 2 * HD + KC;
+  float* const gps = b2s + HD;
+  float* const bps = gps + D;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -416,6 +421,11 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
     for (int ks = 0; ks < C::KS1; ++ks)
       xin[tb][ks] = *reinterpret_cast<const uint4*>(x + min(tw + tb * 16 + fr, (long)T - 1) * D + ks * 32 + fg * 8);
   for (int i = tid; i < 2 * HD; i += C::NT) c1s[i] = c1[i];
+  for (int i = tid; i < HD; i += C::NT) b2s[i] = b2[i];
+  for (int i = tid; i < D; i += C::NT) {
+    gps[i] = g_post[i];
+    bps[i] = b_post[i];
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   issue_chunk(0, 0);
   issue_chunk(1, 1);
@@ -552,8 +562,8 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
       }
     } else {
       const int s2 = ks - C::KS1;
-      const float4 ba = *reinterpret_cast<const float4*>(b2 + s2 * 32 + fg * 4);
-      const float4 bb = *reinterpret_cast<const float4*>(b2 + s2 * 32 + 16 + fg * 4);
+      const float4 ba = *reinterpret_cast<const float4*>(b2s + s2 * 32 + fg * 4);
+      const float4 bb = *reinterpret_cast<const float4*>(b2s + s2 * 32 + 16 + fg * 4);
       uint4 h2f[TB];
 #pragma unroll
       for (int tb = 0; tb < TB; ++tb) {
@@ -575,7 +585,17 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
     }
   }
 
-  // ---- LN_post per token (lane: token tb*16 + fr, columns dt*16 + 4g + j) + residual
+  // ---- LN_post per token (lane: token tb*16 + fr, columns dt*16 + 4g + j) + residual; the
+  // residual of every (tb, dt) is loaded before the first store (a load behind a store waits for it)
+  constexpr bool PRE = D >= 64;     // D = 32 (TB = 4): the preloaded residual would spill
+  uint2 rres[TB][C::DT];
+  if (PRE && res) {
+#pragma unroll
+    for (int tb = 0; tb < TB; ++tb)
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt)
+        rres[tb][dt] = *reinterpret_cast<const uint2*>(res + min(tw + tb * 16 + fr, (long)T - 1) * D + dt * 16 + fg * 4);
+  }
 #pragma unroll
   for (int tb = 0; tb < TB; ++tb) {
     float s = 0.f;
@@ -597,14 +617,14 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
       const int col = dt * 16 + fg * 4;
-      const float4 gp = *reinterpret_cast<const float4*>(g_post + col);
-      const float4 bp = *reinterpret_cast<const float4*>(b_post + col);
+      const float4 gp = *reinterpret_cast<const float4*>(gps + col);
+      const float4 bp = *reinterpret_cast<const float4*>(bps + col);
       float v0 = (acc3[dt][tb][0] - mu) * inv * gp.x + bp.x;
       float v1 = (acc3[dt][tb][1] - mu) * inv * gp.y + bp.y;
       float v2 = (acc3[dt][tb][2] - mu) * inv * gp.z + bp.z;
       float v3 = (acc3[dt][tb][3] - mu) * inv * gp.w + bp.w;
       if (res) {
-        const uint2 r2 = *reinterpret_cast<const uint2*>(res + tok * D + col);
+        const uint2 r2 = PRE ? rres[tb][dt] : *reinterpret_cast<const uint2*>(res + tok * D + col);
         v0 += __uint_as_float(r2.x << 16);
         v1 += __uint_as_float(r2.x & 0xffff0000u);
         v2 += __uint_as_float(r2.y << 16);
@@ -618,7 +638,7 @@ __global__ void __launch_bounds__(64 * NW_, MINB) mhc_fused_pipe_kernel(
 template <int D, int HD, int TB, int MINB, int NW, bool NOMERGE>
 int launch_pipe(const hv_mhc_fused_args* a, hipStream_t s) {
   using C = Cfg<D, HD, TB, NW>;
-  constexpr int LDS = 3 * C::STAGE + (2 * HD + C::KC) * 4;
+  constexpr int LDS = 3 * C::STAGE + (2 * HD + C::KC + HD + 2 * D) * 4;
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
   auto k = mhc_fused_pipe_kernel<D, HD, TB, MINB, NW, NOMERGE>;
   static bool attr = false;
@@ -936,23 +956,39 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
   const float inv = rsqrtf(q * (1.0f / D) + 1e-5f);
   const long tok = tg0 + qq * C::RTW + ltok;
   if (tok < T) {
+    // every load (LN_post affine, residual) issued before the first store: a load behind a
+    // store is waited for together with it (vmcnt retires in order)
+    float4 gpa[C::NP][C::CPL / 4], bpa[C::NP][C::CPL / 4];
+    uint4 rr4[C::NP][C::CPL / 8];
+#pragma unroll
+    for (int dp = 0; dp < C::NP; ++dp)
+#pragma unroll
+      for (int c = 0; c < C::CPL; c += 4) {
+        gpa[dp][c / 4] = *reinterpret_cast<const float4*>(g_post + dp * C::DP + cb + c);
+        bpa[dp][c / 4] = *reinterpret_cast<const float4*>(b_post + dp * C::DP + cb + c);
+      }
+    if (res) {
+#pragma unroll
+      for (int dp = 0; dp < C::NP; ++dp)
+#pragma unroll
+        for (int c = 0; c < C::CPL; c += 8)
+          rr4[dp][c / 8] = *reinterpret_cast<const uint4*>(res + tok * D + dp * C::DP + cb + c);
+    }
 #pragma unroll
     for (int dp = 0; dp < C::NP; ++dp) {
       const int col0 = dp * C::DP + cb;
 #pragma unroll
       for (int c = 0; c < C::CPL; c += 8) {
         const int col = col0 + c;
-        const float4 ga = *reinterpret_cast<const float4*>(g_post + col);
-        const float4 gb = *reinterpret_cast<const float4*>(g_post + col + 4);
-        const float4 ba = *reinterpret_cast<const float4*>(b_post + col);
-        const float4 bb = *reinterpret_cast<const float4*>(b_post + col + 4);
+        const float4 ga = gpa[dp][c / 4], gb = gpa[dp][c / 4 + 1];
+        const float4 ba = bpa[dp][c / 4], bb = bpa[dp][c / 4 + 1];
         const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
         const float bv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (y[dp][c + e] - mu) * inv * gg[e] + bv[e];
         if (res) {
-          const uint4 r4 = *reinterpret_cast<const uint4*>(res + tok * D + col);
+          const uint4 r4 = rr4[dp][c / 8];
           const uint32_t rr[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {

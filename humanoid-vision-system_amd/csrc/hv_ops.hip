@@ -138,6 +138,22 @@ __global__ void __launch_bounds__(256) k_layernorm_v(const TX* __restrict__ x, i
     ok[q] = c0 < cols;
     if (ok[q]) Vec8<TX>::load(p + c0, v[q]);
   }
+  // gamma / beta / residual of a short row (NP <= 2) loaded with x, so their latency hides under
+  // the statistics instead of following them; longer rows load them per part (registers)
+  constexpr bool PRE = NP <= 2;
+  float gp[PRE ? NP : 1][8], bp[PRE ? NP : 1][8], rp[PRE ? NP : 1][8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (!ok[q]) continue;
+      const int c0 = (q * G + l) * 8;
+      if (gamma) { Vec8<float>::load(gamma + c0, gp[q]); Vec8<float>::load(beta + c0, bp[q]); }
+      if (res) {
+        if (res_dt == HV_BF16) Vec8<unsigned short>::load((const unsigned short*)res + (long)r * cols + c0, rp[q]);
+        else Vec8<float>::load((const float*)res + (long)r * cols + c0, rp[q]);
+      }
+    }
+  }
   float mu, rs;
   group_stats<G, NP>(v, ok, cols, eps, mu, rs);
 #pragma unroll
@@ -145,10 +161,15 @@ __global__ void __launch_bounds__(256) k_layernorm_v(const TX* __restrict__ x, i
     if (!ok[q]) continue;
     const int c0 = (q * G + l) * 8;
     float o[8], g[8], b[8], rv[8];
-    if (gamma) { Vec8<float>::load(gamma + c0, g); Vec8<float>::load(beta + c0, b); }
-    if (res) {
-      if (res_dt == HV_BF16) Vec8<unsigned short>::load((const unsigned short*)res + (long)r * cols + c0, rv);
-      else Vec8<float>::load((const float*)res + (long)r * cols + c0, rv);
+    if constexpr (PRE) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { g[j] = gp[q][j]; b[j] = bp[q][j]; rv[j] = rp[q][j]; }
+    } else {
+      if (gamma) { Vec8<float>::load(gamma + c0, g); Vec8<float>::load(beta + c0, b); }
+      if (res) {
+        if (res_dt == HV_BF16) Vec8<unsigned short>::load((const unsigned short*)res + (long)r * cols + c0, rv);
+        else Vec8<float>::load((const float*)res + (long)r * cols + c0, rv);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

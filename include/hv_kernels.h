@@ -153,6 +153,9 @@ typedef struct hv_gemm_desc {
 #define HV_GV_SK_DIAG1     0x2000  /* small-K kernel diagnostics (tools/k256_probe2.py; outputs
                                       garbage): skip the stores */
 #define HV_GV_SK_DIAG2     0x4000  /* ... skip the k-loop */
+#define HV_GV_SK_RES3      0x8000  /* small-K kernel: B-resident column-stationary form (K 192 / 256, no
+                                      residual), 3-stage A ring */
+#define HV_GV_SK_RES4      0x10000 /* ... 4-stage A ring */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

@@ -254,7 +254,7 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
 SMALLK_CASES = [  # (kind, M, N, K): 1-8 k-tiles, ragged M / N (scalar store tail), every epilogue form
     ("plain", 4096, 512, 64), ("plain", 1000, 777, 128), ("ln_gelu", 1500, 1024, 256), ("gelu_res", 2048, 768, 512),
     ("res32_mod", 1200, 640, 256), ("scale_f32", 700, 384, 192), ("conv1x1", 2 * 40 * 40, 256, 128),
-    ("ln_gelu", 8192, 1024, 256)]
+    ("ln_gelu", 8192, 1024, 256), ("ln_gelu", 6416, 3072, 256), ("conv1x1", 2 * 56 * 56, 512, 256)]
 
 
 @pytest.mark.parametrize("kind,M,N,K", SMALLK_CASES)
@@ -309,9 +309,17 @@ def test_gemm_smallk_equals_ring(gpu_device, kind, M, N, K):
         auto = run()
         assert ops.launch_counts()["gemm_smallk"] == 1
         assert torch.equal(auto, fast)
+    # the B-resident column-stationary form (K 192 / 256, no residual; 3- and 4-stage A rings)
+    res_forms = []
+    for v in (_lib.GV_SK_RES3, _lib.GV_SK_RES4):
+        with gemm_variant(_lib.GV_TILE_SMALLK | v):
+            res_forms.append(run())
     torch.cuda.synchronize()
     assert torch.equal(fast.reshape(ring.shape), ring), \
         f"max |diff| {(fast.float().reshape(ring.shape) - ring.float()).abs().max().item()}"
+    for r in res_forms:
+        assert torch.equal(r.reshape(ring.shape), ring), \
+            f"B-resident: max |diff| {(r.float().reshape(ring.shape) - ring.float()).abs().max().item()}"
     tol = 2e-2 if fast.dtype == torch.bfloat16 else 1e-4
     assert rel_err(fast.reshape(ref.shape), ref) < tol
 
