@@ -288,8 +288,7 @@ __device__ __forceinline__ void epi_stage_rows(const hv_gemm_desc& d, const f32x
 // training write-out of 8 staged values (row, col .. col+7): mode 1 stores the pre-activation z
 // to aux (rounded like the fragment epilogue) and returns act(z) * keep; mode 2 reads aux and
 // returns z * keep * act'(aux).  keep(m, n) = hv_drop_scale(seed, m * N + n), as epi_train.
-__device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8], int row, int col, bool vec8,
-                                           const float* zpre = nullptr) {
+__device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8], int row, int col, bool vec8) {
   const bool aux_bf = d.aux_dtype == HV_BF16;
   const long ai = (long)row * d.ld_aux + col;
   const unsigned long long idx0 = (unsigned long long)row * d.N + col;
@@ -327,9 +326,6 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
-  } else if (zpre) {                         // mode 2 with the aux row preloaded by the caller
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(zpre[j], d.act);
   } else {
     if (av && aux_bf) {
       const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
@@ -398,33 +394,6 @@ __device__ __forceinline__ void epi_writeout_v(const hv_gemm_desc& d, int r0, in
   const bool vcol = col + 8 <= d.N;           // whole 8-column vector (the vector path's condition)
   uint4 rb[RES == 1 ? NP : 1];
   float4 rf[RES == 2 ? NP : 1][2];
-  // training mode 2 (the activation backward) reads the stored pre-activation: preloaded too
-  float za[TRAIN ? NP : 1][8];
-  bool zok = false;
-  if constexpr (TRAIN) {
-    zok = d.epi_mode == 2 && vcol && (d.ld_aux & 7) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
-    if (zok) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int row = min(r0 + p * RPP + (int)threadIdx.x / TPR, d.M - 1);
-        const long ai = (long)row * d.ld_aux + col;
-        if (d.aux_dtype == HV_BF16) {
-          const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
-          const unsigned tw[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            za[p][2 * q] = __uint_as_float(tw[q] << 16);
-            za[p][2 * q + 1] = __uint_as_float(tw[q] & 0xffff0000u);
-          }
-        } else {
-          const float4 t0 = *reinterpret_cast<const float4*>((const float*)d.aux + ai);
-          const float4 t1 = *reinterpret_cast<const float4*>((const float*)d.aux + ai + 4);
-          za[p][0] = t0.x; za[p][1] = t0.y; za[p][2] = t0.z; za[p][3] = t0.w;
-          za[p][4] = t1.x; za[p][5] = t1.y; za[p][6] = t1.z; za[p][7] = t1.w;
-        }
-      }
-    }
-  }
   if constexpr (RES != 0) {
     if (vcol) {
 #pragma unroll
@@ -447,7 +416,10 @@ __device__ __forceinline__ void epi_writeout_v(const hv_gemm_desc& d, int r0, in
     if (row >= d.M || col >= d.N) continue;
     const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    if constexpr (TRAIN) epi_train8(d, v, row, col, vcol, zok ? za[p] : nullptr);
+    // training mode 2 loads its aux row here, after the previous pass's stores: preloaded for
+    // every pass like the residual (za[NP][8]) it measured 13 % slower on the 64x128 kernel
+    // (scratch spills at the 3-per-CU register budget)
+    if constexpr (TRAIN) epi_train8(d, v, row, col, vcol);
     if (vcol) {
       if constexpr (RES == 1) {
         const unsigned rw[4] = {rb[p].x, rb[p].y, rb[p].z, rb[p].w};

@@ -63,8 +63,17 @@ struct ConvK {
   __device__ int offset(const hv_gemm_desc& d) const { return (kh * d.conv_w + kw) * d.conv_c + ci; }
 };
 
+// Workgroups per CU the LDS ring admits (at most 4), declared as every instantiation's minimum
+// occupancy: the epilogues would otherwise grow past the register budget of that occupancy
+// (64x128 at 3 per CU needs <= 168 VGPRs; unbounded the compiler took 172)
+template <int TM, int TN, int TS, bool TT>
+struct GldsOcc {
+  static constexpr int lds_w = (160 * 1024) / (TS * (TM + TN) * 128);
+  static constexpr int value = lds_w < 1 ? 1 : (lds_w > 4 ? 4 : lds_w);
+};
+
 template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2, bool SPLIT = false>
-__global__ void __launch_bounds__(256) gemm_glds_kernel(const hv_gemm_desc d) {
+__global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm_glds_kernel(const hv_gemm_desc d) {
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
   constexpr int AI = BM / 32;               // A wave-instructions (8 rows each) per wave
@@ -356,7 +365,7 @@ __device__ __forceinline__ void pp_quadrant(f32x4 (&acc)[8][4], const uint4 (&fa
 #define PP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define PP_SYNC_LDS() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-template <bool CONV, bool STAGED>
+template <bool CONV, bool STAGED, bool TRAIN = false>
 __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
   constexpr int BM = 256, BN = 256;
   constexpr int RM = 8, RN = 4;                       // 16x16 sub-tiles per wave (128 x 64)
@@ -575,8 +584,8 @@ __global__ void __launch_bounds__(512) gemm_pp256_kernel(const hv_gemm_desc d) {
     if (d.a_mean) gemm_epilogue_staged<BM, BN, true, 4, RM, RN, 512, 128>(d, acc, m0, n0, smem);
     else gemm_epilogue_staged<BM, BN, false, 4, RM, RN, 512, 128>(d, acc, m0, n0, smem);
   } else {
-    if (d.a_mean) gemm_epilogue<BM, BN, true, false, 4, RM, RN>(d, acc, m0, n0);
-    else gemm_epilogue<BM, BN, false, false, 4, RM, RN>(d, acc, m0, n0);
+    if (d.a_mean) gemm_epilogue<BM, BN, true, TRAIN, 4, RM, RN>(d, acc, m0, n0);
+    else gemm_epilogue<BM, BN, false, TRAIN, 4, RM, RN>(d, acc, m0, n0);
   }
 }
 
@@ -598,8 +607,16 @@ int launch256(const hv_gemm_desc& d, hipStream_t s) {
   hv_diag_count(HV_KF_GEMM_PP256);
   // fragment-layout epilogue here: the staged one measured 1.3x slower on this kernel (K >= 1024,
   // where the output stream is a small part of the work)
-  if (d.conv_k > 0) gemm_pp256_kernel<true, false><<<grid, 512, 0, s>>>(d);
-  else gemm_pp256_kernel<false, false><<<grid, 512, 0, s>>>(d);
+  if (d.epi_mode) {
+    // training epilogues (store the pre-activation / apply the activation backward) on the
+    // fragment-layout epilogue
+    if (d.conv_k > 0) gemm_pp256_kernel<true, false, true><<<grid, 512, 0, s>>>(d);
+    else gemm_pp256_kernel<false, false, true><<<grid, 512, 0, s>>>(d);
+  } else if (d.conv_k > 0) {
+    gemm_pp256_kernel<true, false><<<grid, 512, 0, s>>>(d);
+  } else {
+    gemm_pp256_kernel<false, false><<<grid, 512, 0, s>>>(d);
+  }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -676,7 +693,7 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
     case 2: return launch<64, 128>(d, s);
     case 3: return launch<128, 64>(d, s);
     case 4: return launch<64, 64>(d, s);
-    case 5: if (!d.epi_mode && d.K % 64 == 0 && d.conv_c % 64 == 0) return launch256(d, s); break;
+    case 5: if (d.K % 64 == 0 && d.conv_c % 64 == 0) return launch256(d, s); break;
     case 6: return hv_gemm_smallk(d, s, true);
     default: {
       const int rc = hv_gemm_smallk(d, s, false);             // persistent small-K kernel (hv_gemm_sk.hip)
@@ -688,7 +705,8 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // CUs.  Measured in the model (tools/gemm_breakdown.py, cold operands): wins for N >= 1024
   // (25600x1024x2048, 6400x2048x4096: -5..11 %); loses to the 128x128 ring for N <= 512 and for
   // the implicit-im2col convolutions (+3..29 %); K = 256 loses everywhere (prologue-bound)
-  if (!d.epi_mode && d.K % 64 == 0 && d.conv_c % 64 == 0 && !(d.variant & HV_GV_NO_BIG) &&
+  if ((!d.epi_mode || (d.variant & HV_GV_TRAIN_BIG)) && d.K % 64 == 0 && d.conv_c % 64 == 0 &&
+      !(d.variant & HV_GV_NO_BIG) &&
       ((d.variant & HV_GV_BIG_ALWAYS) || (d.conv_k == 0 && d.K >= 1024 && d.N >= 1024 && t256 >= 160)))
     return launch256(d, s);
   if (d.N <= 64) return launch<128, 64>(d, s);

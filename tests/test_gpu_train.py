@@ -820,7 +820,7 @@ def test_module_level_training_api(gpu_device):
 
 
 @pytest.mark.parametrize("M,N,K,act,ln", [(300, 136, 128, "gelu", False), (1000, 256, 256, "silu", True),
-                                          (777, 96, 64, "leaky", False)])
+                                          (777, 96, 64, "leaky", False), (1300, 1100, 1024, "gelu", False)])
 def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
     """The LDS-staged training epilogue (the default; variant GV_FLAT_TRAIN = fragment layout) writes exactly the
     bits of the fragment-layout one: pre-activation, dropout(act) output (mode 1) and the
@@ -839,11 +839,16 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
         kw = dict(a_mean=mean, a_rstd=rstd, b_colsum=b.float().sum(1))
     outs = {}
     from conftest import gemm_variant
-    for staged in (1, 0):
-        with gemm_variant(0 if staged else _lib.GV_FLAT_TRAIN):
+    # staged (default) / fragment-layout epilogue, and the 256x256 ping-pong kernel with the
+    # training epilogues (GV_TILE_256 forces it; the automatic choice takes it for long K and wide N)
+    for key, v in (("staged", 0), ("flat", _lib.GV_FLAT_TRAIN), ("pp256", _lib.GV_TILE_256)):
+        if key == "pp256" and K % 64:
+            continue
+        with gemm_variant(v):
             pre = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
             y = T.gemm_train(a, b, mode=1, act=act, aux=pre, bias=bias, drop_p=0.2, seed=5, **kw)
             dpre = T.gemm_train(a, b, mode=2, act=act, aux=pre, drop_p=0.2, seed=5, residual=res)
-            outs[staged] = (pre, y, dpre)
-    for x0, x1 in zip(outs[1], outs[0]):
-        assert torch.equal(x0, x1)
+            outs[key] = (pre, y, dpre)
+    for key in outs:
+        for x0, x1 in zip(outs["staged"], outs[key]):
+            assert torch.equal(x0, x1), key

@@ -17,6 +17,11 @@ from hv_amd.trainer import HVTrainer  # noqa: E402
 
 what = sys.argv[1] if len(sys.argv) > 1 else "all"
 dev = torch.device("cuda")
+if os.environ.get("HV_GEMM_VARIANT"):
+    # A/B only: the training forward / backward run outside any RunCtx (the autograd engine's
+    # device thread would not see a context), so the process-wide default options are patched here
+    from hv_amd import runtime as _rt
+    _rt.DEFAULT_OPTIONS = _rt.HVOptions(gemm_variant=int(os.environ["HV_GEMM_VARIANT"], 0))
 
 
 def tiny(prec):
