@@ -338,9 +338,9 @@ def main():
         model(x)
     n_l, avg_ms, avg_flop, gemm_tflops, avg_bytes = gt.summary()
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
-    if not os.path.exists(tf):
-        tf = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    # newest round's PMC record (rocprofv3 passes of this workload on this build's kernels)
+    tf = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r03", "r02", "r01"))
+               if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"))
     if a.size == 640 and a.batch == 16 and a.precision == "bf16" and os.path.exists(tf):
         with open(tf) as f:
             traffic = json.load(f).get("gemm", {}).get("bytes_per_launch")

@@ -21,7 +21,7 @@ from collections import defaultdict
 FAMILIES = {
     "gemm": ("gemm_glds_kernel", "gemm_kernel", "gemm_pp256_kernel", "gemm_sk_kernel", "k_conv3x3_c32",
              "gemm_sk2_kernel", "gemm_stk_kernel"),
-    "mhc_fused": ("mhc_fused_kernel", "mhc_fused2_kernel", "mhc_fused3_kernel"),
+    "mhc_fused": ("mhc_fused_kernel", "mhc_fused2_kernel", "mhc_fused_pipe_kernel"),
 }
 
 

@@ -14,8 +14,8 @@ import sys
 from collections import defaultdict
 
 FAMILIES = {
-    "gemm": ("gemm_glds_kernel", "gemm_kernel", "gemm_pp256_kernel", "gemm_sk_kernel", "k_conv3x3_c32"),
-    "mhc_fused": ("mhc_fused_kernel",),
+    "gemm": ("gemm_glds_kernel", "gemm_kernel", "gemm_pp256_kernel", "gemm_sk_kernel", "gemm_skr_kernel", "k_conv3x3_c32"),
+    "mhc_fused": ("mhc_fused_kernel", "mhc_fused2_kernel", "mhc_fused_pipe_kernel"),
 }
 
 
