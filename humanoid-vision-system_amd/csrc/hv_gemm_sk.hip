@@ -216,7 +216,12 @@ __global__ void __launch_bounds__(256, 2) gemm_sk_kernel(const hv_gemm_desc d, i
     // the stores issued first the next tile's k-step 1 wait covered their write acknowledgements
     // (one exposed store round trip per tile; the output stream ran at ~2 TB/s, tools/sk_probe.py)
     const bool fast = full && c_bf && !d.residual && DIAG == 0;
-    const bool early_next = fast && next >= 0 && nk >= 2;
+    // the early DMA path holds a workgroup barrier, so its condition must be WORKGROUP-uniform:
+    // `full` is per wave (an edge column tile with N % 128 in 64..127 has full wc=0 waves and
+    // partial wc=1 waves), the whole 128x128 tile being in range is not -- and implies `full`
+    // (hence `fast`) for all four waves
+    const bool tile_full = vec && m0 + SK_BM <= d.M && n0 + SK_BN <= d.N;
+    const bool early_next = fast && tile_full && next >= 0 && nk >= 2;
     // ---- register epilogue: lane (fr, fg) owns columns col0 .. col0+15 of rows m0 + wr*64 + a*16 + fr
     if (fast) {
       // full bf16 tile, no residual: every value first (acc dies as it goes), then the next tile's
@@ -602,7 +607,9 @@ int hv_gemm_smallk(const hv_gemm_desc& d0, hipStream_t s, bool force) {
   if (!force && ntiles < 2L * cus) return HV_EUNSUPPORTED;   // under one persistent round: nothing to overlap
   hv_diag_count(HV_KF_GEMM_SMALLK);
   if ((d.variant & (HV_GV_SK_RES3 | HV_GV_SK_RES4)) && !d.residual && (d.K == 192 || d.K == 256) &&
-      !(d.variant & (HV_GV_SK_DIAG1 | HV_GV_SK_DIAG2)) && (!d.a_mean || d.M >= 4)) {
+      !(d.variant & (HV_GV_SK_DIAG1 | HV_GV_SK_DIAG2)) && (!d.a_mean || (d.M >= 4 && d.M % 4 == 0))) {
+    // (the LN row statistics ride the A DMA as 16-byte groups of 4 rows: with M % 4 != 0 the
+    // clamped last group would shift rows, so those shapes take the streaming kernel)
     // B-resident column-stationary kernel: one workgroup per CU, each on one column block
     const int tilesM = hv_cdiv(d.M, SK_BM), tilesN = hv_cdiv(d.N, SK_BN);
     const int slots = tilesN > cus ? 1 : cus / tilesN;

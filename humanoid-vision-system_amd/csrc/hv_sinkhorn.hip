@@ -704,7 +704,7 @@ extern "C" int hv_sinkhorn_group_backward(const hv_sinkhorn_bwd_entry* tab, int 
   return HV_OK;
 }
 
-extern "C" int hv_abi_version(void) { return 1; }
+extern "C" int hv_abi_version(void) { return HV_ABI_VERSION; }
 extern "C" void hv_struct_sizes(int* out5) {
   out5[0] = (int)sizeof(hv_sinkhorn_entry);
   out5[1] = (int)sizeof(hv_gemm_desc);

@@ -7,6 +7,8 @@ There is no fallback: if the library is missing every op raises.
 from __future__ import annotations
 
 import ctypes as C
+import glob
+import hashlib
 import os
 import threading
 
@@ -23,10 +25,31 @@ MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
+ABI_VERSION = 2          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
 _LIB = None
 _LOCK = threading.Lock()
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # HV_LIB_PATH: load another build of the same C ABI (A/B of two builds in one GPU call)
-LIB_PATH = os.environ.get("HV_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhvs.so")
+LIB_PATH = os.environ.get("HV_LIB_PATH") or os.path.join(_PKG, "hv_amd", "libhvs.so")
+
+
+def source_hash() -> str | None:
+    """The Makefile's HV_SRC_HASH recomputed from the sources in this tree (None when they are
+    absent): sha256 over the sorted csrc/*.hip, csrc/*.h, ../include/*.h, then the Makefile."""
+    files = sorted(glob.glob("csrc/*.hip", root_dir=_PKG) + glob.glob("csrc/*.h", root_dir=_PKG) +
+                   glob.glob("../include/*.h", root_dir=_PKG)) + ["Makefile"]
+    h = hashlib.sha256()
+    for f in files:
+        p = os.path.join(_PKG, f)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    return lib().hv_build_id().decode()
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -119,6 +142,7 @@ _SIGS = {
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),
+    "hv_build_id": ([], C.c_char_p),
     "hv_struct_sizes": ([vp], None),
     "hv_symeig_work_doubles": ([i32], C.c_size_t),
     "hv_symeig_group": ([vp, vp, i32, vp], i32),
@@ -236,6 +260,16 @@ def lib():
                         "`make -C humanoid-vision-system_amd` (there is no CPU fallback)")
                 handle = C.CDLL(LIB_PATH)
                 _declare(handle)
+                if handle.hv_abi_version() != ABI_VERSION:
+                    raise RuntimeError(f"libhvs ABI {handle.hv_abi_version()} != binding ABI {ABI_VERSION}")
+                want = source_hash()
+                got = handle.hv_build_id().decode()
+                # the in-tree library must be built from exactly these sources (A/B builds loaded
+                # through HV_LIB_PATH are older builds by design)
+                if not os.environ.get("HV_LIB_PATH") and want is not None and got != want:
+                    raise RuntimeError(
+                        f"stale libhvs.so: built from sources {got}, tree has {want}; "
+                        "rebuild with `make -C humanoid-vision-system_amd`")
                 _LIB = handle
     return _LIB
 

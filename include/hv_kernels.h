@@ -32,7 +32,14 @@ enum { HV_ACT_NONE = 0, HV_ACT_RELU = 1, HV_ACT_SILU = 2, HV_ACT_GELU = 3,
        HV_ACT_LEAKY = 4 /* slope 0.1 */, HV_ACT_SIGMOID = 5 };
 enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
 
+/* ABI version: 2 since hv_adamw gained `steps`, hv_mhc_fused_supported gained `variant`,
+ * hv_mhc_fused_args grew by 8 bytes and the hv_gemm_set_* / hv_mhc_fused_set_* setters were
+ * removed (round 3).  Bindings compare it with the version they were written against. */
+#define HV_ABI_VERSION 2
 int hv_abi_version(void);
+/* build provenance: a hash of the sources (csrc/*.hip, csrc/*.h, include/*.h, Makefile) the
+ * library was compiled from; the Python loader recomputes it and refuses a stale build */
+const char* hv_build_id(void);
 /* lets bindings verify their struct mirrors */
 void hv_struct_sizes(int* out5);  /* sizeof of the 5 ABI structs, in declaration order */
 

@@ -14,7 +14,7 @@ from conftest import GOLDEN, MODEL_CFG, ROOT
 def _declared():
     src = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("hv_kernels.h", "hv_tuning.h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|void)\s+(hv_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|void|const char\s*\*)\s*(hv_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -25,7 +25,15 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(_lib.EXPORTED), set(declared) ^ set(_lib.EXPORTED)
-    assert lib.hv_abi_version() == 1
+    assert lib.hv_abi_version() == _lib.ABI_VERSION == 2
+
+
+def test_library_built_from_this_tree():
+    """Build provenance: the loaded libhvs.so carries the hash of the sources it was compiled
+    from (Makefile HV_SRC_HASH); it equals the hash of the sources in this tree."""
+    from hv_amd import _lib
+    assert _lib.source_hash() is not None
+    assert _lib.build_id() == _lib.source_hash()
 
 
 def test_no_gpu_calls_needed_for_size_queries():

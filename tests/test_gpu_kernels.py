@@ -254,7 +254,11 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
 SMALLK_CASES = [  # (kind, M, N, K): 1-8 k-tiles, ragged M / N (scalar store tail), every epilogue form
     ("plain", 4096, 512, 64), ("plain", 1000, 777, 128), ("ln_gelu", 1500, 1024, 256), ("gelu_res", 2048, 768, 512),
     ("res32_mod", 1200, 640, 256), ("scale_f32", 700, 384, 192), ("conv1x1", 2 * 40 * 40, 256, 128),
-    ("ln_gelu", 8192, 1024, 256), ("ln_gelu", 6416, 3072, 256), ("conv1x1", 2 * 56 * 56, 512, 256)]
+    ("ln_gelu", 8192, 1024, 256), ("ln_gelu", 6416, 3072, 256), ("conv1x1", 2 * 56 * 56, 512, 256),
+    # bf16 output, no residual, N % 128 in 64..127: edge column tiles whose waves differ in
+    # "full" (the early next-tile DMA must stay workgroup-uniform); M % 4 != 0 under LN
+    ("ln_gelu", 1501, 320, 256), ("bf16", 4096, 448, 128), ("ln_gelu", 26003, 448, 256),
+    ("bf16", 20000, 320, 192)]
 
 
 @pytest.mark.parametrize("kind,M,N,K", SMALLK_CASES)
@@ -274,6 +278,9 @@ def test_gemm_smallk_equals_ring(gpu_device, kind, M, N, K):
     if kind == "plain":
         run = lambda: ops.gemm(a, b, bias=bias, out_dtype=torch.float32)  # noqa: E731
         ref = af @ bfl.T + bias.cpu()
+    elif kind == "bf16":
+        run = lambda: ops.gemm(a, b, bias=bias, act="gelu")  # noqa: E731
+        ref = F.gelu(af @ bfl.T + bias.cpu())
     elif kind == "ln_gelu":
         mean = af.mean(1)
         rstd = 1.0 / torch.sqrt(af.var(1, unbiased=False) + 1e-5)
