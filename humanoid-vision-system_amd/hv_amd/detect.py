@@ -323,12 +323,16 @@ class GraphRunner:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.static_out = model(self.static_in, task=self.task)
+        # thread_local: other threads (the engine's worker pool) may keep running eager forwards
+        # on their own streams while this thread captures
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            self.static_out, ctx = model.forward_eval(self.static_in, task=self.task)
         # the graph reads buffers that live outside its memory pool (the grouped Sinkhorn /
-        # coefficient-prep program and its device tables, frozen plans): keep the capture's RunCtx
-        # alive, or a later set_options / set_precision / cache rebuild would free them under it
-        self.ctx = model._last_ctx
+        # coefficient-prep program and its device tables, frozen plans): keep THIS capture's
+        # RunCtx alive (the one its forward returned -- not a per-model "latest" slot another
+        # thread's forward may have overwritten), or a later set_options / set_precision / cache
+        # rebuild would free them under it
+        self.ctx = ctx
         self.version = model._watch.snapshot()
 
     def replay(self) -> Dict[str, Any]:
@@ -400,7 +404,6 @@ class HybridVisionSystem(nn.Module):
                             if isinstance(a, MultiHeadManifoldAttention)}
         self._frozen: Optional[Tuple[Any, RunCtx]] = None
         self._sk_cache: Dict[str, Any] = {}
-        self._last_ctx: Optional[RunCtx] = None   # the RunCtx of the latest eval forward
         self._watch = VersionWatch(self)
 
     # ---- precision / caching controls
@@ -455,8 +458,16 @@ class HybridVisionSystem(nn.Module):
             # training step: BN batch statistics, dropout, autograd over HIP kernels
             from .train_model import system_forward
             return system_forward(self, x, targets, task, compute_loss)
+        return self.forward_eval(x, targets, task, compute_loss)[0]
+
+    def forward_eval(self, x: torch.Tensor, targets=None, task: str = "detection",
+                     compute_loss: bool = False) -> Tuple[Dict[str, Any], RunCtx]:
+        """The eval forward, returning also the RunCtx it ran under (the prepared coefficients and
+        device tables its kernels read): a graph capture pins exactly that context.  Re-entrant --
+        nothing per call is stored on the module, so concurrent forwards from several threads
+        (the engine's worker pool) do not interfere."""
+        require_cuda(x, "HybridVisionSystem")
         ctx = self._ctx()
-        self._last_ctx = ctx
         with torch.no_grad(), use_ctx(ctx):
             if x.dtype == torch.float32 and x.is_contiguous():
                 bb = self.backbone.forward_nhwc(None, image=x)     # direct stem conv from NCHW
@@ -488,7 +499,7 @@ class HybridVisionSystem(nn.Module):
             outputs["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
             outputs["final_features"] = final
         ctx.join_prep()                        # side-stream prep joined even if no mHC ran
-        return outputs
+        return outputs, ctx
 
     def _final_features(self, fused: Dict[str, torch.Tensor]) -> torch.Tensor:
         """hybrid_vision.py:369-402 with shim S6: GAP x3 -> cat -> mHC(1792) -> Linear/ReLU/Linear."""

@@ -344,10 +344,11 @@ class StreamingPipeline:
         self._capture()
 
     def _forward(self):
+        """-> (outputs, the RunCtx the forward ran under)."""
         H, W = self.input_hw
         x = ops.preprocess(self.frame, H, W, bgr=True, dtype=self.dtype, nhwc=True, out=self.inp,
                            resample=self.resample)
-        return self.model(x, task="detection")
+        return self.model.forward_eval(x, task="detection")
 
     def _capture(self):
         """Graph 1: preprocess + forward + decode.  The NMS plan's device table is then built
@@ -358,15 +359,15 @@ class StreamingPipeline:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s), torch.no_grad():
             for _ in range(2):
-                out = self._forward()
+                out = self._forward()[0]
                 ops.NmsPlan(out["decoded"], *self.nms_args).run()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         del out
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph), torch.no_grad():
-            self.outputs = self._forward()
-        self.ctx = self.model._last_ctx           # buffers graph 1 reads outside its pool (detect.GraphRunner)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"), torch.no_grad():
+            # ctx: the buffers graph 1 reads outside its pool, pinned (detect.GraphRunner)
+            self.outputs, self.ctx = self._forward()
         self._nms = ops.NmsPlan(self.outputs["decoded"], *self.nms_args)
         torch.cuda.synchronize()
         self.nms_graph = torch.cuda.CUDAGraph()

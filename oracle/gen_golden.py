@@ -7,7 +7,7 @@ it is imported at run time; only its outputs (inputs + expected outputs) are sto
 
 Weights come from oracle/weights.py (regenerated from a formula on both sides).
 
-Usage:  python oracle/gen_golden.py [--only sinkhorn,mhc,blocks,model]
+Usage:  python oracle/gen_golden.py [--only sinkhorn,mhc,blocks,model,...,bf16ref] [--bf16ref mhc,model,train]
 """
 from __future__ import annotations
 
@@ -389,6 +389,130 @@ def gen_train(hv, only=None):
         del model, m
 
 
+# ------------------------------------------------------------------ G8 reference bf16 (S8)
+def _rel(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / (b.norm() + 1e-300))
+
+
+def gen_bf16ref(ml, hv, parts):
+    """The reference's OWN bf16 numerics (S8, oracle/autocast_emu.py: CUDA autocast's op policy
+    emulated on CPU) on the fixtures' inputs, so that the HIP bf16 mode is held to a multiple of
+    the error the reference itself makes in bf16 (instead of fixed bounds):
+      mhc   -- every (D, e) of G2, both weight families, the reference's own autocast region
+               (ManifoldHyperConnection.forward body, manifold_layers.py:247-263) in bf16;
+      model -- base 640 B=2 eval (fixture model_base_wc_640_b2), the whole forward under the
+               policy (the trainer's / engine's autocast region, mhc_trainer.py:241);
+      train -- base 224 B=2 train step (fixture train_base_224_b2) under the policy, and base 640
+               B=2 (config C's resolution; x seed 7, target seed 11) in fp32 AND under the policy
+               (no fp64 at 640: the GPU test compares HIP bf16 with HIP fp32 there).
+    Each record stores the reference-bf16 outputs' errors against the reference's fp64 (or fp32)
+    run -- the anchors the GPU tests multiply."""
+    from oracle.autocast_emu import CudaAutocastBF16, MhcOnly
+    if "mhc" in parts:
+        print("G8 mhc bf16ref")
+        for fam in ("wc", "init"):
+            for D, e in MHC_CASES:
+                torch.manual_seed(0)
+                m = ml.ManifoldHyperConnection(D, expansion_rate=e).eval()
+                W.load_formula_weights(m, fam)
+                x = mhc_input(D, e)
+                g = np.load(os.path.join(OUT, f"mhc_{fam}_D{D}_e{e}.npz"))
+                with torch.no_grad(), MhcOnly(ml):
+                    yb = m(x)
+                y64 = torch.from_numpy(g["y64"])
+                rec = {"err_vs_f64": _rel(yb, y64), "maxabs_vs_f64": float((yb.double() - y64.double()).abs().max())}
+                if D <= 512:
+                    rec["y"] = yb
+                save(f"mhc_{fam}_D{D}_e{e}_bf16ref", **rec)
+                print(f"  {fam} D={D} e={e}: rel-L2 {rec['err_vs_f64']:.4f}")
+    if "model" in parts:
+        print("G8 model bf16ref")
+        for tag, tiny, fam, S, B, sub in MODEL_CASES:
+            if tag != "base_wc_640_b2":
+                continue
+            t0 = time.time()
+            torch.manual_seed(0)
+            model = hv.HybridVisionSystem({"image_size": S}).eval()
+            W.load_formula_weights(model, fam)
+            g = np.load(os.path.join(OUT, f"model_{tag}.npz"))
+            x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
+            with torch.no_grad(), CudaAutocastBF16() as mode:
+                out = model(x, task="detection")
+            rec = {"policy_counts": np.array([mode.counts["lower"], mode.counts["fp32"]])}
+            agree = []
+            for s in range(3):
+                step = sub if s == 0 else 1
+                pr = out["predictions"][f"scale_{s}"][:, :, ::step].float()
+                bx = out["decoded"][f"scale_{s}"]["boxes"][:, :, ::step].float()
+                rec[f"pred{s}_err_vs_f64"] = _rel(pr, torch.from_numpy(g[f"pred{s}_f64"]))
+                rec[f"boxes{s}_err_vs_f32"] = _rel(bx, torch.from_numpy(g[f"boxes{s}"]))
+                ci = out["decoded"][f"scale_{s}"]["class_indices"].numpy()
+                sure = g[f"margin{s}"] >= 1e-2
+                if sure.any():
+                    agree.append(float((ci[sure] == g[f"cls{s}_f64"][sure]).mean()))
+            rec["class_agreement_margin_1e-2"] = np.array(agree)
+            ff = out["final_features"].float()
+            rec["final_err_vs_f64"] = _rel(ff, torch.from_numpy(g["final_features_f64"]))
+            save(f"model_{tag}_bf16ref", **rec)
+            print(f"  {tag}: {time.time() - t0:.1f}s", {k: v for k, v in rec.items() if "err" in k}, agree)
+    if "train" in parts:
+        print("G8 train bf16ref")
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "humanoid-vision-system_amd"))
+        from hv_amd.targets import synthetic_targets
+        from oracle.cases import grad_probe
+
+        def step(S, B, xseed, tseed, bf16):
+            torch.manual_seed(0)
+            model = hv.HybridVisionSystem({"image_size": S})
+            W.load_formula_weights(model, "wc")
+            for mod in model.modules():
+                if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+                    mod.p = 0.0
+            model.train()
+            x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(xseed))
+            tg = synthetic_targets(B, S, seed=tseed)
+            if bf16:
+                with CudaAutocastBF16():
+                    out = model(x, targets=tg, compute_loss=True)
+                    loss = out["loss"]
+                    loss["total_loss"].float().backward()
+            else:
+                out = model(x, targets=tg, compute_loss=True)
+                loss = out["loss"]
+                loss["total_loss"].backward()
+            r = {"total_loss": float(loss["total_loss"])}
+            for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
+                r[k] = float(loss[k])
+            r["preds"] = [out["predictions"][f"scale_{s}"].detach().float() for s in range(3)]
+            r["grad_norm"] = np.array([p.grad.double().norm().item() if p.grad is not None else -1.0
+                                       for p in model.parameters()])
+            r["grad_probe"] = np.array([float(p.grad.double().flatten() @ grad_probe(n, p.numel())) / math.sqrt(p.numel())
+                                        if p.grad is not None else 0.0 for n, p in model.named_parameters()])
+            return r
+
+        t0 = time.time()
+        g = np.load(os.path.join(OUT, "train_base_224_b2.npz"))
+        r = step(int(g["S"]), int(g["B"]), 1, int(g["target_seed"]), True)
+        rec = {k: np.float64(r[k]) for k in ("total_loss", "coord_loss", "obj_loss", "noobj_loss", "cls_loss")}
+        rec["grad_norm"], rec["grad_probe"] = r["grad_norm"], r["grad_probe"]
+        for s in range(3):
+            rec[f"pred{s}_err_vs_f64"] = _rel(r["preds"][s], torch.from_numpy(g[f"pred{s}_f64"]))
+        save("train_base_224_b2_bf16ref", **rec)
+        print(f"  224: {time.time() - t0:.1f}s loss {rec['total_loss']:.5f} vs f64 {float(g['total_loss_f64']):.5f}")
+        t0 = time.time()
+        r32 = step(640, 2, 7, 11, False)
+        r16 = step(640, 2, 7, 11, True)
+        rec = {}
+        for k in ("total_loss", "coord_loss", "obj_loss", "noobj_loss", "cls_loss"):
+            rec[k + "_f32"], rec[k + "_bf16"] = np.float64(r32[k]), np.float64(r16[k])
+        rec["grad_norm_f32"], rec["grad_norm_bf16"] = r32["grad_norm"], r16["grad_norm"]
+        rec["grad_probe_f32"], rec["grad_probe_bf16"] = r32["grad_probe"], r16["grad_probe"]
+        rec["logits_rel_l2_bf16_vs_f32"] = np.array([_rel(r16["preds"][s], r32["preds"][s]) for s in range(3)])
+        save("train_base_640_b2_ref", **rec)
+        print(f"  640: {time.time() - t0:.1f}s logits bf16 vs f32 {rec['logits_rel_l2_bf16_vs_f32']}")
+
+
 # ------------------------------------------------------------------ G6 post-processing
 def gen_nms(yh):
     """YOLODetectionHead.post_process (yolo_head.py:571-731) on random decoded outputs."""
@@ -431,6 +555,7 @@ def main():
     ap.add_argument("--only", default="sinkhorn,stability,mhc,blocks,model,layout,train,nms,preproc")
     ap.add_argument("--models", default="")
     ap.add_argument("--trains", default="")
+    ap.add_argument("--bf16ref", default="mhc,model,train")
     a = ap.parse_args()
     torch.set_num_threads(8)
     ml, vb, ve, yh, hv = apply_shims()
@@ -455,6 +580,8 @@ def main():
         gen_preproc()
     if "seeded" in parts:
         gen_seeded_init(hv)
+    if "bf16ref" in parts:
+        gen_bf16ref(ml, hv, [p for p in a.bf16ref.split(",") if p])
 
 
 

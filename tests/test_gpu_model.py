@@ -41,16 +41,29 @@ def test_mhc_fp32_matches_reference(gpu_device, fam, D, e):
         np.testing.assert_allclose(y, g["y"], rtol=0, atol=1e-3)
 
 
+@pytest.mark.parametrize("fam", ["wc", "init"])
 @pytest.mark.parametrize("D,e", cases.MHC_CASES)
-def test_mhc_bf16_agreement(gpu_device, D, e):
+def test_mhc_bf16_agreement(gpu_device, fam, D, e):
+    """bf16 mode held to the reference's OWN bf16 error: the reference under its autocast policy
+    (S8, oracle/autocast_emu.py: bf16 matmuls/linears, fp32 LayerNorm -- manifold_layers.py:186,
+    248) is `err_vs_f64` rel-L2 from its fp64 run on the same input (fixture *_bf16ref); the HIP
+    bf16 mHC must be within 2x that.  The well-conditioned family also keeps the absolute bound
+    5e-2 (centred coefficients keep HIP at the bf16 level; the reference's un-centred
+    H_res + H_post sum loses 0.02-0.12 there and 0.18-1.2 at init)."""
+    from conftest import record_parity
     from hv_amd import ManifoldHyperConnection
-    g = golden(f"mhc_wc_D{D}_e{e}")
+    g = golden(f"mhc_{fam}_D{D}_e{e}")
+    gb = golden(f"mhc_{fam}_D{D}_e{e}_bf16ref")
     m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
-    W.load_formula_weights(m, "wc")
+    W.load_formula_weights(m, fam)
     m = m.to(gpu_device).eval()
     y = m(cases.mhc_input(D, e).to(gpu_device)).float().cpu().numpy()
-    # bf16 activations, fp32 coefficients; centred coefficients keep this at the bf16 level
-    assert rel_l2(y, g["y64"]) < 5e-2
+    err, ref = rel_l2(y, g["y64"]), float(gb["err_vs_f64"])
+    record_parity(f"mhc_bf16_{fam}_D{D}_e{e}", {"hip_bf16_vs_f64": err, "ref_bf16_vs_f64": ref,
+                                                 "ratio": err / ref, "bound_ratio": 2.0})
+    assert err <= 2.0 * ref, (err, ref)
+    if fam == "wc":
+        assert err < 5e-2
 
 
 @pytest.mark.parametrize("D,e,T,with_res", [(32, 4, 64, False), (32, 4, 1000, False), (64, 4, 64, False),
@@ -164,6 +177,11 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
       * the first `nref` images (the reference fixture's input) agree with the reference's fp64
         run at the bf16 contract of test_model_bf16_agreement (rel-L2 < 0.1 on logits, >= 90%
         class agreement on cells with top-1/top-2 margin >= 1e-2);
+      * at 640 they are ALSO held to the reference's own bf16 numerics (fixture
+        model_base_wc_640_b2_bf16ref: the reference under CUDA autocast's bf16 policy, S8):
+        logits (vs fp64), boxes (vs the reference fp32 run) and final features no worse than
+        the reference's own bf16 error (ratio <= 1.0; measured ~0.25-0.35), class agreement no
+        lower;
       * the fp32 HIP path on the same batch meets the fp32 contract on those images (atol 1e-3),
         and on EVERY image of the batch the bf16 step stays near the fp32 step: logits rel-L2
         < 0.1, final features < 0.05, boxes per scale < 1.5x the measured worst.  Measured
@@ -203,11 +221,21 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
         assert counts[fam] > 0, (fam, counts)
     assert counts["glds_128x128"] + counts["glds_64x128"] + counts["glds_64x64"] + counts["glds_128x64"] > 0
     assert counts["attn_scalar"] == 0
-    agree = []
+    agree, anchor = [], {}
+    gb = golden(f"model_{fixture}_bf16ref") if S == 640 else None
     for s in range(3):
         step = sub if s == 0 else 1
         pr = b16["pred"][f"scale_{s}"][:nref, :, ::step]
-        assert rel_l2(pr, g[f"pred{s}_f64"]) < 0.1, s
+        e_log = rel_l2(pr, g[f"pred{s}_f64"])
+        assert e_log < 0.1, s
+        e_box = rel_l2(b16["boxes"][f"scale_{s}"][:nref, :, ::step], g[f"boxes{s}"])
+        if gb is not None:
+            # S8 anchor: the reference under its own autocast policy on the same images
+            r_log, r_box = float(gb[f"pred{s}_err_vs_f64"]), float(gb[f"boxes{s}_err_vs_f32"])
+            anchor[f"scale_{s}"] = {"logits_hip": round(e_log, 5), "logits_ref_bf16": round(r_log, 5),
+                                    "logits_ratio": round(e_log / r_log, 4), "boxes_hip": round(e_box, 5),
+                                    "boxes_ref_bf16": round(r_box, 5), "boxes_ratio": round(e_box / r_box, 4)}
+            assert e_log <= 1.0 * r_log and e_box <= 1.0 * r_box, (s, anchor[f"scale_{s}"])
         ci = b16["cls"][f"scale_{s}"][:nref]
         sure = g[f"margin{s}"] >= 1e-2
         if sure.any():
@@ -215,6 +243,15 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
     assert agree and min(agree) > 0.9, agree
     rec = {"config": f"base {S}x{S} B={B} bf16 hipGraph replay", "fixture": fixture,
            "class_agreement_vs_ref_f64_margin_1e-2": [round(float(a), 5) for a in agree]}
+    if gb is not None:
+        e_fin = rel_l2(b16["final"][:nref], g["final_features_f64"])
+        r_fin = float(gb["final_err_vs_f64"])
+        anchor["final_features"] = {"hip": round(e_fin, 5), "ref_bf16": round(r_fin, 5), "ratio": round(e_fin / r_fin, 4)}
+        anchor["class_agreement_ref_bf16"] = [round(float(a), 5) for a in gb["class_agreement_margin_1e-2"]]
+        anchor["bound"] = "HIP bf16 error <= 1.0x the reference's own bf16 error (S8) on every output"
+        rec["vs_reference_bf16"] = anchor
+        assert e_fin <= 1.0 * r_fin, anchor
+        assert min(agree) >= min(gb["class_agreement_margin_1e-2"]), (agree, anchor)
     m32 = _build("base", "wc", "fp32", gpu_device)
     with torch.no_grad():
         m32(x)
@@ -447,6 +484,52 @@ def test_graph_survives_option_change(gpu_device):
     for k in ref:
         assert torch.equal(a[k], ref[k]), k
         assert torch.equal(b[k], ref[k]), k
+
+
+def test_graph_capture_concurrent_with_eager_forwards(gpu_device):
+    """The engine's worker pool (reference src/inference/engine.py:389-471, 4 workers :577,611-615)
+    may run eager forwards while another thread captures: the runner pins the RunCtx ITS capture
+    forward ran under (forward_eval returns it; nothing per call is stored on the module), so a
+    concurrent forward cannot make it pin a foreign context; the capture runs in thread-local
+    capture mode, so the other thread's launches and allocations do not invalidate it.  After the other thread's contexts are dropped and the
+    cache freed, the replay still equals the eager forward bit for bit."""
+    import threading
+    from hv_amd import _lib
+    m = _build("tiny", "wc", "bf16", gpu_device)
+    x = torch.randn(2, 3, 128, 128, generator=torch.Generator().manual_seed(11)).to(gpu_device)
+    with torch.no_grad():
+        ref = {k: v.clone() for k, v in m(x)["predictions"].items()}
+    stop, errors, seen = threading.Event(), [], []
+
+    def worker():
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s), torch.no_grad():
+                while not stop.is_set():
+                    out, ctx = m.forward_eval(x)
+                    seen.append(id(ctx))
+                    s.synchronize()
+                    del out, ctx
+        except Exception as e:                     # noqa: BLE001  (reported by the main thread)
+            errors.append(repr(e))
+
+    t = threading.Thread(target=worker)
+    t.start()
+    try:
+        with torch.no_grad():
+            runner = m.capture(x)
+    finally:
+        stop.set()
+        t.join(timeout=60)
+    assert not t.is_alive() and not errors, errors
+    assert seen and runner.ctx is not None and runner.ctx.plans
+    with torch.no_grad():
+        m.set_options(mhc_variant=_lib.MV_PIPE)       # drops the model's caches
+        torch.cuda.empty_cache()
+        out = runner(x, owned=True)["predictions"]
+        torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
 
 
 def test_model_pipelined_mhc_bitwise_equal(gpu_device):

@@ -638,53 +638,118 @@ def _base_train_step(gpu_device, precision, B, S, seed_x, target_seed):
     return loss, preds, dict(norms), finite
 
 
+def _anchor_check(mine: dict, ref: dict, what: str):
+    """Per-group errors held to the reference's own bf16 errors (S8): each group within 3x its
+    reference error (floor 1e-2: near-exact groups would otherwise test rounding), and the mean
+    over groups within 2x the reference mean."""
+    bad = {k: (mine[k], ref[k]) for k in ref if mine.get(k, 1.0) > 3.0 * max(ref[k], 1e-2)}
+    assert not bad, (what, bad)
+    m_mean = float(np.mean([mine[k] for k in ref]))
+    r_mean = float(np.mean(list(ref.values())))
+    assert m_mean <= 2.0 * r_mean, (what, m_mean, r_mean)
+    return {"hip_mean": m_mean, "ref_bf16_mean": r_mean}
+
+
 def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
     """Config C's object in its own precision: the base model's bf16 training step (bf16
     activations / GEMMs, fp32 parameters, coefficients and reductions -- the reference's autocast
-    contract, manifold_layers.py:186,248; loss yolo_head.py:374-465) at
-      (1) 224x224 B=2 against the reference fixture train_base_224_b2 (its fp64 run): total loss,
-          and the gradient norm of every (top-level module, clip group) -- the quantities the
-          trainer's per-group clipping (mhc_trainer.py:342-383) acts on;
-      (2) 640x640 B=2 (config C's resolution) against the fp32 HIP step on the same batch:
-          loss components, per-group gradient norms, finiteness of every gradient.
-    Bounds: this forward is ill-conditioned in train mode (BatchNorm batch statistics of bf16
-    activations at init; the reference's OWN fp32 run is 9% rel-L2 from fp64 on the head logits
-    at 224), and bf16 rounding is 2^16x fp32's.  Measured on the round-3 build
-    (profiles/r03/parity/train_bf16_base.json): (1) total loss 2.5% from the reference fp64 run,
-    group gradient norms 10-21%; (2) total loss 0.6% from the fp32 HIP step, group norms 2-20%
-    (the logits themselves differ by ~0.93 rel-L2 in train mode -- recorded, not bounded).
-    The bounds are ~2x the measured worst: loss 5% / 1.5%, group norms 45%.
-    """
+    contract, manifold_layers.py:186,248, mhc_trainer.py:241; loss yolo_head.py:374-465), held to
+    the REFERENCE's OWN bf16 error (S8: the reference run under CUDA autocast's bf16 op policy,
+    oracle/autocast_emu.py, fixtures *_bf16ref / train_base_640_b2_ref):
+      (1) 224x224 B=2 vs the reference's fp64 run (fixture train_base_224_b2): total loss within
+          3x the reference-bf16 loss error; per (top-level module, clip group) gradient norm --
+          the quantities the trainer's per-group clipping (mhc_trainer.py:342-383) acts on --
+          within 3x the reference-bf16 group error, mean over groups within 2x; head logits within
+          1.25x the reference-bf16 logits error;
+      (2) 640x640 B=2 (config C's resolution), HIP bf16 vs HIP fp32 on the same batch, against the
+          reference's bf16-vs-fp32 on that same batch (x seed 7, targets seed 11): the same loss /
+          group / logits bounds, plus finiteness of every gradient.
+    Train-mode logits at init are NOT a usable bf16 observable: BatchNorm batch statistics over
+    B=2 amplify rounding, and the reference's own bf16 logits are 0.89-0.96 rel-L2 from its
+    fp64 / fp32 runs (measured on the fixtures) -- the loss and gradient groups are."""
     import json
     import os
     from conftest import GOLDEN, golden, record_parity
     g = golden("train_base_224_b2")
+    gb = golden("train_base_224_b2_bf16ref")
     names = json.load(open(os.path.join(GOLDEN, "train_base_param_names.json")))
     B, S = int(g["B"]), int(g["S"])
-    loss16, _, n16, fin16 = _base_train_step(gpu_device, "bf16", B, S, 1, int(g["target_seed"]))
+    loss16, p16, n16, fin16 = _base_train_step(gpu_device, "bf16", B, S, 1, int(g["target_seed"]))
     assert fin16
-    ref_groups = _group_norms([(n, v) for n, v in zip(names, g["grad_norm_f64"]) if v >= 0])
-    my_groups = _group_norms(n16.items())
+    ref64 = _group_norms([(n, v) for n, v in zip(names, g["grad_norm_f64"]) if v >= 0])
+    refb = _group_norms([(n, v) for n, v in zip(names, gb["grad_norm"]) if v >= 0])
+    mine = _group_norms(n16.items())
     l64 = float(g["total_loss_f64"])
+    e_groups = {k: abs(mine.get(k, 0.0) / v - 1) for k, v in ref64.items() if v > 0}
+    r_groups = {k: abs(refb[k] / v - 1) for k, v in ref64.items() if v > 0}
+    e_log = {s: float(np.linalg.norm(p16[f"scale_{s}"] - g[f"pred{s}_f64"]) / np.linalg.norm(g[f"pred{s}_f64"]))
+             for s in range(3)}
+    r_log = {s: float(gb[f"pred{s}_err_vs_f64"]) for s in range(3)}
     rec = {"224_b2_vs_ref_f64": {"loss_rel": abs(loss16["total_loss"] / l64 - 1),
-                                 "group_norm_rel": {k: abs(my_groups.get(k, 0.0) / v - 1) for k, v in ref_groups.items()
-                                                    if v > 0}}}
-    # (2) config C's resolution: bf16 vs fp32 HIP on the same batch
+                                 "ref_bf16_loss_rel": abs(float(gb["total_loss"]) / l64 - 1),
+                                 "group_norm_rel": e_groups, "ref_bf16_group_norm_rel": r_groups,
+                                 "logits_rel_l2": e_log, "ref_bf16_logits_rel_l2": r_log}}
+    r1 = rec["224_b2_vs_ref_f64"]
+    r1["groups"] = _anchor_check(e_groups, r_groups, "224 groups")
+    # (2) config C's resolution: bf16 vs fp32 HIP on the same batch, against the reference's own
+    gr = golden("train_base_640_b2_ref")
     loss32, p32, n32, fin32 = _base_train_step(gpu_device, "fp32", 2, 640, 7, 11)
     loss16b, p16b, n16b, fin16b = _base_train_step(gpu_device, "bf16", 2, 640, 7, 11)
     assert fin32 and fin16b
     g32, g16 = _group_norms(n32.items()), _group_norms(n16b.items())
+    rf32 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_f32"]) if v >= 0])
+    rf16 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_bf16"]) if v >= 0])
+    e2 = {k: abs(g16.get(k, 0.0) / v - 1) for k, v in g32.items() if v > 0}
+    r2g = {k: abs(rf16[k] / v - 1) for k, v in rf32.items() if v > 0}
     rec["640_b2_bf16_vs_fp32"] = {
         "loss_rel": {k: abs(loss16b[k] / loss32[k] - 1) for k in loss32 if abs(loss32[k]) > 1e-6},
-        "group_norm_rel": {k: abs(g16.get(k, 0.0) / v - 1) for k, v in g32.items() if v > 0},
-        "logits_rel_l2": {k: float(np.linalg.norm(p16b[k] - p32[k]) / np.linalg.norm(p32[k])) for k in p32}}
+        "ref_bf16_loss_rel": abs(float(gr["total_loss_bf16"]) / float(gr["total_loss_f32"]) - 1),
+        "group_norm_rel": e2, "ref_bf16_group_norm_rel": r2g,
+        "logits_rel_l2": {k: float(np.linalg.norm(p16b[k] - p32[k]) / np.linalg.norm(p32[k])) for k in p32},
+        "ref_bf16_logits_rel_l2": [float(v) for v in gr["logits_rel_l2_bf16_vs_f32"]]}
+    r2 = rec["640_b2_bf16_vs_fp32"]
+    r2["groups"] = _anchor_check(e2, r2g, "640 groups")
     record_parity("train_bf16_base", rec)
-    r1, r2 = rec["224_b2_vs_ref_f64"], rec["640_b2_bf16_vs_fp32"]
-    assert r1["loss_rel"] < 0.05, r1
-    assert max(r1["group_norm_rel"].values()) < 0.45, r1
-    assert r2["loss_rel"]["total_loss"] < 0.015, r2
-    assert max(r2["group_norm_rel"].values()) < 0.45, r2
+    assert r1["loss_rel"] <= 3.0 * r1["ref_bf16_loss_rel"], r1
+    for s in range(3):
+        assert e_log[s] <= 1.25 * r_log[s], (s, e_log, r_log)
+    assert r2["loss_rel"]["total_loss"] <= 3.0 * r2["ref_bf16_loss_rel"], r2
+    for s in range(3):
+        assert r2["logits_rel_l2"][f"scale_{s}"] <= 1.25 * r2["ref_bf16_logits_rel_l2"][s], r2
     assert set(g16) == set(g32)
+
+
+def test_large_1024_train_step_bf16_vs_fp32(gpu_device):
+    """Config D's training leg at its per-GPU shape (1024x1024, B=8 -- bench.py's `large`
+    training line): the bf16 step against the fp32 HIP step on the same batch.  No reference
+    run exists at this size (the CPU reference needs ~1 h per precision), so the anchors are the
+    reference's own bf16-vs-fp32 errors at config C's 640 B=2 (fixture train_base_640_b2_ref,
+    S8): total loss within 3x, per-group gradient norms within 3x (mean 2x); every gradient
+    finite; the loss components all present and positive."""
+    from conftest import golden, record_parity
+    import json
+    import os
+    from conftest import GOLDEN
+    names = json.load(open(os.path.join(GOLDEN, "train_base_param_names.json")))
+    gr = golden("train_base_640_b2_ref")
+    loss32, _, n32, fin32 = _base_train_step(gpu_device, "fp32", 8, 1024, 5, 13)
+    loss16, _, n16, fin16 = _base_train_step(gpu_device, "bf16", 8, 1024, 5, 13)
+    assert fin32 and fin16
+    g32, g16 = _group_norms(n32.items()), _group_norms(n16.items())
+    rf32 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_f32"]) if v >= 0])
+    rf16 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_bf16"]) if v >= 0])
+    e = {k: abs(g16.get(k, 0.0) / v - 1) for k, v in g32.items() if v > 0}
+    r = {k: abs(rf16[k] / v - 1) for k, v in rf32.items() if v > 0}
+    rec = {"config": "base 1024x1024 B=8 train step, bf16 vs fp32 HIP",
+           "loss_bf16": loss16, "loss_fp32": loss32,
+           "loss_rel": abs(loss16["total_loss"] / loss32["total_loss"] - 1),
+           "ref640_bf16_loss_rel": abs(float(gr["total_loss_bf16"]) / float(gr["total_loss_f32"]) - 1),
+           "group_norm_rel": e, "ref640_bf16_group_norm_rel": r}
+    rec["groups"] = _anchor_check(e, r, "1024 groups")
+    record_parity("train_bf16_large_1024", rec)
+    for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss", "total_loss"):
+        assert loss16[k] > 0 and np.isfinite(loss16[k]), (k, loss16)
+    assert rec["loss_rel"] <= 3.0 * rec["ref640_bf16_loss_rel"], rec
 
 
 def test_tiny_train_step_bf16_runs_and_agrees(gpu_device):

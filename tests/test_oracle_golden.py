@@ -262,3 +262,44 @@ def test_stability_monitor_oracle_matches_reference(D, fam):
     np.testing.assert_allclose(float(g["history0"]), float(g["signal_ratio"]), rtol=1e-6)
     for k in ("row_sum_error", "col_sum_error"):
         np.testing.assert_allclose(float(r[k]), float(g[k]), rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e", [c for c in cases.MHC_CASES if c[0] <= 512])
+def test_autocast_emulation_reproduces_reference_bf16(fam, D, e):
+    """S8 (oracle/autocast_emu.py): the oracle's mHC restatement run under the emulated CUDA
+    autocast bf16 policy reproduces the reference's own bf16 output (fixture *_bf16ref, written
+    by the reference's ManifoldHyperConnection under the same policy) -- the bf16 anchors the GPU
+    tests multiply are the reference's numerics, not an artefact of where the casts sit -- and the
+    recorded error anchor is what that output's distance from fp64 is."""
+    from oracle.autocast_emu import CudaAutocastBF16
+    g = golden(f"mhc_{fam}_D{D}_e{e}")
+    gb = golden(f"mhc_{fam}_D{D}_e{e}_bf16ref")
+    sd = _mhc_sd(D, e, fam)
+    x = cases.mhc_input(D, e)
+    with torch.no_grad(), CudaAutocastBF16() as mode:
+        y = O.mhc(sd, "", x, 20).float()
+    assert mode.counts["lower"] >= 4 and mode.counts["fp32"] >= 2
+    ref = torch.from_numpy(gb["y"])
+    assert float((y - ref).norm() / ref.norm()) < 2e-2
+    y64 = torch.from_numpy(g["y64"]).double()
+    err = float((ref.double() - y64).norm() / y64.norm())
+    np.testing.assert_allclose(err, float(gb["err_vs_f64"]), rtol=1e-6)
+
+
+def test_autocast_emulation_policy():
+    """The emulated CUDA autocast bf16 policy: GEMM-class ops compute in bf16, LayerNorm /
+    softmax / reductions in fp32, the rest keeps its input dtype; autograd sees the casts."""
+    from oracle.autocast_emu import CudaAutocastBF16
+    lin = torch.nn.Linear(8, 8)
+    x = torch.randn(4, 8, requires_grad=True)
+    with CudaAutocastBF16():
+        h = lin(x)
+        z = torch.nn.functional.layer_norm(h, (8,))
+        s = torch.softmax(h, -1)
+        a = torch.nn.functional.gelu(h)
+        loss = (z.sum() + s.sum() + a.float().sum())
+    assert h.dtype == torch.bfloat16 and a.dtype == torch.bfloat16
+    assert z.dtype == torch.float32 and s.dtype == torch.float32
+    loss.backward()
+    assert x.grad.dtype == torch.float32 and lin.weight.grad.dtype == torch.float32
