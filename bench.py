@@ -60,6 +60,8 @@ def parse():
                          "default: on (every N)")
     ap.add_argument("--no-train", dest="train", action="store_false")
     ap.add_argument("--train-batch", type=int, default=16)
+    ap.add_argument("--train-eager", dest="train_graph", action="store_false",
+                    help="host-launched training steps instead of the captured step graph")
     ap.add_argument("--train-steps", type=int, default=4)
     ap.add_argument("--no-stream", dest="stream", action="store_false",
                     help="skip the paced 30-FPS streaming leg (config E)")
@@ -197,7 +199,9 @@ def train_bench(a, dev, world, rank, size, batch, steps, gflop_step_img):
     from hv_amd.trainer import HVTrainer
     torch.manual_seed(0)
     model = HybridVisionSystem({"image_size": size, "precision": a.precision, "verbose": False}).to(dev).train()
-    tr = HVTrainer(model)
+    # single GPU: the whole step is one hipGraph replay (HVTrainer graph mode); DDP: eager steps
+    # with the bucketed all-reduces overlapping the backward
+    tr = HVTrainer(model, graph=a.train_graph)
     x = torch.randn(batch, 3, size, size, device=dev)
     tg = [t.to(dev) for t in synthetic_targets(batch, size, seed=1000 + rank)]
     for _ in range(2):
@@ -213,6 +217,7 @@ def train_bench(a, dev, world, rank, size, batch, steps, gflop_step_img):
            "ms_per_step": round(el / steps * 1e3, 2), "per_gpu_batch": batch, "steps": steps, "n_gpus": world,
            "workload": f"hybrid_vision base {size}x{size} training, bf16 activations, fp32 params, "
                        f"{'DDP over RCCL (bucketed all-reduce overlapped with backward)' if world > 1 else 'single GPU'}",
+           "step_mode": "hipGraph replay of the whole step" if tr.replays else "eager",
            "loss": round(box["loss"]["total_loss"].item(), 3),
            "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}
     if gflop_step_img:

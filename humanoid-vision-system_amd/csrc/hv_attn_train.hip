@@ -27,7 +27,8 @@ __device__ __forceinline__ float dot_row(const float* a, const T* row) {
 // forward: wave per (b, h, i)
 template <typename T, int HD>
 __global__ void __launch_bounds__(256) k_attn_fwd(const T* q, const T* k, const T* v, T* o, float* lse, int n, int L,
-                                                  int H, int hd, float scale, float p, uint32_t seed) {
+                                                  int H, int hd, float scale, float p, uint32_t seed, const unsigned int* soff) {
+  seed = hv_seed(seed, soff);
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)n * H * L) return;
@@ -66,7 +67,8 @@ __global__ void __launch_bounds__(256) k_attn_fwd(const T* q, const T* k, const 
 template <typename T, int HD>
 __global__ void __launch_bounds__(256) k_attn_bwd_q(const T* q, const T* k, const T* v, const T* o, const T* dout,
                                                     const float* lse, int n, int L, int H, int hd, float scale, float p,
-                                                    uint32_t seed, T* dq, float* Drow) {
+                                                    uint32_t seed, const unsigned int* soff, T* dq, float* Drow) {
+  seed = hv_seed(seed, soff);
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)n * H * L) return;
@@ -104,7 +106,8 @@ __global__ void __launch_bounds__(256) k_attn_bwd_q(const T* q, const T* k, cons
 template <typename T, int HD>
 __global__ void __launch_bounds__(256) k_attn_bwd_kv(const T* q, const T* k, const T* v, const T* dout,
                                                      const float* lse, const float* Drow, int n, int L, int H, int hd,
-                                                     float scale, float p, uint32_t seed, T* dk, T* dv) {
+                                                     float scale, float p, uint32_t seed, const unsigned int* soff, T* dk, T* dv) {
+  seed = hv_seed(seed, soff);
   const long krow = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (krow >= (long)n * H * L) return;
@@ -188,7 +191,8 @@ __global__ void __launch_bounds__(256) k_attn_fwd_mfma(const unsigned short* __r
                                                        const unsigned short* __restrict__ k,
                                                        const unsigned short* __restrict__ vt,
                                                        unsigned short* __restrict__ out, float* __restrict__ lse,
-                                                       int L, int Lp, int heads, float sl2, float p, uint32_t seed) {
+                                                       int L, int Lp, int heads, float sl2, float p, uint32_t seed, const unsigned int* soff) {
+  seed = hv_seed(seed, soff);
   const int b = blockIdx.z, h = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int D = heads * 32;
@@ -279,8 +283,9 @@ __global__ void __launch_bounds__(256) k_attn_bwd_kv_mfma(const unsigned short* 
                                                           const unsigned short* __restrict__ dot,
                                                           const unsigned short* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          int L, int Lp, int heads, float scale, float p, uint32_t seed,
+                                                          int L, int Lp, int heads, float scale, float p, uint32_t seed, const unsigned int* soff,
                                                           unsigned short* __restrict__ dk, unsigned short* __restrict__ dv) {
+  seed = hv_seed(seed, soff);
   const int b = blockIdx.z, h = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int D = heads * 32;
@@ -347,8 +352,9 @@ __global__ void __launch_bounds__(256) k_attn_bwd_q_mfma(const unsigned short* _
                                                          const unsigned short* __restrict__ kt,
                                                          const unsigned short* __restrict__ dout,
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                         int L, int Lp, int heads, float scale, float p, uint32_t seed,
+                                                         int L, int Lp, int heads, float scale, float p, uint32_t seed, const unsigned int* soff,
                                                          unsigned short* __restrict__ dq) {
+  seed = hv_seed(seed, soff);
   const int b = blockIdx.z, h = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fr = lane & 15, fg = lane >> 4;
   const int D = heads * 32;
@@ -407,7 +413,8 @@ extern "C" size_t hv_attention_train_mfma_work_elems(int n, int L, int heads) {
 }
 
 extern "C" int hv_attention_train_mfma(const void* q, const void* k, const void* v, void* o, float* lse, int n, int L,
-                                       int heads, float sm_scale, float drop_p, unsigned int seed, void* vt_work,
+                                       int heads, float sm_scale, float drop_p, unsigned int seed,
+                                       const unsigned int* seed_offset, void* vt_work,
                                        hv_stream_t stream) {
   if (!q || !k || !v || !o || !lse || !vt_work || n <= 0 || L <= 0 || heads <= 0) return HV_EINVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o | (uintptr_t)vt_work) & 15) return HV_EUNSUPPORTED;
@@ -418,7 +425,7 @@ extern "C" int hv_attention_train_mfma(const void* q, const void* k, const void*
                                                                 (unsigned short*)vt_work);
   k_attn_fwd_mfma<<<dim3(hv_cdiv(L, 64), heads, n), 256, 0, s>>>(
       (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)vt_work, (unsigned short*)o, lse, L, Lp,
-      heads, sm_scale * 1.4426950408889634f, drop_p, seed);
+      heads, sm_scale * 1.4426950408889634f, drop_p, seed, seed_offset);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -427,8 +434,8 @@ extern "C" int hv_attention_train_mfma(const void* q, const void* k, const void*
    floats (Delta) */
 extern "C" int hv_attention_backward_mfma(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                           const float* lse, int n, int L, int heads, float sm_scale, float drop_p,
-                                          unsigned int seed, void* dq, void* dk, void* dv, void* work,
-                                          hv_stream_t stream) {
+                                          unsigned int seed, const unsigned int* seed_offset, void* dq, void* dk,
+                                          void* dv, void* work, hv_stream_t stream) {
   if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv || !work || n <= 0 || L <= 0) return HV_EINVAL;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o | (uintptr_t)dout | (uintptr_t)work | (uintptr_t)dq |
        (uintptr_t)dk | (uintptr_t)dv) & 15)
@@ -450,39 +457,39 @@ extern "C" int hv_attention_backward_mfma(const void* q, const void* k, const vo
   const dim3 g(hv_cdiv(L, 64), heads, n);
   k_attn_bwd_kv_mfma<<<g, 256, 0, s>>>((const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, qt,
                                        dot, (const unsigned short*)dout, lse, delta, L, Lp, heads, sm_scale, drop_p,
-                                       seed, (unsigned short*)dk, (unsigned short*)dv);
+                                       seed, seed_offset, (unsigned short*)dk, (unsigned short*)dv);
   k_attn_bwd_q_mfma<<<g, 256, 0, s>>>((const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, kt,
                                       (const unsigned short*)dout, lse, delta, L, Lp, heads, sm_scale, drop_p, seed,
-                                      (unsigned short*)dq);
+                                      seed_offset, (unsigned short*)dq);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
 extern "C" int hv_attention_train(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int n,
                                   int L, int heads, int hd, float sm_scale, float drop_p, unsigned int seed,
-                                  hv_stream_t stream) {
+                                  const unsigned int* seed_offset, hv_stream_t stream) {
   if (!q || !k || !v || !o || !lse || hd != 32) return HV_EINVAL;
   const unsigned grid = hv_cdiv((long)n * heads * L, 4);
   HV_DISPATCH(dtype, (k_attn_fwd<T, 32><<<grid, 256, 0, (hipStream_t)stream>>>((const T*)q, (const T*)k, (const T*)v,
                                                                            (T*)o, lse, n, L, heads, hd, sm_scale,
-                                                                           drop_p, seed)));
+                                                                           drop_p, seed, seed_offset)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
 extern "C" int hv_attention_backward(int dtype, const void* q, const void* k, const void* v, const void* o,
                                      const void* dout, const float* lse, int n, int L, int heads, int hd,
-                                     float sm_scale, float drop_p, unsigned int seed, void* dq, void* dk, void* dv,
-                                     float* work, hv_stream_t stream) {
+                                     float sm_scale, float drop_p, unsigned int seed, const unsigned int* seed_offset,
+                                     void* dq, void* dk, void* dv, float* work, hv_stream_t stream) {
   if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv || !work || hd != 32) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = hv_cdiv((long)n * heads * L, 4);
   HV_DISPATCH(dtype, (k_attn_bwd_q<T, 32><<<grid, 256, 0, s>>>((const T*)q, (const T*)k, (const T*)v, (const T*)o,
                                                            (const T*)dout, lse, n, L, heads, hd, sm_scale, drop_p,
-                                                           seed, (T*)dq, work)));
+                                                           seed, seed_offset, (T*)dq, work)));
   HV_DISPATCH(dtype, (k_attn_bwd_kv<T, 32><<<grid, 256, 0, s>>>((const T*)q, (const T*)k, (const T*)v, (const T*)dout,
                                                             lse, work, n, L, heads, hd, sm_scale, drop_p, seed,
-                                                            (T*)dk, (T*)dv)));
+                                                            seed_offset, (T*)dk, (T*)dv)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

@@ -98,6 +98,10 @@ __device__ __forceinline__ float hv_drop_scale(uint32_t seed, unsigned long long
   return u >= p ? 1.0f / (1.0f - p) : 0.f;
 }
 
+// effective dropout seed of a call: its seed argument plus the optional device offset word
+// (hv_kernels.h seed_offset; a captured training graph advances it on every replay)
+__device__ __forceinline__ uint32_t hv_seed(uint32_t seed, const unsigned int* off) { return off ? seed + *off : seed; }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -16,6 +16,11 @@
 // Training epilogue modes (hv_gemm_desc.epi_mode 1/2, see hv_kernels.h).  A lane holds 4
 // consecutive columns: the pre-activation is stored / loaded as one 8-byte (bf16) or 16-byte
 // (fp32) vector when the row allows it.
+// dropout seed of a training epilogue (hv_gemm_desc.drop_seed + *seed_offset), loaded once
+__device__ __forceinline__ uint32_t epi_seed(const hv_gemm_desc& d) {
+  return d.drop_p > 0.f ? hv_seed(d.drop_seed, d.seed_offset) : 0u;
+}
+
 __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 acc, int row, int col, const f32x4 sc,
                                            const f32x4 bi, const f32x4 cs, float mean, float rstd, bool ln_epi) {
   f32x4 v;
@@ -53,8 +58,9 @@ __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 ac
         }
       }
     }
+    const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
+    for (int j = 0; j < 4; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
   } else {
     if (vec) {
       if (aux_bf) {
@@ -71,9 +77,10 @@ __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 ac
         z[j] = col + j < d.N ? (aux_bf ? bf2f(((const unsigned short*)d.aux)[ai + j]) : ((const float*)d.aux)[ai + j])
                              : 0.f;
     }
+    const uint32_t sd_ = epi_seed(d);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      v[j] = acc[j] * d.alpha * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+      v[j] = acc[j] * d.alpha * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
   }
   return v;
 }
@@ -324,8 +331,9 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
         }
       }
     }
+    const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p);
+    for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
   } else {
     if (av && aux_bf) {
       const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
@@ -345,8 +353,9 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
         z[j] = col + j < d.N ? (aux_bf ? bf2f(((const unsigned short*)d.aux)[ai + j]) : ((const float*)d.aux)[ai + j])
                              : 0.f;
     }
+    const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(d.drop_seed, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
   }
 }
 

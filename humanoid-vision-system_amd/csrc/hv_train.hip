@@ -120,6 +120,7 @@ struct ColRed {
   int act;
   float p;
   uint32_t seed;
+  const unsigned int* soff;   // device seed offset (hv_kernels.h), may be NULL
 };
 
 template <typename T> __device__ __forceinline__ void ld4(const T* p, long i, float (&v)[4]);
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(256) k_colred(const ColRed r, int nblk, float*
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float xh = (a[j] - rmu) * rrs;
-            const float g = b[j] * hv_drop_scale(r.seed, (unsigned long long)(o + j), r.p);
+            const float g = b[j] * hv_drop_scale(hv_seed(r.seed, r.soff), (unsigned long long)(o + j), r.p);
             acc[0][c][j] += g * xh;
             acc[1][c][j] += g;
           }
@@ -378,8 +379,9 @@ __device__ __forceinline__ float group_sum(float v) {
 template <typename TX, typename TY, int G, int NP>
 __global__ void __launch_bounds__(256) k_rownorm_train(int mode, const TX* __restrict__ x, int rows, int cols,
                                                        float eps, const float* g, const float* b, float p,
-                                                       uint32_t seed, TY* y, const TY* res, float* mean,
-                                                       float* rstd) {
+                                                       uint32_t seed, const unsigned int* soff, TY* y,
+                                                       const TY* res, float* mean, float* rstd) {
+  seed = hv_seed(seed, soff);
   constexpr int RPW = 64 / G;
   const int lane = threadIdx.x & 63, gl = lane % G;
   const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
@@ -430,8 +432,9 @@ __global__ void __launch_bounds__(256) k_rownorm_train(int mode, const TX* __res
 template <typename TX, typename TD, typename TO, int G, int NP>
 __global__ void __launch_bounds__(256) k_rownorm_bwd(int mode, const TX* __restrict__ x, const TD* __restrict__ dy,
                                                      int rows, int cols, const float* mean, const float* rstd,
-                                                     const float* g, float p, uint32_t seed, TO* dx,
-                                                     const TO* dx_add) {
+                                                     const float* g, float p, uint32_t seed,
+                                                     const unsigned int* soff, TO* dx, const TO* dx_add) {
+  seed = hv_seed(seed, soff);
   constexpr int RPW = 64 / G;
   const int lane = threadIdx.x & 63, gl = lane % G;
   const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
@@ -486,12 +489,13 @@ inline void rown_shape(int cols, int* G, int* NP) {
 
 template <typename TX, typename TY>
 int rown_train_launch(int mode, const void* x, int rows, int cols, float eps, const float* gamma, const float* beta,
-                      float p, uint32_t seed, void* y, const void* res, float* mean, float* rstd, hipStream_t s) {
+                      float p, uint32_t seed, const unsigned int* soff, void* y, const void* res, float* mean,
+                      float* rstd, hipStream_t s) {
   int G, NP;
   rown_shape(cols, &G, &NP);
   const unsigned grid = hv_cdiv(rows, 4 * (64 / G));
 #define RT(GG, PP) k_rownorm_train<TX, TY, GG, PP><<<grid, 256, 0, s>>>(mode, (const TX*)x, rows, cols, eps, gamma, \
-      beta, p, seed, (TY*)y, (const TY*)res, mean, rstd)
+      beta, p, seed, soff, (TY*)y, (const TY*)res, mean, rstd)
   if (G == 8) RT(8, 1);
   else if (G == 16) RT(16, 1);
   else if (G == 32) RT(32, 1);
@@ -507,12 +511,13 @@ int rown_train_launch(int mode, const void* x, int rows, int cols, float eps, co
 
 template <typename TX, typename TD, typename TO>
 int rown_bwd_launch(int mode, const void* x, const void* dy, int rows, int cols, const float* mean, const float* rstd,
-                    const float* gamma, float p, uint32_t seed, void* dx, const void* dx_add, hipStream_t s) {
+                    const float* gamma, float p, uint32_t seed, const unsigned int* soff, void* dx,
+                    const void* dx_add, hipStream_t s) {
   int G, NP;
   rown_shape(cols, &G, &NP);
   const unsigned grid = hv_cdiv(rows, 4 * (64 / G));
 #define RBK(GG, PP) k_rownorm_bwd<TX, TD, TO, GG, PP><<<grid, 256, 0, s>>>(mode, (const TX*)x, (const TD*)dy, rows, \
-      cols, mean, rstd, gamma, p, seed, (TO*)dx, (const TO*)dx_add)
+      cols, mean, rstd, gamma, p, seed, soff, (TO*)dx, (const TO*)dx_add)
   if (G == 8) RBK(8, 1);
   else if (G == 16) RBK(16, 1);
   else if (G == 32) RBK(32, 1);
@@ -529,13 +534,15 @@ int rown_bwd_launch(int mode, const void* x, const void* dy, int rows, int cols,
 // ------------------------------------------------------------------ elementwise
 template <typename T>
 __global__ void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ pre, long n, int act, float p,
-                          uint32_t seed, T* dpre) {
+                          uint32_t seed, const unsigned int* soff, T* dpre) {
+  seed = hv_seed(seed, soff);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     st<T>(dpre, i, ld<T>(dy, i) * hv_drop_scale(seed, (unsigned long long)i, p) * hv_act_grad(ld<T>(pre, i), act));
 }
 
 template <typename T>
-__global__ void k_dropout(const T* __restrict__ x, long n, float p, uint32_t seed, T* y) {
+__global__ void k_dropout(const T* __restrict__ x, long n, float p, uint32_t seed, const unsigned int* soff, T* y) {
+  seed = hv_seed(seed, soff);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     st<T>(y, i, ld<T>(x, i) * hv_drop_scale(seed, (unsigned long long)i, p));
 }
@@ -796,13 +803,13 @@ __device__ __forceinline__ int find_param(const hv_param_entry* t, int count, in
   return lo;
 }
 
-__global__ void __launch_bounds__(256) k_grad_sq(const hv_param_entry* tab, int count, float* part) {
+__global__ void __launch_bounds__(256) k_grad_sq(const hv_param_entry* tab, int count, const int* active, float* part) {
   __shared__ float scratch[16];
   const int ei = find_param(tab, count, blockIdx.x);
   const hv_param_entry e = tab[ei];
   const long b0 = (long)(blockIdx.x - e.blk) * PB_ELEMS;
   float s = 0.f;
-  if (e.grad) {
+  if (e.grad && (!active || active[ei])) {
     for (long i = b0 + threadIdx.x; i < min(e.n, b0 + PB_ELEMS); i += 256) {
       const float g = e.grad[i];
       s += g * g;
@@ -843,10 +850,10 @@ __global__ void __launch_bounds__(256) k_grad_norm_final(int nblk, const float* 
 
 __global__ void __launch_bounds__(256) k_adamw(const hv_param_entry* tab, int count, const float* coefs, float lr,
                                                float b1, float b2, float eps, float wd, float bc1, float bc2s,
-                                               const int* __restrict__ steps) {
+                                               const int* __restrict__ steps, const int* __restrict__ active) {
   const int ei = find_param(tab, count, blockIdx.x);
   const hv_param_entry e = tab[ei];
-  if (!e.grad) return;
+  if (!e.grad || (active && !active[ei])) return;     // no gradient this step: no decay, no update
   if (steps) {                                  // per-parameter bias correction (torch state['step'])
     const float t = (float)max(steps[ei], 1);
     bc1 = 1.f - powf(b1, t);
@@ -1015,21 +1022,22 @@ extern "C" int hv_bn_backward(int dtype, const void* x, const void* dy, int rows
 }
 
 extern "C" int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, int cols, float eps,
-                                const float* gamma, const float* beta, float drop_p, unsigned int seed, int y_dtype,
-                                void* y, const void* residual, float* mean, float* rstd, hv_stream_t stream) {
+                                const float* gamma, const float* beta, float drop_p, unsigned int seed,
+                                const unsigned int* seed_offset, int y_dtype, void* y, const void* residual,
+                                float* mean, float* rstd, hv_stream_t stream) {
   if (!x || !y || !rstd || rows <= 0 || cols <= 0 || cols % 4 || cols > 64 * RQ || (mode == 0 && !mean))
     return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (x_dtype == HV_F32 && y_dtype == HV_F32)
-    return rown_train_launch<float, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual, mean, rstd, s);
+    return rown_train_launch<float, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, seed_offset, y, residual, mean, rstd, s);
   if (x_dtype == HV_F32 && y_dtype == HV_BF16)
-    return rown_train_launch<float, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual,
+    return rown_train_launch<float, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, seed_offset, y, residual,
                                                     mean, rstd, s);
   if (x_dtype == HV_BF16 && y_dtype == HV_BF16)
-    return rown_train_launch<unsigned short, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y,
+    return rown_train_launch<unsigned short, unsigned short>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, seed_offset, y,
                                                              residual, mean, rstd, s);
   if (x_dtype == HV_BF16 && y_dtype == HV_F32)
-    return rown_train_launch<unsigned short, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, y, residual,
+    return rown_train_launch<unsigned short, float>(mode, x, rows, cols, eps, gamma, beta, drop_p, seed, seed_offset, y, residual,
                                                     mean, rstd, s);
   return HV_EINVAL;
 }
@@ -1040,8 +1048,8 @@ extern "C" size_t hv_rownorm_work_floats(int rows, int cols) {
 
 extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, const void* dy, int rows,
                                    int cols, const float* mean, const float* rstd, const float* gamma, float drop_p,
-                                   unsigned int seed, int dx_dtype, void* dx, const void* dx_add, float* dgamma,
-                                   float* dbeta, float* work, hv_stream_t stream) {
+                                   unsigned int seed, const unsigned int* seed_offset, int dx_dtype, void* dx,
+                                   const void* dx_add, float* dgamma, float* dbeta, float* work, hv_stream_t stream) {
   if (!x || !dy || !dx || !rstd || rows <= 0 || cols <= 0 || cols > 64 * RQ || (mode == 0 && !mean))
     return HV_EINVAL;
   const bool params = dgamma || dbeta;
@@ -1051,7 +1059,7 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
   const int key = x_dtype * 4 + dy_dtype * 2 + dx_dtype;
   int rc;
 #define RB_LAUNCH(TX, TD, TO) rc = rown_bwd_launch<TX, TD, TO>(mode, x, dy, rows, cols, mean, rstd, gamma, drop_p, seed, \
-      dx, dx_add, s)
+      seed_offset, dx, dx_add, s)
   switch (key) {
     case 0: RB_LAUNCH(float, float, float); break;
     case 1: RB_LAUNCH(float, float, unsigned short); break;
@@ -1069,7 +1077,7 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
     float* sums = work + colred_work(rows, cols, 1, 2);   // [sum g xhat | sum g]
     ColRed r{};
     r.a = x; r.b = dy; r.rows = rows; r.cols = cols;
-    r.mean = mode == 0 ? mean : nullptr; r.rstd = rstd; r.p = drop_p; r.seed = seed;
+    r.mean = mode == 0 ? mean : nullptr; r.rstd = rstd; r.p = drop_p; r.seed = seed; r.soff = seed_offset;
     int rc;
     if (x_dtype == HV_F32 && dy_dtype == HV_F32) rc = colred_run<float, float, CR_ROWN>(r, 1, work, sums, 0, s);
     else if (x_dtype == HV_F32) rc = colred_run<float, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
@@ -1083,18 +1091,19 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
 }
 
 extern "C" int hv_act_backward(int dtype, const void* dy, const void* pre, long n, int act, float drop_p,
-                               unsigned int seed, void* dpre, hv_stream_t stream) {
+                               unsigned int seed, const unsigned int* seed_offset, void* dpre, hv_stream_t stream) {
   if (!dy || !pre || !dpre || n <= 0) return HV_EINVAL;
   HV_DISPATCH(dtype, (k_act_bwd<T><<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const T*)dy, (const T*)pre, n, act,
-                                                                                 drop_p, seed, (T*)dpre)));
+                                                                                 drop_p, seed, seed_offset,
+                                                                                 (T*)dpre)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
-extern "C" int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed, void* y,
-                          hv_stream_t stream) {
+extern "C" int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed,
+                          const unsigned int* seed_offset, void* y, hv_stream_t stream) {
   if (!x || !y || n <= 0) return HV_EINVAL;
-  HV_DISPATCH(dtype, (k_dropout<T><<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const T*)x, n, drop_p, seed, (T*)y)));
+  HV_DISPATCH(dtype, (k_dropout<T><<<grid_for(n), 256, 0, (hipStream_t)stream>>>((const T*)x, n, drop_p, seed, seed_offset, (T*)y)));
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -1207,11 +1216,12 @@ extern "C" int hv_yolo_loss(int dtype, const void* logits, const float* targets,
 extern "C" int hv_param_blocks(long n) { return (int)((n + PB_ELEMS - 1) / PB_ELEMS); }
 
 extern "C" int hv_grad_norms(const hv_param_entry* tab, int count, int total_blocks, int groups,
-                             const float* max_norm, float* norms, float* coefs, float* work, hv_stream_t stream) {
+                             const float* max_norm, float* norms, float* coefs, float* work, const int* active,
+                             hv_stream_t stream) {
   if (!tab || count <= 0 || total_blocks <= 0 || groups < 1 || groups > 4 || !max_norm || !norms || !coefs || !work)
     return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  k_grad_sq<<<total_blocks, 256, 0, s>>>(tab, count, work);
+  k_grad_sq<<<total_blocks, 256, 0, s>>>(tab, count, active, work);
   float m[4] = {1.f, 1.f, 1.f, 1.f};
   for (int g = 0; g < groups; ++g) m[g] = max_norm[g];
   k_grad_norm_final<<<1, 256, 0, s>>>(total_blocks, work, groups, m[0], m[1], m[2], m[3], norms, coefs);
@@ -1221,12 +1231,12 @@ extern "C" int hv_grad_norms(const hv_param_entry* tab, int count, int total_blo
 
 extern "C" int hv_adamw(const hv_param_entry* tab, int count, int total_blocks, const float* coefs, float lr,
                         float beta1, float beta2, float eps, float weight_decay, int step, const int* steps,
-                        hv_stream_t stream) {
+                        const int* active, hv_stream_t stream) {
   if (!tab || count <= 0 || total_blocks <= 0 || (step < 1 && !steps)) return HV_EINVAL;
   const float bc1 = 1.f - powf(beta1, (float)max(step, 1));
   const float bc2s = sqrtf(1.f - powf(beta2, (float)max(step, 1)));
   k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, lr, beta1, beta2, eps, weight_decay, bc1,
-                                                         bc2s, steps);
+                                                         bc2s, steps, active);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

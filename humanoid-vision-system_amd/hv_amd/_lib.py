@@ -79,7 +79,8 @@ class GemmDesc(C.Structure):
                 ("conv_oh", i32), ("conv_ow", i32), ("b_colsum", vp),
                 ("aux", vp), ("ld_aux", i64), ("aux_dtype", i32), ("epi_mode", i32),
                 ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("variant", i32),
-                ("splitk_work", vp), ("splitk_count", vp), ("splitk", i32), ("pad2_", i32)]
+                ("splitk_work", vp), ("splitk_count", vp), ("splitk", i32), ("pad2_", i32),
+                ("seed_offset", vp)]
 
 
 class CopySegment(C.Structure):
@@ -200,14 +201,14 @@ _SIGS = {
     "hv_bn_stats": ([i32, vp, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp], i32),
     "hv_bn_apply": ([i32, vp, i32, i32, vp, vp, vp, vp, i32, vp, vp], i32),
     "hv_bn_backward": ([i32, vp, vp, i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp], i32),
-    "hv_rownorm_train": ([i32, i32, vp, i32, i32, f32, vp, vp, f32, C.c_uint, i32, vp, vp, vp, vp, vp], i32),
+    "hv_rownorm_train": ([i32, i32, vp, i32, i32, f32, vp, vp, f32, C.c_uint, vp, i32, vp, vp, vp, vp, vp], i32),
     "hv_rownorm_work_floats": ([i32, i32], C.c_size_t),
-    "hv_rownorm_backward": ([i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, f32, C.c_uint, i32, vp, vp, vp, vp,
+    "hv_rownorm_backward": ([i32, i32, vp, i32, vp, i32, i32, vp, vp, vp, f32, C.c_uint, vp, i32, vp, vp, vp, vp,
                              vp, vp], i32),
-    "hv_act_backward": ([i32, vp, vp, i64, i32, f32, C.c_uint, vp, vp], i32),
+    "hv_act_backward": ([i32, vp, vp, i64, i32, f32, C.c_uint, vp, vp, vp], i32),
     "hv_mhc_param_backward_work_floats": ([i32, i32], C.c_size_t),
     "hv_mhc_param_backward": ([i32, i32] + [vp] * 14 + [vp], i32),
-    "hv_dropout": ([i32, vp, i64, f32, C.c_uint, vp, vp], i32),
+    "hv_dropout": ([i32, vp, i64, f32, C.c_uint, vp, vp, vp], i32),
     "hv_sinkhorn_bwd_work_floats": ([i32, i32, i32], C.c_size_t),
     "hv_sinkhorn_group_backward": ([vp, i32, i32, i32, i32, i32, vp], i32),
     "hv_chan_dot_work_floats": ([i32, i32, i32], C.c_size_t),
@@ -219,18 +220,19 @@ _SIGS = {
     "hv_vit_assemble": ([i32, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "hv_vit_assemble_backward": ([i32, vp, i32, i32, i32, vp, vp, vp, vp], i32),
     "hv_scatter_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
-    "hv_attention_train": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp], i32),
-    "hv_attention_backward": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp,
+    "hv_attention_train": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp, vp], i32),
+    "hv_attention_backward": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp, vp,
                                vp, vp], i32),
     "hv_attention_train_mfma_work_elems": ([i32, i32, i32], C.c_size_t),
-    "hv_attention_train_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp], i32),
-    "hv_attention_backward_mfma": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp, vp, vp],
+    "hv_attention_train_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp], i32),
+    "hv_attention_backward_mfma": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, C.c_uint, vp, vp, vp, vp, vp,
+                                    vp],
                                    i32),
     "hv_yolo_loss_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_yolo_loss": ([i32, vp, vp, i32, i32, i32, i32, i32, f32, f32, f32, f32, vp, i32, vp, vp, vp], i32),
     "hv_param_blocks": ([i64], i32),
-    "hv_grad_norms": ([vp, i32, i32, i32, vp, vp, vp, vp, vp], i32),
-    "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp, vp], i32),
+    "hv_grad_norms": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),
+    "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp, vp, vp], i32),
 }
 
 EXPORTED = tuple(_SIGS)

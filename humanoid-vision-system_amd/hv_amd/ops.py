@@ -25,14 +25,44 @@ def _cuda(*ts):
             raise RuntimeError("hv_amd ops require CUDA(HIP) tensors; there is no CPU path")
 
 
+_KEEPALIVE: list = []     # stack of lists collecting the pinned sources of uploads under capture
+
+
+class capture_keepalive:
+    """While a HIP graph is being captured, a table upload becomes a memcpy NODE that re-reads its
+    pinned host source on every replay: `with capture_keepalive(keep):` collects those sources
+    (and the device tables) into `keep`, which the graph's owner holds as long as the graph."""
+
+    def __init__(self, keep: list):
+        self.keep = keep
+
+    def __enter__(self):
+        _KEEPALIVE.append(self.keep)
+        return self.keep
+
+    def __exit__(self, *exc):
+        _KEEPALIVE.pop()
+        return False
+
+
+def keep_if_capturing(*objs) -> None:
+    """Register host sources of an upload issued while the current stream captures a graph."""
+    if _KEEPALIVE and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        _KEEPALIVE[-1].append(objs)
+
+
 def upload_table(entries, device) -> Tensor:
     """ctypes struct array -> device bytes, asynchronously (pinned staging + non_blocking copy
     on the current stream): a table upload never synchronises the host with the GPU, so it can
-    sit inside a training forward/backward without draining the queue."""
+    sit inside a training forward/backward without draining the queue (or a graph capture:
+    see capture_keepalive)."""
     host = torch.frombuffer(bytearray(bytes(entries)), dtype=torch.uint8)
     if torch.device(device).type == "cuda":
         host = host.pin_memory()
-    return host.to(device, non_blocking=True)
+    dev = host.to(device, non_blocking=True)
+    if torch.device(device).type == "cuda":
+        keep_if_capturing(host, dev)
+    return dev
 
 
 def _contig(t: Tensor, name: str) -> Tensor:

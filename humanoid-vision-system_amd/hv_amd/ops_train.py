@@ -15,7 +15,7 @@ from torch.autograd.graph import increment_version
 from . import _lib as L
 from ._lib import check, dtype_code, ptr, stream_ptr
 from .ops import _contig, _cuda, f32
-from .runtime import options
+from .runtime import options, seed_offset_ptr
 
 Tensor = torch.Tensor
 
@@ -60,6 +60,7 @@ def gemm_train(a: Tensor, b: Tensor, *, mode: int, act: str = "none", aux: Optio
             raise ValueError("gemm_train: aux must be a contiguous [M, N] tensor")
         d.aux, d.ld_aux, d.aux_dtype = aux.data_ptr(), N, dtype_code(aux.dtype)
     d.drop_p, d.drop_seed = float(drop_p), int(seed) & 0xFFFFFFFF
+    d.seed_offset = seed_offset_ptr()
     if residual is not None:
         _contig(residual, "residual")
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), N, dtype_code(residual.dtype)
@@ -255,7 +256,8 @@ def rownorm_train(mode: int, x: Tensor, eps: float, gamma=None, beta=None, drop_
         if residual.dtype != y.dtype:
             raise TypeError("rownorm_train: residual dtype must match the output")
     check(L.lib().hv_rownorm_train(mode, dtype_code(x.dtype), x.data_ptr(), rows, cols, eps, ptr(g), ptr(b),
-                                   float(drop_p), int(seed) & 0xFFFFFFFF, dtype_code(y.dtype), y.data_ptr(),
+                                   float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(), dtype_code(y.dtype),
+                                   y.data_ptr(),
                                    ptr(residual), ptr(mean), rstd.data_ptr(), stream_ptr()), "hv_rownorm_train")
     return y, mean, rstd
 
@@ -280,7 +282,8 @@ def rownorm_backward(mode: int, x: Tensor, dy: Tensor, mean, rstd, gamma=None, d
     g = f32(gamma)
     check(L.lib().hv_rownorm_backward(mode, dtype_code(x.dtype), x.data_ptr(), dtype_code(dy.dtype), dy.data_ptr(),
                                       rows, cols, ptr(mean), rstd.data_ptr(), ptr(g), float(drop_p),
-                                      int(seed) & 0xFFFFFFFF, dtype_code(dx.dtype), dx.data_ptr(), ptr(dx_add),
+                                      int(seed) & 0xFFFFFFFF, seed_offset_ptr(), dtype_code(dx.dtype), dx.data_ptr(),
+                                      ptr(dx_add),
                                       ptr(dg), ptr(db), ptr(work), stream_ptr()), "hv_rownorm_backward")
     return dx, dg, db
 
@@ -292,7 +295,8 @@ def act_backward(dy: Tensor, pre: Tensor, act: str, drop_p: float = 0.0, seed: i
         raise ValueError("act_backward: dy/pre mismatch")
     out = torch.empty_like(dy)
     check(L.lib().hv_act_backward(dtype_code(dy.dtype), dy.data_ptr(), pre.data_ptr(), dy.numel(), L.ACT[act],
-                                  float(drop_p), int(seed) & 0xFFFFFFFF, out.data_ptr(), stream_ptr()),
+                                  float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(), out.data_ptr(),
+                                  stream_ptr()),
           "hv_act_backward")
     return out
 
@@ -301,7 +305,7 @@ def dropout(x: Tensor, p: float, seed: int) -> Tensor:
     _contig(x, "x")
     y = torch.empty_like(x)
     check(L.lib().hv_dropout(dtype_code(x.dtype), x.data_ptr(), x.numel(), float(p), int(seed) & 0xFFFFFFFF,
-                             y.data_ptr(), stream_ptr()), "hv_dropout")
+                             seed_offset_ptr(), y.data_ptr(), stream_ptr()), "hv_dropout")
     return y
 
 
@@ -412,12 +416,14 @@ def attention_train(q: Tensor, k: Tensor, v: Tensor, heads: int, drop_p: float, 
         vt = torch.empty(L.lib().hv_attention_train_mfma_work_elems(n, Lq, heads), device=q.device, dtype=q.dtype)
         check(L.lib().hv_attention_train_mfma(_contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
                                               _contig(v, "v").data_ptr(), o.data_ptr(), lse.data_ptr(), n, Lq, heads,
-                                              hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, vt.data_ptr(),
+                                              hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(),
+                                              vt.data_ptr(),
                                               stream_ptr()), "hv_attention_train_mfma")
         return o, lse
     check(L.lib().hv_attention_train(dtype_code(q.dtype), _contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
                                      _contig(v, "v").data_ptr(), o.data_ptr(), lse.data_ptr(), n, Lq, heads, hd,
-                                     hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, stream_ptr()),
+                                     hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(),
+                                     stream_ptr()),
           "hv_attention_train")
     return o, lse
 
@@ -432,14 +438,16 @@ def attention_backward(q, k, v, o, do, lse, heads: int, drop_p: float, seed: int
         check(L.lib().hv_attention_backward_mfma(_contig(q, "q").data_ptr(), _contig(k, "k").data_ptr(),
                                                  _contig(v, "v").data_ptr(), _contig(o, "o").data_ptr(),
                                                  _contig(do, "dout").data_ptr(), lse.data_ptr(), n, Lq, heads,
-                                                 hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, dq.data_ptr(),
+                                                 hd ** -0.5, float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(),
+                                                 dq.data_ptr(),
                                                  dk.data_ptr(), dv.data_ptr(), work.data_ptr(), stream_ptr()),
               "hv_attention_backward_mfma")
         return dq, dk, dv
     work = _work(n * heads * Lq, q.device)
     check(L.lib().hv_attention_backward(dtype_code(q.dtype), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                                         _contig(do, "dout").data_ptr(), lse.data_ptr(), n, Lq, heads, hd, hd ** -0.5,
-                                        float(drop_p), int(seed) & 0xFFFFFFFF, dq.data_ptr(), dk.data_ptr(),
+                                        float(drop_p), int(seed) & 0xFFFFFFFF, seed_offset_ptr(), dq.data_ptr(),
+                                        dk.data_ptr(),
                                         dv.data_ptr(), work.data_ptr(), stream_ptr()), "hv_attention_backward")
     return dq, dk, dv
 

@@ -72,10 +72,36 @@ def current() -> Optional[RunCtx]:
     return _CTX.get()
 
 
+class _TrainState:
+    """Process-level state of the training step in progress (train_model.system_forward sets it,
+    HVTrainer clears it after the step).  Training forwards enter no RunCtx, and autograd runs
+    their backward on its own worker thread, where a ContextVar set by the forward is not
+    visible -- so the model's HVOptions and the dropout seed-offset word of a training step live
+    here, read by the forward and the backward launches alike.  One training step at a time per
+    process (the trainer's contract)."""
+    opts: HVOptions = DEFAULT_OPTIONS
+    seed_offset: Optional[torch.Tensor] = None      # device int32 [1] (hv_kernels.h seed_offset)
+
+
+_TRAIN = _TrainState()
+
+
+def set_train_state(opts: Optional[HVOptions] = None, seed_offset: Optional[torch.Tensor] = None) -> None:
+    _TRAIN.opts = opts if opts is not None else DEFAULT_OPTIONS
+    _TRAIN.seed_offset = seed_offset
+
+
+def seed_offset_ptr() -> Optional[int]:
+    """Device pointer of the current training step's dropout seed offset (None: seeds by value)."""
+    t = _TRAIN.seed_offset
+    return None if t is None else t.data_ptr()
+
+
 def options() -> HVOptions:
-    """The options of the forward in progress (the defaults outside any forward)."""
+    """The options of the forward in progress: its RunCtx's, else the training step's (set by
+    system_forward for the forward and its backward), else the defaults."""
     ctx = _CTX.get()
-    return ctx.opts if ctx is not None else DEFAULT_OPTIONS
+    return ctx.opts if ctx is not None else _TRAIN.opts
 
 
 class use_ctx:

@@ -272,7 +272,11 @@ def head_logits(ph, x, H):
 # ------------------------------------------------------------------------- system
 def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection",
                    compute_loss: bool = False) -> Dict[str, Any]:
-    """HybridVisionSystem.forward(x, targets, task, compute_loss) with model.training True."""
+    """HybridVisionSystem.forward(x, targets, task, compute_loss) with model.training True.
+    The model's HVOptions (kernel variants) apply to this forward and its backward
+    (runtime._TRAIN: the backward runs on autograd's worker thread, outside any RunCtx)."""
+    from .runtime import _TRAIN, module_options
+    _TRAIN.opts = module_options(model)
     dt = PRECISIONS[model.hv_precision]
     H = _hres_table(model)
     xin = to_nhwc(x.detach(), dt)

@@ -95,9 +95,19 @@ class GradBuckets:
         # in bucket order.  Step 1 (nothing agreed yet) reduces everything in finish().
         self.agreed = [False] * len(self.buckets)
         self._next = 0
+        # the gradients were pre-divided by world (HVTrainer scales the loss by 1/world, exact for
+        # power-of-two worlds): the all-reduce then sums, with no per-bucket division pass
+        self.prescaled = False
+        # device-side 'received a gradient' flags (OR over ranks), read by the clipping / AdamW
+        # kernels -- no host round trip; the host copy (`received`) is materialised on demand
+        self.active_dev: Optional[Tensor] = None
+        self._flags_key = None
+        self._flags_local: Optional[Tensor] = None
+        self._flag_reads: List = []            # (event, pinned host copy) of reduced flags, oldest first
+        self._received_host: Optional[List[bool]] = None
         # which parameters received a gradient this step: the optimizer skips the others like
         # torch.optim skips grad=None (optimizer.py:144)
-        self.received = [False] * len(self.params)
+        self._received_local = [False] * len(self.params)
         self._index = {id(p): i for i, p in enumerate(self.params)}
         # the engine runs a leaf's hooks even when its producer returned None for it (e.g. the
         # grouped Sinkhorn's unused final-fusion projection), so receipt is read from the
@@ -108,7 +118,7 @@ class GradBuckets:
     def _flag_hook(self, idx: int):
         def hook(g):
             if g is not None:
-                self.received[idx] = True
+                self._received_local[idx] = True
         return hook
 
     def _span(self, i: int):
@@ -149,7 +159,8 @@ class GradBuckets:
         if self.world > 1:
             lo, hi = self._span(i)
             view = self.flat[lo:hi]
-            view.div_(self.world)
+            if not self.prescaled:
+                view.div_(self.world)
             self._pending.append(dist.all_reduce(view, group=self.group, async_op=True))
 
     def _issue_agreed(self) -> None:
@@ -178,12 +189,36 @@ class GradBuckets:
         self.flat.zero_()
         for p in self.params:
             p.grad = None
-        self.received = [False] * len(self.params)
+        self._received_local = [False] * len(self.params)
+        self._received_host = None
         self._ready = [set() for _ in self.buckets]
         self._flushed = [False] * len(self.buckets)
         self._reduced = [False] * len(self.buckets)
         self._next = 0
         self._pending = []
+        self._consume_flag_reads(lag=2)
+
+    @property
+    def received(self) -> List[bool]:
+        """Per-parameter 'received a gradient this step' (OR over ranks), on the host.  The step
+        itself only uses the device copy (`active_dev`); reading this synchronises with it."""
+        if self._received_host is None:
+            if self.active_dev is None:
+                return list(self._received_local)
+            self._received_host = [bool(v) for v in self.active_dev.tolist()]
+        return self._received_host
+
+    def _consume_flag_reads(self, lag: int) -> None:
+        """Apply the reduced 'bucket completed through the hooks' flags of the step `lag` steps
+        back as the agreed set.  Every rank applies the same step's flags at the same point, so
+        the collective order stays identical; lag 2 means the event has long completed (the host
+        never waits on the current step's GPU work)."""
+        while len(self._flag_reads) >= lag:
+            ev, host = self._flag_reads.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            n = len(self.params)
+            self.agreed = [v == 0 for v in host[n:].tolist()]
 
     def finish(self):
         """Flush and reduce the buckets not reduced from the hooks -- the agreed ones still open
@@ -206,21 +241,41 @@ class GradBuckets:
         self._pending = []
         for p, v in zip(self.params, self.views):
             p.grad = v
+        n = len(self.params)
+        key = tuple(self._received_local) + tuple(hooked)
+        if key != self._flags_key:              # new local flags: one async upload (then cached)
+            host = torch.tensor([int(r) for r in self._received_local] + [1 - int(h) for h in hooked],
+                                dtype=torch.int32)
+            if self.flat.is_cuda:
+                host = host.pin_memory()
+            self._flags_local = host.to(self.flat.device, non_blocking=True)
+            if self.flat.is_cuda:
+                from .ops import keep_if_capturing
+                keep_if_capturing(host)
+            self._flags_key = key
         if self.world > 1:
-            flags = torch.tensor([int(r) for r in self.received] + [1 - int(h) for h in hooked],
-                                 dtype=torch.int32, device=self.flat.device)
+            flags = self._flags_local.clone()
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
-            f = flags.tolist()
-            n = len(self.params)
-            self.received = [bool(v) for v in f[:n]]
-            self.agreed = [v == 0 for v in f[n:]]
+            self.active_dev = flags[:n]
+            if flags.is_cuda:                   # read back two steps later, without a stall
+                host = torch.empty(flags.shape, dtype=flags.dtype).pin_memory()
+                host.copy_(flags, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._flag_reads.append((ev, host))
+            else:                               # gloo on CPU: the reduce is done, apply it now
+                self._flag_reads.append((None, flags.clone()))
+                self._consume_flag_reads(lag=1)
         else:
+            self.active_dev = self._flags_local[:n]
             self.agreed = hooked
 
 
 class FusedAdamW:
     """Per-group grad-norm clipping + AdamW as HIP kernels over a device table (hv_grad_norms,
-    hv_adamw); no host synchronisation."""
+    hv_adamw); no host synchronisation.  Which parameters take part in a step ('received a
+    gradient', torch.optim's grad-is-None skip) is a DEVICE flag array read by the kernels, so a
+    data-parallel step never waits on the host for it and the whole step is graph-capturable."""
 
     def __init__(self, named_params: Sequence, lr: float = 1e-3, weight_decay: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norms=(0.5, 1.0)):
@@ -231,17 +286,25 @@ class FusedAdamW:
         self.exp_avg = [torch.zeros_like(p) for _, p in self.named]
         self.exp_avg_sq = [torch.zeros_like(p) for _, p in self.named]
         self.step_count = 0
-        self.param_steps = [0] * len(self.named)   # per-parameter steps (reference state['step'])
-        # the same counts on the device, for the per-parameter bias correction of hv_adamw
+        # per-parameter step counts (reference / torch.optim state['step']) live on the device,
+        # advanced by the active flags; param_steps reads them back on demand
         self._steps_dev = torch.zeros(len(self.named), device=self.named[0][1].device, dtype=torch.int32)
-        self._active_dev = None
+        self._active_cache = (None, None)
         self.norms = torch.zeros(len(self.max_norms), device=dev, dtype=torch.float32)
         self.coefs = torch.ones(len(self.max_norms), device=dev, dtype=torch.float32)
         self._table = None
         self._key = None
         self.device = dev
 
-    def _build(self, active):
+    @property
+    def param_steps(self) -> List[int]:
+        return [int(v) for v in self._steps_dev.tolist()]
+
+    @param_steps.setter
+    def param_steps(self, steps: Sequence[int]) -> None:
+        self._steps_dev.copy_(torch.tensor([int(v) for v in steps], dtype=torch.int32))
+
+    def _build(self):
         lib = L.lib()
         ents = (L.ParamEntry * len(self.named))()
         blk = 0
@@ -250,7 +313,7 @@ class FusedAdamW:
                 raise TypeError(f"{name}: FusedAdamW needs contiguous fp32 parameters")
             e = ents[i]
             e.param = p.data_ptr()
-            e.grad = p.grad.data_ptr() if p.grad is not None and active[i] else None
+            e.grad = p.grad.data_ptr() if p.grad is not None else None
             e.exp_avg, e.exp_avg_sq = self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr()
             e.n = p.numel()
             e.group = mhc_group(name)
@@ -261,34 +324,51 @@ class FusedAdamW:
         self._table = upload_table(ents, self.device)
         self._work = torch.empty(2 * blk, device=self.device, dtype=torch.float32)
 
-    def step(self, clip: bool = True, active: Optional[Sequence[bool]] = None):
-        """active[i] False = parameter i got no gradient this step: no clipping contribution,
+    def _active_tensor(self, active) -> Tensor:
+        """Device int32 [count] flags from a device tensor (used as is), a host sequence (uploaded
+        once per distinct value) or None (every parameter with a gradient)."""
+        if isinstance(active, torch.Tensor):
+            if active.numel() != len(self.named) or active.dtype != torch.int32 or not active.is_cuda:
+                raise ValueError("active: device int32 tensor with one flag per parameter")
+            return active
+        key = tuple(bool(a) for a in active) if active is not None else (True,) * len(self.named)
+        if self._active_cache[0] != key:
+            host = torch.tensor([int(a) for a in key], dtype=torch.int32).pin_memory()
+            self._active_cache = (key, host.to(self.device, non_blocking=True))
+            from .ops import keep_if_capturing
+            keep_if_capturing(host)
+        return self._active_cache[1]
+
+    def step(self, clip: bool = True, active=None):
+        """active[i] false = parameter i got no gradient this step: no clipping contribution,
         no weight decay, no moment update (torch.optim's grad-is-None skip)."""
-        active = tuple(active) if active is not None else (True,) * len(self.named)
-        key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named) + active
+        key = tuple((p.data_ptr(), None if p.grad is None else p.grad.data_ptr()) for _, p in self.named)
         if key != self._key:
-            self._build(active)
+            self._build()
             self._key = key
-            self._active_dev = torch.tensor([int(a) for a in active], dtype=torch.int32).to(self.device)
+        act = self._active_tensor(active)
         lib = L.lib()
         self.step_count += 1
-        for i, a in enumerate(active):
-            self.param_steps[i] += int(a)
-        self._steps_dev.add_(self._active_dev)
+        self._steps_dev.add_(act)
         coefs = None
         if clip:
             mx = (C.c_float * len(self.max_norms))(*self.max_norms)
             check(lib.hv_grad_norms(self._table.data_ptr(), len(self.named), self._blocks, len(self.max_norms), mx,
                                     self.norms.data_ptr(), self.coefs.data_ptr(), self._work.data_ptr(),
-                                    stream_ptr()), "hv_grad_norms")
+                                    act.data_ptr(), stream_ptr()), "hv_grad_norms")
             coefs = self.coefs.data_ptr()
         b1, b2 = self.betas
         check(lib.hv_adamw(self._table.data_ptr(), len(self.named), self._blocks, coefs, self.lr, b1, b2, self.eps,
-                           self.wd, self.step_count, self._steps_dev.data_ptr(), stream_ptr()), "hv_adamw")
+                           self.wd, self.step_count, self._steps_dev.data_ptr(), act.data_ptr(), stream_ptr()),
+              "hv_adamw")
         # the kernel wrote the parameters behind autograd's back: bump their version counters as
         # an in-place torch update would, so frozen coefficients / captured graphs (VersionWatch)
-        # see the new weights
-        increment_version([p for (_, p), a in zip(self.named, active) if a])
+        # see the new weights (every parameter: the skipped ones are unchanged but a version
+        # bump is harmless, and knowing which were skipped would need the device flags)
+        self.bump_versions()
+
+    def bump_versions(self) -> None:
+        increment_version([p for _, p in self.named])
 
     # ---- torch.optim-compatible state (checkpoints load into / from torch.optim.AdamW)
     def state_dict(self) -> Dict:
@@ -296,8 +376,9 @@ class FusedAdamW:
         ManifoldAwareOptimizer (optimizer.py:31-70: its param group also carries mhc_params and
         manifold_update_freq, read by step() at :125).  Parameters that never received a
         gradient have no state, as in torch."""
-        state = {i: {"step": torch.tensor(float(self.param_steps[i])), "exp_avg": self.exp_avg[i],
-                     "exp_avg_sq": self.exp_avg_sq[i]} for i in range(len(self.named)) if self.param_steps[i] > 0}
+        steps = self.param_steps
+        state = {i: {"step": torch.tensor(float(steps[i])), "exp_avg": self.exp_avg[i],
+                     "exp_avg_sq": self.exp_avg_sq[i]} for i in range(len(self.named)) if steps[i] > 0}
         return {"state": state,
                 "param_groups": [{"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
                                   "weight_decay": self.wd, "amsgrad": False, "maximize": False,
@@ -310,46 +391,75 @@ class FusedAdamW:
     def load_state_dict(self, sd: Dict) -> None:
         g = sd["param_groups"][0]
         self.lr, self.betas, self.eps, self.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
-        steps = []
+        steps = [0] * len(self.named)
         for i, (name, p) in enumerate(self.named):
             st = sd["state"].get(i, sd["state"].get(str(i)))
             if st is None:
                 continue
             self.exp_avg[i].copy_(st["exp_avg"])
             self.exp_avg_sq[i].copy_(st["exp_avg_sq"])
-            self.param_steps[i] = int(float(st["step"]))
-            steps.append(self.param_steps[i])
-        if steps:
+            steps[i] = int(float(st["step"]))
+        if any(steps):
             self.step_count = max(steps)
-        self._steps_dev.copy_(torch.tensor(self.param_steps, dtype=torch.int32))
+        self._steps_dev.copy_(torch.tensor(steps, dtype=torch.int32))
 
     def total_norm(self) -> Tensor:
         """sqrt(sum of squared group norms) (mhc_trainer.py:383), a device scalar."""
         return self.norms.pow(2).sum().sqrt()
 
 
+SEED_STRIDE = 0x2545F491        # dropout seed-offset advance per step (odd: all 2^32 offsets visited)
+
+
 class HVTrainer:
-    """One training step = forward (train mode) + YOLOLoss + backward + all-reduce + clip + AdamW."""
+    """One training step = forward (train mode) + YOLOLoss + backward + all-reduce + clip + AdamW.
+
+    graph=True (single process, HIP device): the whole step -- forward, loss, backward, gradient
+    flush, clipping and AdamW -- is captured ONCE into a hipGraph (torch.cuda.CUDAGraph) and
+    replayed every later step: ~3,000 kernel launches per step at 640^2 leave the host (an eager
+    step spends ~90 ms issuing them).  The first step runs eagerly (it populates the caching
+    allocator, the device tables and the optimizer's table), the second captures and replays.
+    Dropout stays random per step: every dropout kernel adds the device word `seed_offset` to its
+    seed, and the graph advances that word at its start.  Steps that run the stability monitor
+    (every `monitor_every`-th, metrics only) run eagerly.  Inputs are copied into the graph's
+    static buffers; the returned loss tensors are the graph's static outputs (overwritten by the
+    next step).  A change of parameter storage or input shape re-captures."""
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_grad_norm: float = 1.0, mhc_max_norm: float = 0.5, bucket_mb: int = 64,
-                 broadcast_buffers: bool = True, group=None, monitor_every: int = 50):
+                 broadcast_buffers: bool = True, group=None, monitor_every: int = 50, graph: bool = False):
         self.model = model
         # _monitor_stability (eigvalsh of every H_res, signal ratios) is metrics-only: run it
         # every `monitor_every` steps instead of every forward (0 disables it)
         from .manifold import ManifoldHyperConnection
-        for m in model.modules():
-            if isinstance(m, ManifoldHyperConnection):
-                m.monitor_every = monitor_every
+        self._mhc = [m for m in model.modules() if isinstance(m, ManifoldHyperConnection)]
+        self.monitor_every = monitor_every
+        self._set_monitor(monitor_every)
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         self.grads = GradBuckets(named, bucket_mb << 20, group)
         self.opt = FusedAdamW(named, lr, weight_decay, betas, eps, (mhc_max_norm, max_grad_norm))
         self.world = self.grads.world
         self.group = group
+        # DDP averaging: the loss is scaled by 1/world before the backward (exact for power-of-two
+        # worlds), so the bucket all-reduces sum with no division pass over the gradients
+        self.grads.prescaled = self.world > 1
         self.broadcast_buffers = broadcast_buffers and self.world > 1
         if self.world > 1:                         # DDP construction: replicas start identical
             self._broadcast(list(model.parameters()) + list(model.buffers()))
         self._buf_flats = self._flatten_buffers() if self.broadcast_buffers else []
+        dev = named[0][1].device
+        self.seed_offset = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = bool(graph) and self.world == 1 and dev.type == "cuda"
+        self.steps_done = 0
+        self.replays = 0
+        self.captures = 0
+        self._g: Optional[Dict] = None
+
+    def _set_monitor(self, every: int, reset: bool = False) -> None:
+        for m in self._mhc:
+            m.monitor_every = every
+            if reset:
+                m._mon_count = 0
 
     def _flatten_buffers(self):
         """Rebind every buffer of the model as a view of one flat tensor per dtype, so the
@@ -403,6 +513,59 @@ class HVTrainer:
                 return False
         return True
 
+    def _body(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
+        """zero -> forward -> loss -> backward -> flush/all-reduce -> clip + AdamW (all launches on
+        the current stream; capturable at world 1)."""
+        from .runtime import module_options, set_train_state
+        set_train_state(module_options(self.model), self.seed_offset)
+        try:
+            self.seed_offset.add_(SEED_STRIDE)         # new dropout masks every step
+            self.grads.zero()
+            out = self.model(images, targets=targets, compute_loss=True)
+            loss = out["loss"]
+            total = loss["total_loss"]
+            (total * (1.0 / self.world) if self.world > 1 else total).backward()
+            self.grads.finish()
+            self.opt.step(clip=True, active=self.grads.active_dev)
+        finally:
+            set_train_state()
+        return loss
+
+    def _eager(self, images: Tensor, targets: List[Tensor], monitor: bool) -> Dict[str, Tensor]:
+        from .manifold import flush_stability
+        if self.graph:                             # the graph never monitors; eager steps do on cadence
+            self._set_monitor(1 if monitor else 0, reset=True)
+        try:
+            loss = self._body(images, targets)
+        finally:
+            if self.graph:
+                self._set_monitor(0)
+        flush_stability()                          # monitors' eigenvalue buffers current after every step
+        return loss
+
+    def _graph_key(self, images: Tensor, targets: List[Tensor]):
+        return (tuple(images.shape), images.dtype, tuple(tuple(t.shape) for t in targets),
+                tuple(p.data_ptr() for p in self.grads.params), self.model.hv_precision
+                if hasattr(self.model, "hv_precision") else None)
+
+    def _capture(self, images: Tensor, targets: List[Tensor], key) -> None:
+        from . import ops
+        self._g = None
+        torch.cuda.synchronize()
+        static_x = images.detach().clone()
+        static_t = [t.detach().clone() for t in targets]
+        self._set_monitor(0)
+        keep: List = []
+        graph = torch.cuda.CUDAGraph()
+        # thread_local: the autograd engine's worker thread issues the backward's launches onto
+        # the capturing stream; the device-table uploads inside the step become graph memcpy
+        # nodes whose pinned sources `keep` holds for the graph's lifetime
+        with ops.capture_keepalive(keep):
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                loss = self._body(static_x, static_t)
+        self._g = {"graph": graph, "x": static_x, "t": static_t, "loss": loss, "keep": keep, "key": key}
+        self.captures += 1
+
     def step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
         self.model.train()
         if self._buf_flats and not self._buffers_still_flat():
@@ -410,15 +573,24 @@ class HVTrainer:
             # every rank sees the same module tree changes)
         for flat in self._buf_flats:               # DDP broadcast_buffers: rank 0's buffers
             dist.broadcast(flat, 0, group=self.group)
-        self.grads.zero()
-        out = self.model(images, targets=targets, compute_loss=True)
-        loss = out["loss"]
-        loss["total_loss"].backward()
-        self.grads.finish()
-        self.opt.step(clip=True, active=self.grads.received)
-        from .manifold import flush_stability
-        flush_stability()                          # monitors' eigenvalue buffers current after every step
-        return loss
+        monitor = self.monitor_every > 0 and self.steps_done % self.monitor_every == 0
+        self.steps_done += 1
+        if not self.graph:
+            return self._eager(images, targets, monitor)
+        key = self._graph_key(images, targets)
+        if monitor or self.steps_done == 1:        # step 1 warms the allocator and the device tables
+            return self._eager(images, targets, monitor)
+        if self._g is None or self._g["key"] != key:
+            self._capture(images, targets, key)
+        g = self._g
+        g["x"].copy_(images)
+        for dst, src in zip(g["t"], targets):
+            dst.copy_(src)
+        g["graph"].replay()
+        self.replays += 1
+        self.opt.step_count += 1
+        self.opt.bump_versions()                   # the replay's AdamW wrote the parameters
+        return g["loss"]
 
 
 def save_checkpoint(path: str, model, trainer: Optional["HVTrainer"] = None, epoch: int = 0, global_step: int = 0,

@@ -32,9 +32,10 @@ enum { HV_ACT_NONE = 0, HV_ACT_RELU = 1, HV_ACT_SILU = 2, HV_ACT_GELU = 3,
        HV_ACT_LEAKY = 4 /* slope 0.1 */, HV_ACT_SIGMOID = 5 };
 enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
 
-/* ABI version: 2 since hv_adamw gained `steps`, hv_mhc_fused_supported gained `variant`,
+/* ABI version: 2 since hv_adamw gained `steps` and `active`, hv_grad_norms `active`, the dropout
+ * entry points and hv_gemm_desc a device `seed_offset`, hv_mhc_fused_supported gained `variant`,
  * hv_mhc_fused_args grew by 8 bytes and the hv_gemm_set_* / hv_mhc_fused_set_* setters were
- * removed (round 3).  Bindings compare it with the version they were written against. */
+ * removed.  Bindings compare it with the version they were written against. */
 #define HV_ABI_VERSION 2
 int hv_abi_version(void);
 /* build provenance: a hash of the sources (csrc/*.hip, csrc/*.h, include/*.h, Makefile) the
@@ -142,6 +143,10 @@ typedef struct hv_gemm_desc {
   int* splitk_count;
   int splitk;
   int pad2_;
+  /* dropout seed offset (device, may be NULL): the epilogues' keep(m, n) uses drop_seed +
+     *seed_offset, so a graph-captured training step draws new masks on every replay by
+     advancing one device word (the seed arguments baked into the graph stay constant) */
+  const unsigned int* seed_offset;
 } hv_gemm_desc;
 
 #define HV_SPLITK_MAX_TILES 4096
@@ -452,7 +457,9 @@ int hv_preprocess_pil(const uint8_t* img, int n, int h, int w, int swap_rb, int 
  * dropout, YOLOLoss, clipping and AdamW.  Same conventions as above (caller-owned
  * buffers, asynchronous, graph-capturable); gradients of parameters are fp32.
  * Dropout masks are never stored: keep(idx) is regenerated from (seed, element index)
- * by the forward and the backward kernels alike (hv_common.h hv_drop_scale).
+ * by the forward and the backward kernels alike (hv_common.h hv_drop_scale).  Every dropout
+ * entry point also takes `seed_offset` (device word, may be NULL): the effective seed is
+ * seed + *seed_offset, read by the kernel -- a captured training graph advances it per replay.
  * ==================================================================================== */
 
 /* Weight-gradient GEMM C[N1, N2] (+)= sum_p A[p, n1] * B[p, n2]  (both token-major).
@@ -508,15 +515,15 @@ int hv_bn_backward(int dtype, const void* x, const void* dy, int rows, int c, co
    forward: y = dropout(norm(x) * gamma + beta) (+ residual); saves mean (LN) and rstd. */
 int hv_rownorm_train(int mode, int x_dtype, const void* x, int rows, int cols, float eps,
                      const float* gamma, const float* beta, float drop_p, unsigned int seed,
-                     int y_dtype, void* y, const void* residual, float* mean, float* rstd,
-                     hv_stream_t stream);
+                     const unsigned int* seed_offset, int y_dtype, void* y, const void* residual, float* mean,
+                     float* rstd, hv_stream_t stream);
 /* backward: g = dy * keep; dx = norm'(x)^T (g * gamma) (+ dx_add); dgamma/dbeta (may be NULL)
    = column sums of g * xhat / g.  gamma == NULL: no affine (the folded mHC LN_pre). */
 size_t hv_rownorm_work_floats(int rows, int cols);
 int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_dtype, const void* dy, int rows,
                         int cols, const float* mean, const float* rstd, const float* gamma,
-                        float drop_p, unsigned int seed, int dx_dtype, void* dx, const void* dx_add,
-                        float* dgamma, float* dbeta, float* work, hv_stream_t stream);
+                        float drop_p, unsigned int seed, const unsigned int* seed_offset, int dx_dtype, void* dx,
+                        const void* dx_add, float* dgamma, float* dbeta, float* work, hv_stream_t stream);
 /* Coefficient backward of one mHC site (autograd of constrained_matrices, manifold_layers.py:
    205-221, through the fold of DESIGN.md §2): from dGc [D, Hd] (gradient of the centred gate),
    du [Hd], dWc_x [D, D] and dWc_h [Hd, D] (gradients of the centred output coefficients):
@@ -528,10 +535,10 @@ int hv_mhc_param_backward(int D, int Hd, const float* dgc, const float* du, cons
                           float* dbeta, float* dh_res, float* dh_post_raw, float* work, hv_stream_t stream);
 /* dpre[i] = dy[i] * keep(i) * act'(pre[i])  (elementwise; dy/pre/dpre share dtype) */
 int hv_act_backward(int dtype, const void* dy, const void* pre, long n, int act, float drop_p,
-                    unsigned int seed, void* dpre, hv_stream_t stream);
+                    unsigned int seed, const unsigned int* seed_offset, void* dpre, hv_stream_t stream);
 /* y = dropout(x) (elementwise, idx = element index) */
-int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed, void* y,
-               hv_stream_t stream);
+int hv_dropout(int dtype, const void* x, long n, float drop_p, unsigned int seed,
+               const unsigned int* seed_offset, void* y, hv_stream_t stream);
 
 /* Sinkhorn backward through every iteration, grouped (autograd of manifold_layers.py:56-73).
    Uses the a_t / b_t scaling vectors the forward left in each entry's `work`; recomputes K
@@ -579,23 +586,24 @@ int hv_scatter_rows(int dtype, const void* dy, long stride_rows, int n, int c, v
    backward recomputes P from lse:  dq, dk, dv. */
 int hv_attention_train(int dtype, const void* q, const void* k, const void* v, void* o, float* lse,
                        int n, int L, int heads, int hd, float sm_scale, float drop_p, unsigned int seed,
-                       hv_stream_t stream);
+                       const unsigned int* seed_offset, hv_stream_t stream);
 /* work: n * heads * L floats (row dots dout . o) */
 int hv_attention_backward(int dtype, const void* q, const void* k, const void* v, const void* o,
                           const void* dout, const float* lse, int n, int L, int heads, int hd,
-                          float sm_scale, float drop_p, unsigned int seed, void* dq, void* dk, void* dv,
-                          float* work, hv_stream_t stream);
+                          float sm_scale, float drop_p, unsigned int seed, const unsigned int* seed_offset,
+                          void* dq, void* dk, void* dv, float* work, hv_stream_t stream);
 /* The same two operations on the matrix cores (bf16, head_dim 32): identical dropout keep(i, j)
    and lse convention, so the forward and backward of either path pair.  vt_work /  work hold
    transposed zero-padded [n*heads, 32, Lp] operand copies (hv_attention_train_mfma_work_elems
    bf16 elements each; the backward needs 3 of them followed by n*heads*L floats). */
 size_t hv_attention_train_mfma_work_elems(int n, int L, int heads);
 int hv_attention_train_mfma(const void* q, const void* k, const void* v, void* o, float* lse, int n, int L,
-                            int heads, float sm_scale, float drop_p, unsigned int seed, void* vt_work,
-                            hv_stream_t stream);
+                            int heads, float sm_scale, float drop_p, unsigned int seed,
+                            const unsigned int* seed_offset, void* vt_work, hv_stream_t stream);
 int hv_attention_backward_mfma(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                const float* lse, int n, int L, int heads, float sm_scale, float drop_p,
-                               unsigned int seed, void* dq, void* dk, void* dv, void* work, hv_stream_t stream);
+                               unsigned int seed, const unsigned int* seed_offset, void* dq, void* dk, void* dv,
+                               void* work, hv_stream_t stream);
 
 /* YOLOLoss for one scale (yolo_head.py:374-465): logits NHWC [n, h, w, A*P], targets
    [n, A, h, w, P] fp32.  Writes sums[0..3] = raw coord / obj / noobj / cls sums, sums[4] =
@@ -617,17 +625,19 @@ typedef struct hv_param_entry {
 } hv_param_entry;
 int hv_param_blocks(long n);
 /* norms[g] = ||grads of group g||_2 ; coefs[g] = min(1, max_norm[g] / (norms[g] + 1e-6));
-   work: 2 * total_blocks floats */
+   work: 2 * total_blocks floats.  active (device [count], may be NULL): entries with active[i] == 0
+   received no gradient this step (torch.optim's grad-is-None) and are skipped -- a data-parallel
+   step decides this on the device (flags all-reduced over ranks), with no host round trip. */
 int hv_grad_norms(const hv_param_entry* dev_table, int count, int total_blocks, int groups,
                   const float* max_norm /* host [groups] */, float* norms, float* coefs, float* work,
-                  hv_stream_t stream);
+                  const int* active, hv_stream_t stream);
 /* AdamW step with the clip coefficient of each parameter's group (coefs may be NULL).  Bias
    correction 1 - beta^t uses each parameter's own step count steps[i] (device [count], the
    torch.optim.AdamW per-parameter state['step']; a parameter that skipped steps keeps its own
    count) or, with steps == NULL, `step` for every parameter. */
 int hv_adamw(const hv_param_entry* dev_table, int count, int total_blocks, const float* coefs,
              float lr, float beta1, float beta2, float eps, float weight_decay, int step,
-             const int* steps, hv_stream_t stream);
+             const int* steps, const int* active /* as hv_grad_norms */, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Stability monitor (ManifoldHyperConnection._monitor_stability, reference

@@ -144,7 +144,7 @@ def _trainer_worker(rank, world, port, q):
                     m.running_mean.fill_(float(rank + 1))
         tr = HVTrainer(net, bucket_mb=1)
         calls = []
-        tr.opt.step = lambda clip=True, active=None: calls.append(list(active))
+        tr.opt.step = lambda clip=True, active=None: calls.append([bool(v) for v in active])
         init = {n: p.detach().clone().numpy() for n, p in net.named_parameters()}
         bufs0 = {n: b.detach().clone().numpy() for n, b in net.named_buffers()}
         res = []

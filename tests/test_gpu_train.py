@@ -814,6 +814,69 @@ def test_trainer_step_reduces_loss(gpu_device):
     assert losses[-1] < losses[0]
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_trainer_graph_step_equals_eager(gpu_device, precision):
+    """HVTrainer(graph=True): step 1 eager, step 2 captured into a hipGraph and replayed, later
+    steps replays (monitor steps eager) -- forward, YOLOLoss, backward (Sinkhorn autograd
+    included), gradient flush, clipping and AdamW.  With dropout off, every step leaves the
+    parameters, the optimizer moments and the BN statistics BITWISE equal to the eager trainer's
+    on the same batches (the graph replays exactly the launches an eager step issues)."""
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer
+    ma, _ = _tiny_model(gpu_device, precision)
+    mb, _ = _tiny_model(gpu_device, precision)
+    ta = HVTrainer(ma, lr=1e-3, monitor_every=4)
+    tb = HVTrainer(mb, lr=1e-3, monitor_every=4, graph=True)
+    B, S = 2, 96
+    gen = torch.Generator().manual_seed(5)
+    for step in range(6):
+        x = torch.randn(B, 3, S, S, generator=gen).to(gpu_device)
+        tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=20 + step)]
+        la = {k: float(v) for k, v in ta.step(x, tg).items()}
+        lb = {k: float(v) for k, v in tb.step(x, tg).items()}
+        torch.cuda.synchronize()
+        assert la == lb, (step, la, lb)
+        for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            assert torch.equal(pa, pb), (step, n)
+        for (n, ba), (_, bb) in zip(ma.named_buffers(), mb.named_buffers()):
+            if "running" in n or "num_batches" in n:
+                assert torch.equal(ba, bb), (step, n)
+        for a, b in zip(ta.opt.exp_avg_sq, tb.opt.exp_avg_sq):
+            assert torch.equal(a, b)
+    assert tb.captures == 1 and tb.replays == 4          # steps 2-4 and 6; 1 (warm-up) and 5 (monitor) eager
+    assert ta.opt.param_steps == tb.opt.param_steps
+
+
+def test_trainer_graph_dropout_masks_change_per_replay(gpu_device):
+    """With dropout on, the replayed graph draws NEW masks every step (the dropout kernels add
+    the device seed-offset word the graph advances), so two replays on the same batch with lr = 0
+    (parameters unchanged) give different losses -- and identical ones with dropout off."""
+    from hv_amd import HybridVisionSystem
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer, SEED_STRIDE
+    from oracle import weights as W
+    B, S = 2, 96
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(3)).to(gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=4)]
+    res = {}
+    for drop in (True, False):
+        m = HybridVisionSystem(dict(num_blocks=[1, 1, 1, 1], vit_depth=1, sk_iters=5, verbose=False))
+        W.load_formula_weights(m, "wc")
+        m = m.to(gpu_device).train()
+        if not drop:
+            for mod in m.modules():
+                if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+                    mod.p = 0.0
+        tr = HVTrainer(m, lr=0.0, weight_decay=0.0, monitor_every=0, graph=True)
+        off0 = int(tr.seed_offset.item())
+        losses = [float(tr.step(x, tg)["total_loss"]) for _ in range(4)]
+        assert tr.replays == 3
+        assert int(tr.seed_offset.item()) == (off0 + 4 * SEED_STRIDE + 2 ** 31) % 2 ** 32 - 2 ** 31
+        res[drop] = losses
+    assert res[True][2] != res[True][3] and res[True][1] != res[True][2]
+    assert res[False][1] == res[False][2] == res[False][3]
+
+
 def test_trainer_skips_parameters_without_gradient(gpu_device):
     """final_fusion / output_projection feed no loss term, so their gradients stay None in the
     reference and torch.optim / ManifoldAwareOptimizer (optimizer.py:144) skip them: no weight
@@ -917,3 +980,41 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
     for key in outs:
         for x0, x1 in zip(outs["staged"], outs[key]):
             assert torch.equal(x0, x1), key
+
+
+def test_dropout_seed_offset_word(gpu_device):
+    """hv_kernels.h seed_offset: every dropout kernel (GEMM training epilogue, row norm,
+    elementwise dropout / activation backward, MFMA attention forward + backward) uses
+    seed + *seed_offset -- bitwise the same masks as passing that sum as the seed."""
+    from hv_amd.runtime import set_train_state
+    T = OT()
+    g = torch.Generator().manual_seed(8)
+    bf = torch.bfloat16
+    a = torch.randn(200, 64, generator=g).to(bf).to(gpu_device)
+    b = (torch.randn(96, 64, generator=g) / 8).to(bf).to(gpu_device)
+    x = torch.randn(70, 256, generator=g).to(bf).to(gpu_device)
+    q, k, v = (torch.randn(2, 50, 256, generator=g).to(bf).to(gpu_device) for _ in range(3))
+    off = torch.tensor([123457], dtype=torch.int32, device=gpu_device)
+    s0 = 1000
+
+    def run(seed):
+        pre = torch.empty(200, 96, device=gpu_device, dtype=bf)
+        out = [T.gemm_train(a, b, mode=1, act="gelu", aux=pre, drop_p=0.3, seed=seed)]
+        out.append(T.gemm_train(a, b, mode=2, act="gelu", aux=pre, drop_p=0.3, seed=seed))
+        out.append(T.rownorm_train(0, x, 1e-5, None, None, 0.3, seed)[0])
+        out.append(T.dropout(x, 0.3, seed))
+        out.append(T.act_backward(x, x, "gelu", 0.3, seed))
+        o, lse = T.attention_train(q, k, v, 8, 0.2, seed)
+        out += [o, *T.attention_backward(q, k, v, o, o, lse, 8, 0.2, seed)]
+        return out
+
+    set_train_state(seed_offset=off)
+    try:
+        with_off = run(s0)
+    finally:
+        set_train_state()
+    plain = run(s0 + 123457)
+    other = run(s0)
+    for i, (u, w) in enumerate(zip(with_off, plain)):
+        assert torch.equal(u, w), i
+    assert not torch.equal(with_off[3], other[3])
