@@ -78,9 +78,24 @@ struct GldsOcc {
   static constexpr int value = lds_w < 1 ? 1 : (lds_w > 4 ? 4 : lds_w);
 };
 
+// Wait until at most `ahead` younger K-tiles (DPT DMA instructions each) are still in flight
+// (vmcnt takes an immediate: one branch per possible count)
+template <int DPT, int MAXA>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  if constexpr (MAXA > 0) {
+    if (ahead >= MAXA) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXA * DPT) : "memory");
+      return;
+    }
+    ring_wait<DPT, MAXA - 1>(ahead);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 template <int BM, int BN, bool CONV, bool TRAIN, bool STAGED = false, int NS = 2, bool SPLIT = false>
 __global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm_glds_kernel(const hv_gemm_desc d) {
-  static_assert(NS >= 2 && NS <= 4, "stages");
+  static_assert(NS >= 2 && NS <= 8, "stages");
   constexpr int STAGE_BYTES = (BM + BN) * ROW;
   constexpr int AI = BM / 32;               // A wave-instructions (8 rows each) per wave
   constexpr int BI = BN / 32;
@@ -218,17 +233,7 @@ __global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(NS - 2, nk - 1 - kt);
-    if constexpr (NS == 4) {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPT) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (NS == 3) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    ring_wait<DPT, NS - 2>(min(NS - 2, nk - 1 - kt));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kb + kt + NS - 1);
@@ -643,6 +648,16 @@ int launch_infer_ns(const hv_gemm_desc& d, hipStream_t s) {
 template <int BM, int BN>
 int launch_infer(const hv_gemm_desc& d, hipStream_t s) {
   constexpr int NS = deep_stages<BM, BN>();
+  if constexpr (BM == 64 && BN == 64) {
+    // 8-stage ring (128 KB LDS, one workgroup per CU) for grids that put at most one workgroup on
+    // each CU anyway (the B=1 frame's 401-token ViT GEMMs: 28-112 tiles), where the k-loop is
+    // bound by DMA latency / K-tiles in flight (0.28 us per 64-deep K-tile with 3 in flight,
+    // profiles/r03/s3/small_gemm_probe_ns4.txt)
+    const long tiles = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64);
+    if (!(d.variant & (HV_GV_SHALLOW | HV_GV_NO_DEEP8)) &&
+        ((d.variant & HV_GV_DEEP8) || (tiles <= 256 && d.K >= 512)))
+      return launch_infer_ns<64, 64, 8>(d, s);
+  }
   if constexpr (NS > 2) {
     if (!(d.variant & HV_GV_SHALLOW)) return launch_infer_ns<BM, BN, NS>(d, s);
   }

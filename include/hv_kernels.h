@@ -170,6 +170,8 @@ typedef struct hv_gemm_desc {
 #define HV_GV_SK_RES4      0x10000 /* ... 4-stage A ring */
 #define HV_GV_TRAIN_BIG    0x20000 /* training epilogues (epi_mode 1 / 2) may take the 256x256 ping-pong kernel
                                       (measured +1.2 % train-step time at B=16, so opt-in) */
+#define HV_GV_DEEP8        0x40000 /* 64x64 tiles on the 8-stage ring whatever the grid (inference epilogues) */
+#define HV_GV_NO_DEEP8     0x80000 /* never the 8-stage ring (automatic: <= 256 tiles and K >= 512) */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

@@ -339,8 +339,9 @@ PP256_CASES = [  # (kind, M, N, K): ragged M/N, 1-3 K-tiles (prologue/tail vmcnt
 
 @pytest.mark.parametrize("kind,M,N,K", PP256_CASES)
 def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
-    """The 256x256 ping-pong LDS-DMA kernel (variant GV_BIG_ALWAYS forces it) against the
-    default tiles: same per-element k order, so bit-identical outputs; plus a CPU fp32 check."""
+    """The 256x256 ping-pong LDS-DMA kernel (variant GV_BIG_ALWAYS forces it) and the 8-stage
+    64x64 ring (GV_DEEP8) against the default tiles: same per-element k order, so bit-identical
+    outputs; plus a CPU fp32 check."""
     ops = _ops()
     from hv_amd import _lib
     g = torch.Generator().manual_seed(M * 7 + N + K)
@@ -385,6 +386,9 @@ def test_gemm_pingpong256_equals_default(gpu_device, kind, M, N, K):
                 outs["base", staged, deep] = run()
         with gemm_variant(flat | _lib.GV_BIG_ALWAYS):
             outs["pp", staged] = run()
+        # 64x64 tiles on the 8-stage ring (fewer K-tiles than stages included: K = 64 .. 192)
+        with gemm_variant(flat | _lib.GV_TILE_64x64 | _lib.GV_DEEP8):
+            outs["deep8", staged] = run()
     torch.cuda.synchronize()
     pp, base = outs["pp", 1], outs["base", 0, 0]
     for key, o in outs.items():
