@@ -649,14 +649,12 @@ template <int BM, int BN>
 int launch_infer(const hv_gemm_desc& d, hipStream_t s) {
   constexpr int NS = deep_stages<BM, BN>();
   if constexpr (BM == 64 && BN == 64) {
-    // 8-stage ring (128 KB LDS, one workgroup per CU) for grids that put at most one workgroup on
-    // each CU anyway (the B=1 frame's 401-token ViT GEMMs: 28-112 tiles), where the k-loop is
-    // bound by DMA latency / K-tiles in flight (0.28 us per 64-deep K-tile with 3 in flight,
-    // profiles/r03/s3/small_gemm_probe_ns4.txt)
-    const long tiles = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64);
-    if (!(d.variant & (HV_GV_SHALLOW | HV_GV_NO_DEEP8)) &&
-        ((d.variant & HV_GV_DEEP8) || (tiles <= 256 && d.K >= 512)))
-      return launch_infer_ns<64, 64, 8>(d, s);
+    // 8-stage ring (128 KB LDS, one workgroup per CU), opt-in (HV_GV_DEEP8): built for the B=1
+    // frame's small grids on the theory that their k-loop waits on DMA latency / K-tiles in
+    // flight -- measured no faster than the 4-stage ring (the 2-stage ring is fastest there) and
+    // B=1 p50 5.23 vs 4.97-5.04 ms (profiles/r04/deep8_rejected.txt): the per-K-tile cost is the
+    // barrier / LDS-read / MFMA dependency chain of a lone workgroup, not the DMA
+    if (d.variant & HV_GV_DEEP8) return launch_infer_ns<64, 64, 8>(d, s);
   }
   if constexpr (NS > 2) {
     if (!(d.variant & HV_GV_SHALLOW)) return launch_infer_ns<BM, BN, NS>(d, s);

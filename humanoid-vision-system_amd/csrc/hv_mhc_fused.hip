@@ -675,9 +675,12 @@ struct Cfg2 {
   static constexpr int TOKG = 32768 / HD, TOK = NG * TOKG, TT = TOKG / 16;   // tokens per group / WG
   static constexpr int TW1 = TOK / NW, TBW = TW1 / 16;                         // GEMM1 tokens per wave
   static constexpr int HQ = HD / 4, HQT = HQ / 16, KC = 32, NCH = 2 * HD / KC, KS1 = D / 32, CPA = D / 8;
+  static constexpr int XPW = KS1 / 4;                                 // 32-wide x chunks per quarter wave
   static constexpr int A1B = KC * D * 2, W2B = HD * 64, STAGE = A1B + W2B, H1B = (TOK / 16) * 1024;
   static constexpr int MAIN = 3 * STAGE + 2 * H1B + 2 * HD * 4;       // + c1 (fp32) kept in LDS
-  static constexpr int NP = 2 * NG, DP = D / NP, DT3 = DP / 16, KT3 = (D + HD) / 32;   // GEMM3 column parts
+  static constexpr int A1P = KC * CPA / NT, W2P = HD * 4 / NT;        // chunk DMA pieces per thread
+  // GEMM3 column parts of 32 output columns: one part's Wc^T slice (all D + HD k) fits a stage
+  static constexpr int NP = D / 32, DP = D / NP, DT3 = DP / 16, KT3 = (D + HD) / 32;
   static constexpr int WCP = KT3 * DP * 64, PROW = DP + 4, PARTG = 4 * TOKG * PROW * 4;   // per group
   static constexpr int RTW = TOKG / 4, LPT = 64 / RTW, CPL = DP / LPT;            // reduce: tokens / lanes
   static constexpr int WPT = KT3 * DP * 4 / NT;                                   // Wc DMA pieces / thread
@@ -685,12 +688,15 @@ struct Cfg2 {
   // in the third stage, group 1's from 3*STAGE on (over the h1 slots and c1)
   static constexpr int LDS3 = 3 * STAGE + (NG > 1 ? PARTG : 0);
   static constexpr int LDS = MAIN > LDS3 ? MAIN : LDS3;
-  static_assert(TBW >= 1 && HQT % 2 == 0 && KS1 <= 4 && DT3 >= 1 && CPL % 4 == 0, "shape");
+  static_assert(TBW >= 1 && HQT % 2 == 0 && KS1 % 4 == 0 && KS1 <= 8 && DT3 >= 1 && CPL % 4 == 0, "shape");
+  static_assert(KC * CPA % NT == 0 && HD * 4 % NT == 0, "uniform chunk DMA per thread");
   static_assert(WCP <= STAGE && PARTG <= STAGE && NG <= 2 && KT3 * DP * 4 % NT == 0, "GEMM3 layout");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int D, int HD, int NG>
+// SPLITW: the end-of-iteration wait leaves the W2 half of chunk ch+2 in flight (it is first read
+// one iteration later than the A1^T half), so the larger W2 DMA gets two iterations of cover
+template <int D, int HD, int NG, bool SPLITW = false>
 __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
     const unsigned short* __restrict__ x, int T, const unsigned short* __restrict__ a1t,
     const float* __restrict__ c1, const unsigned short* __restrict__ w2, const float* __restrict__ b2,
@@ -846,8 +852,15 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
     // iteration recomputes chunk NCH-1 into the idle h1 slot: straight-line code, no branch.
     gemm1(ch + 1 < C::NCH ? ch + 1 : C::NCH - 1, (ch + 1) & 1);
     // this wave's DMAs of chunk ch+2 (or the Wc part) landed; every wave's reads of this
-    // iteration retired and its h1(ch+1) writes visible
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // iteration retired and its h1(ch+1) writes visible.  SPLITW: only the A1^T half of chunk
+    // ch+2 (read by GEMM1 next iteration) and everything older -- W2(ch+1) included -- landed;
+    // in the Wc tail only the part before the newest
+    if constexpr (SPLITW) {
+      if (ch + 2 < C::NCH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::W2P) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::WPT) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -867,13 +880,14 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
                              pack_bf16x2(hv_gelu_fast(q[2] + bb.z), hv_gelu_fast(q[3] + bb.w)));
     }
   }
-  const bool has_x = qq < C::KS1;                      // x chunk qq (32 input columns) on quarter qq
-  uint4 xg[TT];
-  if (has_x) {
+  // x chunks qq, qq + 4, ... (32 input columns each) on quarter qq
+  uint4 xg[C::XPW][TT];
+#pragma unroll
+  for (int xc = 0; xc < C::XPW; ++xc)
 #pragma unroll
     for (int t = 0; t < TT; ++t)
-      xg[t] = *reinterpret_cast<const uint4*>(x + min(tg0 + t * 16 + fr, (long)T - 1) * D + qq * 32 + fg * 8);
-  }
+      xg[xc][t] = *reinterpret_cast<const uint4*>(x + min(tg0 + t * 16 + fr, (long)T - 1) * D + (qq + 4 * xc) * 32 +
+                                                  fg * 8);
 
   // ---- GEMM3 (split-K over the 4 quarter waves of a group) + cross-wave reduce, NP column parts;
   // part dp+2's Wc DMA overlaps the reduce of part dp and the MFMAs of part dp+1
@@ -908,13 +922,14 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
         for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, h2f[j][t], acc3[dt][t]);
       }
     }
-    if (has_x) {
+#pragma unroll
+    for (int xc = 0; xc < C::XPW; ++xc) {
 #pragma unroll
       for (int dt = 0; dt < C::DT3; ++dt) {
         const int r = dt * 16 + fr;
-        const uint4 af = *reinterpret_cast<const uint4*>(wcp + (qq * C::DP + r) * 64 + swz64(r, fg) * 16);
+        const uint4 af = *reinterpret_cast<const uint4*>(wcp + ((qq + 4 * xc) * C::DP + r) * 64 + swz64(r, fg) * 16);
 #pragma unroll
-        for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, xg[t], acc3[dt][t]);
+        for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, xg[xc][t], acc3[dt][t]);
       }
     }
     // partial y^T tiles -> part[quarter][token][col]  (lane: token t*16 + fr, cols dt*16 + 4fg ..)
@@ -1003,10 +1018,10 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
   }
 }
 
-template <int D, int HD, int NG>
+template <int D, int HD, int NG, bool SPLITW = false>
 int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
   using C = Cfg2<D, HD, NG>;
-  auto k = mhc_fused2_kernel<D, HD, NG>;
+  auto k = mhc_fused2_kernel<D, HD, NG, SPLITW>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -1026,7 +1041,7 @@ int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
 extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant) {
   if (dtype != HV_BF16) return 0;
   return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
-         (D == 256 && Hd == 512 && (variant & HV_MV_WIDE));
+         (D == 256 && Hd == 512 && (variant & (HV_MV_WIDE | HV_MV_SPLIT256)));
 }
 
 extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
@@ -1071,7 +1086,14 @@ extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
     // variant 5 = the per-wave 4-wave kernel, 2 = per-wave 8-wave
     if (shape == 2) return launch<128, 512, 1, 1>(a, s);
     if (shape == 5) return launch<128, 512, 1, 2, 4>(a, s);
+    if (shape == 12) return launch2<128, 512, 2, true>(a, s);
     return launch2<128, 512, 2>(a, s);
+  }
+  // D = 256 (ViT / FPN / head sites, Hd = 512): the split-hidden kernel, one 4-wave group of 64
+  // tokens per workgroup (three 48 KiB weight stages fill the LDS)
+  if (a->variant & HV_MV_SPLIT256) {
+    if (shape == 12) return launch2<256, 512, 1, true>(a, s);
+    return launch2<256, 512, 1>(a, s);
   }
   // D=256 (ViT, off by default): at T=6416 / 25600 the unfused chain wins (65 / 150 us vs
   // 94 / 139 us fused, tools/mhc_ab.py); 8-wave groups here, variant 1 = 4-wave

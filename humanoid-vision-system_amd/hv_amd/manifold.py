@@ -346,7 +346,9 @@ class MultiHeadManifoldAttention(nn.Module):
         ctx = current()
         opts = options()
         grp = ctx.plans.get(("group", id(self))) if (ctx is not None and opts.group_qkv) else None
-        if grp is not None and not self.training:
+        # a fused one-launch chain per projection beats sharing GEMM1 across q / k / v
+        fused = opts.use_fused_mhc and ops.mhc_fused_supported(self.q_proj.input_dim, self.q_proj.hidden_dim, x.dtype)
+        if grp is not None and not self.training and not fused:
             q, k, v = (t.view(n, L, -1) for t in self._qkv_grouped(x, grp))
             o = ops.attention(q, k, v, self.num_heads)
             return self.out_proj.forward_tokens(o.view(n * L, -1))

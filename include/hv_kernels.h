@@ -38,7 +38,7 @@ enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
  * removed.  Bindings compare it with the version they were written against. */
 #define HV_ABI_VERSION 2
 int hv_abi_version(void);
-/* build provenance: a hash of the sources (csrc/*.hip, csrc/*.h, include/*.h, Makefile) the
+/* build provenance: a hash of the sources (the .hip / .h files of csrc, the include headers, the Makefile) the
  * library was compiled from; the Python loader recomputes it and refuses a stale build */
 const char* hv_build_id(void);
 /* lets bindings verify their struct mirrors */
@@ -170,8 +170,8 @@ typedef struct hv_gemm_desc {
 #define HV_GV_SK_RES4      0x10000 /* ... 4-stage A ring */
 #define HV_GV_TRAIN_BIG    0x20000 /* training epilogues (epi_mode 1 / 2) may take the 256x256 ping-pong kernel
                                       (measured +1.2 % train-step time at B=16, so opt-in) */
-#define HV_GV_DEEP8        0x40000 /* 64x64 tiles on the 8-stage ring whatever the grid (inference epilogues) */
-#define HV_GV_NO_DEEP8     0x80000 /* never the 8-stage ring (automatic: <= 256 tiles and K >= 512) */
+#define HV_GV_DEEP8        0x40000 /* 64x64 tiles on the 8-stage ring (inference epilogues; measured no gain) */
+#define HV_GV_NO_DEEP8     0x80000 /* (kept for the A/B tools: the 8-stage ring is never automatic) */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
@@ -236,8 +236,10 @@ typedef struct hv_mhc_fused_args {
                                     7 (D = 32/64) per-wave kernel with unmerged fragment reads,
                                     8 / 9 (D = 32/64) the software-pipelined per-wave kernel
                                     (9: unmerged fragment reads), 10 (D = 32/64) the per-wave
-                                    kernel without pipelining */
-#define HV_MV_WIDE        0x100  /* also run (256, 512) fused (slower than the GEMM chain; tests) */
+                                    kernel without pipelining, 12 (D = 128 / 256 split-hidden) the
+                                    chunk loop waits for the A1^T half of the next-next chunk only */
+#define HV_MV_WIDE        0x100  /* also run (256, 512) fused, per-wave kernel (slower than the GEMM chain; tests) */
+#define HV_MV_SPLIT256    0x200  /* (256, 512) on the split-hidden kernel */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
 int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant);

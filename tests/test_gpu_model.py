@@ -577,6 +577,37 @@ def test_mhc_fused_split_hidden_matches_unfused(gpu_device, T, with_res):
     assert rel_l2(y3.numpy(), y2.numpy()) < 1e-2
 
 
+@pytest.mark.parametrize("D,e,T,with_res", [(256, 2, 64, False), (256, 2, 401, True), (256, 2, 6416, False),
+                                             (256, 2, 25601, True), (128, 4, 6417, True)])
+def test_mhc_fused_split_hidden_d256_and_splitw(gpu_device, D, e, T, with_res):
+    """The split-hidden kernel at D = 256 (Hd = 512: the ViT / FPN / head sites; one 4-wave group
+    of 64 tokens per workgroup, GEMM3 in eight 32-column parts, two x chunks per quarter wave)
+    and its split-wait form (variant 12: the chunk loop leaves the W2 half of chunk c+2 in
+    flight) vs the unfused chain (bf16): ragged T, residual; the split-wait form is bitwise equal
+    to the plain one (same arithmetic, other waits) and both are deterministic."""
+    from hv_amd import ManifoldHyperConnection, _lib, ops
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    g = torch.Generator().manual_seed(T + D)
+    x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
+    res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
+    v = _lib.MV_SPLIT256 if D == 256 else 0
+    with torch.no_grad():
+        with run_options(mhc_variant=v):
+            ops.launch_counts(reset=True)
+            y1 = m.forward_tokens(x, residual=res).float().cpu()
+            assert ops.launch_counts()["mhc_fused"] == 1
+            y1b = m.forward_tokens(x, residual=res).float().cpu()
+        with run_options(mhc_variant=v | _lib.MV_SPLITW):
+            y2 = m.forward_tokens(x, residual=res).float().cpu()
+        with run_options(use_fused_mhc=False):
+            y0 = m.forward_tokens(x, residual=res).float().cpu()
+    assert torch.equal(y1, y1b)
+    assert torch.equal(y1, y2)
+    assert rel_l2(y1.numpy(), y0.numpy()) < 1e-2 and (y1 - y0).abs().max() < 0.1
+
+
 # ------------------------------------------------------------------------------ call-site surface (§8b)
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_attention_cross_mask_weights_match_reference(gpu_device, precision):
