@@ -65,6 +65,14 @@ __device__ inline int find_entry(const E* t, int count, int b) {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// XCD-local workgroup order: the hardware deals consecutive workgroups round-robin over the 8
+// XCDs; this bijection gives each XCD a CONTIGUOUS range of logical block indices, so
+// neighbouring tiles (which share operand rows) run on one XCD and meet in its L2
+__device__ __forceinline__ int xcd_local(int bid, int G) {
+  const int xcd = bid & 7, q = G >> 3, r = G & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 // ------------------------------------------------------------------ phase 1
 __global__ void __launch_bounds__(256) k_pg1(const hv_mhc_prep_entry* __restrict__ tab, int count) {
   __shared__ float red[2][4][PT];
@@ -285,11 +293,15 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
 template <typename T>
 __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict__ tab, int count) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 144];
-  const int ei = find_entry<hv_mhc_prep_entry, 2>(tab, count, blockIdx.x);
+  // the fold tiles of one 64-row block of W1 (one per 64 columns of D) are consecutive logical
+  // blocks: on one XCD they read those W1 rows from HBM once (W1 is the dominant operand, 390 MB
+  // per forward over all sites; dealt round-robin it was re-fetched by every XCD's L2)
+  const int bx = xcd_local(blockIdx.x, gridDim.x);
+  const int ei = find_entry<hv_mhc_prep_entry, 2>(tab, count, bx);
   const hv_mhc_prep_entry& e = tab[ei];
   const PrepSizes s = prep_sizes(e.D, e.Hd, e.fold);
   const Scratch sc = carve(e);
-  const int b = blockIdx.x - e.blk[2];
+  const int b = bx - e.blk[2];
   if (b < s.fold) {
     fold_tile<T>(e, sc, b, lds);
     return;
@@ -336,14 +348,20 @@ __device__ __forceinline__ void wp_cast(const hv_wprep_entry& e, int b) {
   T* y = (T*)e.dst;
   const bool vec = ((((uintptr_t)e.src) | ((uintptr_t)e.dst)) & 15) == 0;
   if (vec && end - base == WP_CAST_CHUNK) {
+    // 8 elements per thread and pass: two 16-byte loads, one 16-byte bf16 store (the scalar
+    // 2-byte stores this replaced held the cast pass near half the HBM rate); all loads first
 #pragma unroll
-    for (int q = 0; q < WP_CAST_CHUNK / 1024; ++q) {
-      const long i = base + (q * 256 + threadIdx.x) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(e.src + i);
-      Elem<T>::store(y, i, v.x);
-      Elem<T>::store(y, i + 1, v.y);
-      Elem<T>::store(y, i + 2, v.z);
-      Elem<T>::store(y, i + 3, v.w);
+    for (int q = 0; q < WP_CAST_CHUNK / 2048; ++q) {
+      const long i = base + (q * 256 + threadIdx.x) * 8;
+      const float4 v0 = *reinterpret_cast<const float4*>(e.src + i);
+      const float4 v1 = *reinterpret_cast<const float4*>(e.src + i + 4);
+      if constexpr (std::is_same<T, unsigned short>::value) {
+        *reinterpret_cast<uint4*>(y + i) = make_uint4(pack_bf16x2(v0.x, v0.y), pack_bf16x2(v0.z, v0.w),
+                                                      pack_bf16x2(v1.x, v1.y), pack_bf16x2(v1.z, v1.w));
+      } else {
+        *reinterpret_cast<float4*>(y + i) = v0;
+        *reinterpret_cast<float4*>(y + i + 4) = v1;
+      }
     }
   } else {
     for (long i = base + threadIdx.x; i < end; i += 256) Elem<T>::store(y, i, e.src[i]);
