@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--no-large", dest="large", action="store_false",
                     help="skip the 1024² legs (config D)")
     ap.add_argument("--large-batch", type=int, default=8)
+    ap.add_argument("--no-pmc", dest="pmc", action="store_false",
+                    help="skip the live rocprofv3 PMC passes (roofline traffic + mfma_busy) at N=1")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercise the launcher, rendezvous and the one-line report (CPU tests)")
     return ap.parse_args()
@@ -153,22 +156,36 @@ class GemmTimer:
         return n, ms / n, fl / n, fl / (ms * 1e-3) / 1e12, by / n
 
 
-def cpu_baseline(model_cpu_sd, size, threads):
-    """Oracle (CPU restatement of the reference path) on the host cores: a bounded sample."""
+def pmc_child(a):
+    """The workload of a live PMC pass (tools/pmc_live.py): two eager forwards of the bench's
+    model and batch (the second with every weight and plan prepared), nothing printed."""
+    from hv_amd import HybridVisionSystem
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = HybridVisionSystem({"image_size": a.size, "precision": a.precision, "verbose": False}).to(dev).eval()
+    x = torch.randn(a.batch, 3, a.size, a.size, device=dev)
+    with torch.no_grad():
+        for _ in range(2):
+            model(x)
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(model_cpu_sd, size, threads, batch=16):
+    """Oracle (CPU restatement of the reference path) on the host cores: a bounded sample of the
+    SAME workload as the GPU line -- one batch of `batch` images (config B: 16) -- after a
+    single-image warmup."""
     from oracle import hv_oracle as O
     torch.set_num_threads(threads)
-    x = torch.randn(1, 3, size, size, generator=torch.Generator().manual_seed(1))
+    x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(1))
     with torch.no_grad():
-        O.system_forward(model_cpu_sd, x, O.BASE)          # warmup
+        O.system_forward(model_cpu_sd, x[:1], O.BASE)      # warmup
         t0 = time.perf_counter()
-        n = 0
-        while n < 3 or (time.perf_counter() - t0 < 10 and n < 8):
-            O.system_forward(model_cpu_sd, x, O.BASE)
-            n += 1
+        O.system_forward(model_cpu_sd, x, O.BASE)
         dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} single-image {size}x{size} fp32 forwards of the oracle (oracle/hv_oracle.py), "
-                      f"same random-init weights, after 1 warmup"}
+    return {"value": round(batch / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"one batch of {batch} {size}x{size} images (config B's batch), fp32 forward of the "
+                      f"oracle (oracle/hv_oracle.py), same random-init weights, after a 1-image warmup; "
+                      f"{dt:.1f} s"}
 
 
 def _sync_time(world, dev, fn):
@@ -304,6 +321,20 @@ def main():
         sys.exit(launch_ranks(a.gpus))
     if a.dry_run:
         return dry_run(a, world, rank)
+    if a.pmc_child:
+        return pmc_child(a)
+    pmc = None
+    if a.pmc and world == 1 and a.size == 640 and a.batch == 16 and a.precision == "bf16":
+        # live PMC passes of this workload, as child processes BEFORE this process touches the GPU
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        try:
+            import pmc_live
+            pmc = pmc_live.collect([os.path.abspath(__file__), "--pmc-child", "--size", str(a.size), "--batch",
+                                    str(a.batch), "--precision", a.precision],
+                                   os.path.join(ROOT, "gpurun_out", "pmc_live"))
+        except Exception as e:                   # noqa: BLE001  (fall back to the committed record)
+            sys.stderr.write(f"live PMC passes failed: {e!r}\n")
+            pmc = None
     torch.cuda.set_device(local)                 # the device first: RCCL binds the rank to it
     dev = torch.device("cuda", local)
     if world > 1:
@@ -342,13 +373,21 @@ def main():
     with torch.no_grad(), GemmTimer(ops) as gt:
         model(x)
     n_l, avg_ms, avg_flop, gemm_tflops, avg_bytes = gt.summary()
-    traffic = None
-    # newest round's PMC record (rocprofv3 passes of this workload on this build's kernels)
-    tf = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r03", "r02", "r01"))
-               if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"))
-    if a.size == 640 and a.batch == 16 and a.precision == "bf16" and os.path.exists(tf):
-        with open(tf) as f:
-            traffic = json.load(f).get("gemm", {}).get("bytes_per_launch")
+    traffic, mfma_busy = None, None
+    traffic_source = None
+    if pmc is not None:
+        traffic, mfma_busy = pmc["bytes_per_launch"], pmc["mfma_busy"]
+        traffic_source = ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE "
+                          "passes run by this bench invocation on this workload (FETCH x2 x1KiB gfx950 correction, "
+                          f"WRITE x1KiB; {pmc['launches_per_pass']} GEMM-family dispatches per pass)")
+    else:
+        # newest round's PMC record (rocprofv3 passes of this workload on this build's kernels)
+        tf = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r04", "r03", "r02"))
+                   if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"))
+        if a.size == 640 and a.batch == 16 and a.precision == "bf16" and os.path.exists(tf):
+            with open(tf) as f:
+                traffic = json.load(f).get("gemm", {}).get("bytes_per_launch")
+            traffic_source = f"committed record {os.path.relpath(tf, ROOT)} (live PMC passes not run)"
     del runner
 
     lat = None
@@ -429,8 +468,8 @@ def main():
                          "achieved": round(gemm_tflops, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gemm_tflops / BF16_PEAK_TFLOPS, 4),
                          "traffic": round(traffic) if traffic else None,
-                         "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload "
-                                           f"(FETCH x2 gfx950 correction), {os.path.relpath(tf, ROOT)}",
+                         "traffic_source": traffic_source,
+                         "mfma_busy": round(mfma_busy, 4) if mfma_busy is not None else None,
                          "algorithmic_bytes_per_launch": round(avg_bytes),
                          "launches_per_step": n_l, "avg_launch_ms": round(avg_ms, 4),
                          "avg_flop_per_launch": avg_flop},

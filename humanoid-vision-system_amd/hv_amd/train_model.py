@@ -304,6 +304,12 @@ def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection"
         out["detections"] = dets
         if compute_loss and targets is not None:
             out["loss"] = yolo_loss(head.loss_fn, logits, targets, head.num_anchors)
+            w = float(getattr(model, "hv_manifold_weight", 0.0))
+            if w > 0:
+                # the reference trainer's total (mhc_trainer.py:248-255): det + manifold_weight * reg
+                reg = manifold_regularization(H)
+                out["loss"]["manifold_loss"] = reg.detach()
+                out["loss"]["total_loss"] = out["loss"]["total_loss"] + w * reg
     out["final_features"] = final_features(model, fused, H)
     bbv = {k: to_nchw_view(v) for k, v in bb.items() if k != "raw_features"}
     bbv["raw_features"] = {k: to_nchw_view(v) for k, v in bb["raw_features"].items()}
@@ -311,6 +317,24 @@ def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection"
     out["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
     flush_stability()              # this forward's monitored sites: one grouped eigensolve
     return out
+
+
+def manifold_regularization(H: Dict[int, torch.Tensor]) -> torch.Tensor:
+    """ManifoldConstrainedTrainer._compute_manifold_regularization (mhc_trainer.py:299-340), as
+    intended (the committed call passes kwargs SinkhornKnoppProjection does not take):
+    over every mHC site, with H = SK(H_res_raw) -- here the SAME differentiable projections the
+    forward used (the grouped Sinkhorn), so the gradient flows through its grouped backward --
+    mean|rowsum(H) - 1| + mean|colsum(H) - 1| + 0.1 mean relu(eigvalsh(H) - 1), averaged over the
+    sites.  eigvalsh reads H's lower triangle as torch.linalg.eigvalsh does (the reference calls it
+    on the unsymmetrised projection)."""
+    terms = []
+    for h in H.values():
+        h2 = h if h.dim() == 2 else h.reshape(h.shape[-2], h.shape[-1])
+        row = (h2.sum(1) - 1.0).abs().mean()
+        col = (h2.sum(0) - 1.0).abs().mean()
+        ev = torch.linalg.eigvalsh(h2)
+        terms.append(row + col + 0.1 * F.relu(ev - 1.0).mean())
+    return torch.stack(terms).mean()
 
 
 class _PredViewFn(torch.autograd.Function):

@@ -427,8 +427,15 @@ class HVTrainer:
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_grad_norm: float = 1.0, mhc_max_norm: float = 0.5, bucket_mb: int = 64,
-                 broadcast_buffers: bool = True, group=None, monitor_every: int = 50, graph: bool = False):
+                 broadcast_buffers: bool = True, group=None, monitor_every: int = 50, graph: bool = False,
+                 manifold_weight: float = 0.0):
         self.model = model
+        # the reference trainer's manifold regularisation term (mhc_trainer.py:248-255,299-340;
+        # its default weight 0.01): off by default -- the committed reference never runs it (D10)
+        if manifold_weight > 0:
+            if graph:
+                raise ValueError("manifold_weight > 0 (torch.linalg.eigvalsh) is not graph-capturable; use graph=False")
+            model.hv_manifold_weight = float(manifold_weight)
         # _monitor_stability (eigvalsh of every H_res, signal ratios) is metrics-only: run it
         # every `monitor_every` steps instead of every forward (0 disables it)
         from .manifold import ManifoldHyperConnection

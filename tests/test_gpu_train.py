@@ -1018,3 +1018,44 @@ def test_dropout_seed_offset_word(gpu_device):
     for i, (u, w) in enumerate(zip(with_off, plain)):
         assert torch.equal(u, w), i
     assert not torch.equal(with_off[3], other[3])
+
+
+def test_trainer_manifold_regularization_matches_reference_formula(gpu_device):
+    """HVTrainer(manifold_weight=w): total_loss = detection + w * reg with the reference trainer's
+    regulariser (mhc_trainer.py:248-255,299-340): mean over the mHC sites of mean|rowsum(H)-1| +
+    mean|colsum(H)-1| + 0.1 mean relu(eigvalsh(H)-1), H = SK(H_res_raw).  The value equals the
+    formula evaluated in fp64 on the oracle's Sinkhorn of every site, and the gradient the term
+    adds to an H_res_raw (through the grouped Sinkhorn backward) equals fp64 autograd of it."""
+    import torch.nn.functional as Fn
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.train_model import manifold_regularization  # noqa: F401  (the product function)
+    from oracle import hv_oracle as O
+    B, S, w = 2, 64, 0.5
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1)).to(gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=3)]
+    res = {}
+    for weight in (0.0, w):
+        m, _ = _tiny_model(gpu_device)
+        m.hv_manifold_weight = weight
+        out = m(x, targets=tg, compute_loss=True)
+        out["loss"]["total_loss"].backward()
+        torch.cuda.synchronize()
+        res[weight] = (m, {k: float(v) for k, v in out["loss"].items() if torch.is_tensor(v) and v.numel() == 1})
+    m0, l0 = res[0.0]
+    m1, l1 = res[w]
+    mods = [mm for mm in m1.modules() if hasattr(mm, "H_res_raw")]
+    raws = [mm.H_res_raw.detach().double().cpu().requires_grad_(True) for mm in mods]
+    terms = []
+    for mm, r in zip(mods, raws):
+        h = O.sinkhorn(r, mm.sinkhorn.num_iterations)
+        terms.append((h.sum(1) - 1).abs().mean() + (h.sum(0) - 1).abs().mean() +
+                     0.1 * Fn.relu(torch.linalg.eigvalsh(h) - 1).mean())
+    reg = torch.stack(terms).mean()
+    reg.backward()
+    assert abs(l1["manifold_loss"] / reg.item() - 1) < 1e-4, (l1["manifold_loss"], reg.item())
+    assert abs((l1["total_loss"] - l0["total_loss"]) - w * reg.item()) < 1e-4 * max(1.0, abs(l0["total_loss"]))
+    named0, named1 = dict(m0.named_parameters()), dict(m1.named_parameters())
+    for (n, p1), r in zip([(n, p) for n, p in m1.named_parameters() if n.endswith("H_res_raw")], raws):
+        extra = (p1.grad - named0[n].grad).double().cpu()
+        ref = w * r.grad
+        assert (extra - ref).norm() <= 1e-3 * ref.norm() + 1e-9, n

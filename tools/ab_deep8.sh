@@ -11,8 +11,8 @@ cat $OUT/sg_probe.txt
 for i in 1 2; do
   HV_LIB_PATH=$GRAFT_REPO_ROOT/abl/libhvs_head.so timeout -k 10 120 python tools/quick_bench.py head >> $OUT/ab.txt 2>&1 || exit 1
   timeout -k 10 120 python tools/quick_bench.py new >> $OUT/ab.txt 2>&1 || exit 1
-  HV_LIB_PATH=$GRAFT_REPO_ROOT/abl/libhvs_head.so timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-train --no-stream --no-large --steps 5 > $OUT/lat_head_$i.json 2>> $OUT/lat.err || exit 1
-  timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-train --no-stream --no-large --steps 5 > $OUT/lat_new_$i.json 2>> $OUT/lat.err || exit 1
+  HV_LIB_PATH=$GRAFT_REPO_ROOT/abl/libhvs_head.so timeout -k 10 200 python -u bench.py --no-pmc --no-cpu-baseline --no-train --no-stream --no-large --steps 5 > $OUT/lat_head_$i.json 2>> $OUT/lat.err || exit 1
+  timeout -k 10 200 python -u bench.py --no-pmc --no-cpu-baseline --no-train --no-stream --no-large --steps 5 > $OUT/lat_new_$i.json 2>> $OUT/lat.err || exit 1
   python -c "import json,sys; [print(f, json.load(open(f))['latency']) for f in sys.argv[1:]]" $OUT/lat_head_$i.json $OUT/lat_new_$i.json
 done
 grep -v amdgpu.ids $OUT/ab.txt

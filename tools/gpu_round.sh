@@ -11,18 +11,18 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; } ; tail -3 $OUT/tests.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; } ; tail -2 $OUT/smoke.log ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
-    benchq) timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
-    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-stream --no-large --steps 20 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; } ; f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/prof_summary.txt; head -25 $OUT/prof_summary.txt ;;
-    profinf) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profinf -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 20 > $OUT/profinf.log 2>&1 || { tail -30 $OUT/profinf.log; exit 1; } ; f=$(find $OUT/profinf -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/profinf_summary.txt; head -25 $OUT/profinf_summary.txt ;;
+    benchq) timeout -k 10 300 python -u bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large --steps 20 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; } ; f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/prof_summary.txt; head -25 $OUT/prof_summary.txt ;;
+    profinf) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profinf -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 20 > $OUT/profinf.log 2>&1 || { tail -30 $OUT/profinf.log; exit 1; } ; f=$(find $OUT/profinf -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/profinf_summary.txt; head -25 $OUT/profinf_summary.txt ;;
     breakdown) timeout -k 10 300 python -u tools/gemm_breakdown.py > $OUT/gemm_breakdown.txt 2>&1 || { tail -30 $OUT/gemm_breakdown.txt; exit 1; } ; head -50 $OUT/gemm_breakdown.txt ;;
-    pmc) for c in FETCH_SIZE WRITE_SIZE; do timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { tail -30 $OUT/pmc_$c.log; exit 1; } ; done ; python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_traffic.json ;;
+    pmc) for c in FETCH_SIZE WRITE_SIZE; do timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { tail -30 $OUT/pmc_$c.log; exit 1; } ; done ; python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_traffic.json ;;
     mfma) timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
           i=0
           for set in "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
                      "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE"; do
             i=$((i+1)); cs=""
             for c in $set; do if grep -qw "$c" $OUT/counters.txt; then cs="$cs $c"; else echo "counter $c not listed"; fi; done
-            timeout -s KILL 240 rocprofv3 --pmc $cs -d $OUT/mfma_p$i -o run --output-format csv -- python bench.py --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/mfma_p$i.log 2>&1 || { tail -30 $OUT/mfma_p$i.log; exit 1; }
+            timeout -s KILL 240 rocprofv3 --pmc $cs -d $OUT/mfma_p$i -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/mfma_p$i.log 2>&1 || { tail -30 $OUT/mfma_p$i.log; exit 1; }
           done
           python tools/pmc_mfma.py $OUT/pmc_mfma.json $OUT/mfma_p1 $OUT/mfma_p2 > $OUT/pmc_mfma.txt; head -50 $OUT/pmc_mfma.txt ;;
     latprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/latprof -o run --output-format csv -- python tools/lat_prof.py > $OUT/latprof.log 2>&1 || { tail -30 $OUT/latprof.log; exit 1; } ; f=$(find $OUT/latprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 1 40 > $OUT/latprof_summary.txt; head -25 $OUT/latprof_summary.txt ;;
