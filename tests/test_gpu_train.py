@@ -1021,15 +1021,41 @@ def test_dropout_seed_offset_word(gpu_device):
 
 
 def test_trainer_manifold_regularization_matches_reference_formula(gpu_device):
-    """HVTrainer(manifold_weight=w): total_loss = detection + w * reg with the reference trainer's
-    regulariser (mhc_trainer.py:248-255,299-340): mean over the mHC sites of mean|rowsum(H)-1| +
-    mean|colsum(H)-1| + 0.1 mean relu(eigvalsh(H)-1), H = SK(H_res_raw).  The value equals the
-    formula evaluated in fp64 on the oracle's Sinkhorn of every site, and the gradient the term
-    adds to an H_res_raw (through the grouped Sinkhorn backward) equals fp64 autograd of it."""
+    """HVTrainer(manifold_weight=w) / model.hv_manifold_weight: total_loss = detection + w * reg
+    with the reference trainer's regulariser (mhc_trainer.py:248-255,299-340): mean over the mHC
+    sites of mean|rowsum(H)-1| + mean|colsum(H)-1| + 0.1 mean relu(eigvalsh(H)-1), H =
+    SK(H_res_raw).
+      * the formula (hv_amd.train_model.manifold_regularization) on matrices FAR from doubly
+        stochastic (so rounding does not decide the |.| signs), value and gradient, vs fp64 autograd
+        of the reference expression on the CPU;
+      * in the model: the reported manifold_loss equals the formula on the oracle's fp64 Sinkhorn of
+        every site up to fp32 rounding of the row / column sums (the projections are column-exact:
+        the term is ~1e-5, at the rounding level of a 1792-element fp32 sum), total_loss -
+        detection == w * manifold_loss, and the term adds a finite, nonzero gradient to the
+        H_res_raw parameters only."""
     import torch.nn.functional as Fn
     from hv_amd.targets import synthetic_targets
-    from hv_amd.train_model import manifold_regularization  # noqa: F401  (the product function)
+    from hv_amd.train_model import manifold_regularization
     from oracle import hv_oracle as O
+
+    def ref_formula(hs):
+        terms = [(h.sum(1) - 1).abs().mean() + (h.sum(0) - 1).abs().mean() +
+                 0.1 * Fn.relu(torch.linalg.eigvalsh(h) - 1).mean() for h in hs]
+        return torch.stack(terms).mean()
+
+    g = torch.Generator().manual_seed(4)
+    hs = [(torch.rand(n, n, generator=g) * 2.5 / n).double() for n in (8, 32, 100)]
+    hs[1] = hs[1] + torch.eye(32, dtype=torch.float64) * 0.8          # eigenvalues above 1 too
+    mine = [h.float().to(gpu_device).requires_grad_(True) for h in hs]
+    val = manifold_regularization({i: h for i, h in enumerate(mine)})
+    val.backward()
+    refs = [h.clone().requires_grad_(True) for h in hs]
+    rv = ref_formula(refs)
+    rv.backward()
+    assert abs(val.item() / rv.item() - 1) < 1e-5
+    for a, b in zip(mine, refs):
+        assert (a.grad.double().cpu() - b.grad).norm() <= 1e-5 * b.grad.norm()
+
     B, S, w = 2, 64, 0.5
     x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1)).to(gpu_device)
     tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=3)]
@@ -1043,19 +1069,19 @@ def test_trainer_manifold_regularization_matches_reference_formula(gpu_device):
         res[weight] = (m, {k: float(v) for k, v in out["loss"].items() if torch.is_tensor(v) and v.numel() == 1})
     m0, l0 = res[0.0]
     m1, l1 = res[w]
-    mods = [mm for mm in m1.modules() if hasattr(mm, "H_res_raw")]
-    raws = [mm.H_res_raw.detach().double().cpu().requires_grad_(True) for mm in mods]
-    terms = []
-    for mm, r in zip(mods, raws):
-        h = O.sinkhorn(r, mm.sinkhorn.num_iterations)
-        terms.append((h.sum(1) - 1).abs().mean() + (h.sum(0) - 1).abs().mean() +
-                     0.1 * Fn.relu(torch.linalg.eigvalsh(h) - 1).mean())
-    reg = torch.stack(terms).mean()
-    reg.backward()
-    assert abs(l1["manifold_loss"] / reg.item() - 1) < 1e-4, (l1["manifold_loss"], reg.item())
-    assert abs((l1["total_loss"] - l0["total_loss"]) - w * reg.item()) < 1e-4 * max(1.0, abs(l0["total_loss"]))
-    named0, named1 = dict(m0.named_parameters()), dict(m1.named_parameters())
-    for (n, p1), r in zip([(n, p) for n, p in m1.named_parameters() if n.endswith("H_res_raw")], raws):
-        extra = (p1.grad - named0[n].grad).double().cpu()
-        ref = w * r.grad
-        assert (extra - ref).norm() <= 1e-3 * ref.norm() + 1e-9, n
+    with torch.no_grad():
+        hs = [O.sinkhorn(mm.H_res_raw.detach().double().cpu(), mm.sinkhorn.num_iterations)
+              for mm in m1.modules() if hasattr(mm, "H_res_raw")]
+        reg = ref_formula(hs).item()
+    assert abs(l1["manifold_loss"] - reg) < 5e-7, (l1["manifold_loss"], reg)
+    assert abs((l1["total_loss"] - l0["total_loss"]) - w * l1["manifold_loss"]) < 1e-5 * max(1.0, abs(l0["total_loss"]))
+    named0 = dict(m0.named_parameters())
+    moved = 0
+    for n, p1 in m1.named_parameters():
+        extra = p1.grad - named0[n].grad
+        assert torch.isfinite(extra).all(), n
+        if n.endswith("H_res_raw"):
+            moved += int(extra.abs().max().item() > 0)
+        else:
+            assert extra.abs().max().item() <= 1e-6 * max(1.0, named0[n].grad.abs().max().item()), n
+    assert moved > 0
