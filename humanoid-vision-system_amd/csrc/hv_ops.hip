@@ -467,15 +467,28 @@ __global__ void __launch_bounds__(256) k_chan_final(const float* part, int n, in
     out[(long)b * c + ch] = ((red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192])) * inv;
 }
 
-// SE gate MLP (vision_backbone.py:77-83): one block per image.
+// The pooled mean of channel ch of image b straight from k_chan_partial's chunk sums, in
+// k_chan_final's exact order (lane q = chunks q, q+4, ...; lanes combined pairwise), so the SE
+// gate computed from the partials is bitwise the gate of hv_channel_mean -> hv_se_mlp2.
+__device__ __forceinline__ float pooled_from_part(const float* part, int b, int nchunk, int c, int ch, float inv) {
+  float r[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* pp = part + (long)b * nchunk * c + ch;
+  for (int k = 0; k < nchunk; ++k) r[k & 3] += pp[(long)k * c];
+  return ((r[0] + r[1]) + (r[2] + r[3])) * inv;
+}
+
+// SE gate MLP (vision_backbone.py:77-83): one block per image.  PART: `pooled` is the
+// [n, nchunk, c] chunk-sum buffer of k_chan_partial (the mean is finished here: one launch fewer).
+template <bool PART>
 __global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int cr, const float* w1,
                                                 const float* b1, const float* w2, const float* b2,
-                                                float* gate) {
+                                                float* gate, int nchunk, float inv) {
   extern __shared__ float sh[];
   float* p = sh;           // [c]
   float* h = sh + c;       // [cr]
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < c; i += blockDim.x) p[i] = pooled[(long)b * c + i];
+  for (int i = threadIdx.x; i < c; i += blockDim.x)
+    p[i] = PART ? pooled_from_part(pooled, b, nchunk, c, i, inv) : pooled[(long)b * c + i];
   __syncthreads();
   for (int o = threadIdx.x; o < cr; o += blockDim.x) {
     float s = b1[o];
@@ -495,10 +508,10 @@ __global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int 
 // one wave per hidden unit o, lanes across the input channels (coalesced weight-row reads), the
 // dots of up to NB images accumulated together and reduced by xor shuffles; stage 2 the same per
 // output channel over the hidden vector.  Fixed summation order: deterministic.
-template <int NB, int ACT>
+template <int NB, int ACT, bool PART = false>
 __global__ void __launch_bounds__(256) k_se_fc(const float* __restrict__ in, int n, int k, int nout,
                                                const float* __restrict__ w, const float* __restrict__ bias,
-                                               float* __restrict__ out) {
+                                               float* __restrict__ out, int nchunk = 0, float inv = 0.f) {
   const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int b0 = blockIdx.y * NB;
   if (o >= nout) return;
@@ -510,7 +523,8 @@ __global__ void __launch_bounds__(256) k_se_fc(const float* __restrict__ in, int
     const float wv = wr[i];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
-      if (b0 + j < n) acc[j] += wv * in[(long)(b0 + j) * k + i];
+      if (b0 + j < n)
+        acc[j] += wv * (PART ? pooled_from_part(in, b0 + j, nchunk, k, i, inv) : in[(long)(b0 + j) * k + i]);
   }
 #pragma unroll
   for (int j = 0; j < NB; ++j) acc[j] = wave_sum(acc[j]);
@@ -1013,7 +1027,37 @@ extern "C" int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float
       k_se_fc<4, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
     }
   } else {
-    k_se_mlp<<<n, 256, (c + cr) * sizeof(float), s>>>(pooled, c, cr, w1, b1, w2, b2, gate);
+    k_se_mlp<false><<<n, 256, (c + cr) * sizeof(float), s>>>(pooled, c, cr, w1, b1, w2, b2, gate, 0, 0.f);
+  }
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+// Whole SE gate of an NHWC map (vision_backbone.py:77-83, the channel_attention call of
+// ConvMHCLayer.forward): chunk sums of the pool, then the MLP finishing the mean from them.
+// Bitwise equal to hv_channel_mean followed by hv_se_mlp2 with the same `hidden` choice.
+extern "C" int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr, const float* w1,
+                          const float* b1, const float* w2, const float* b2, float* work, float* hidden,
+                          float* gate, hv_stream_t stream) {
+  if (n <= 0 || hw <= 0 || c <= 0 || cr <= 0 || !work || !gate) return HV_EINVAL;
+  const int vec = dtype == HV_BF16 ? 8 : 4;
+  if (c % vec || c / vec > 256 || ((uintptr_t)x & 15)) return HV_EINVAL;
+  const int rows = cm_rows_per_chunk(c, vec);
+  const int nchunk = (hw + rows - 1) / rows;
+  const float inv = 1.0f / hw;
+  hipStream_t s = (hipStream_t)stream;
+  HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(nchunk, n), 256, 0, s>>>((const T*)x, hw, c, nchunk, work)));
+  if (n <= 4 && hidden) {
+    if (n == 1) {
+      k_se_fc<1, 0, true><<<hv_cdiv(cr, 4), 256, 0, s>>>(work, n, c, cr, w1, b1, hidden, nchunk, inv);
+      k_se_fc<1, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
+    } else {
+      k_se_fc<4, 0, true><<<dim3(hv_cdiv(cr, 4), hv_cdiv(n, 4)), 256, 0, s>>>(work, n, c, cr, w1, b1, hidden,
+                                                                              nchunk, inv);
+      k_se_fc<4, 1><<<dim3(hv_cdiv(c, 4), hv_cdiv(n, 4)), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
+    }
+  } else {
+    k_se_mlp<true><<<n, 256, (c + cr) * sizeof(float), s>>>(work, c, cr, w1, b1, w2, b2, gate, nchunk, inv);
   }
   HV_CHECK_LAUNCH();
   return HV_OK;

@@ -171,6 +171,7 @@ _SIGS = {
     "hv_channel_mean": ([i32, vp, i32, i32, i32, vp, vp, vp], i32),
     "hv_se_mlp": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),
     "hv_se_mlp2": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp], i32),
+    "hv_se_gate": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_scale_residual": ([i32, vp, vp, vp, i32, i32, i32, vp, vp], i32),
     "hv_upsample_add": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp], i32),
     "hv_add_scaled": ([i32, vp, vp, i64, f32, vp, vp], i32),

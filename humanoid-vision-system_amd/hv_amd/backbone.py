@@ -81,7 +81,7 @@ class ConvMHCLayer(nn.Module):
             y = self.mhc.forward_tokens(y.view(-1, c)).view(n, h, w, c)
             if self.channel_attention is not None:
                 ca = self.channel_attention
-                gate = ops.se_mlp(ops.channel_mean(y), ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
+                gate = ops.se_gate(y, ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
                 y = ops.scale_residual(y, gate, x if self.use_residual else None)
                 if extra_residual is not None:
                     y = ops.add_scaled(y, extra_residual, 1.0)
@@ -97,7 +97,7 @@ class ConvMHCLayer(nn.Module):
         n, h, w, c = y.shape
         y = self.mhc.forward_tokens(y.view(-1, c)).view(n, h, w, c)
         ca = self.channel_attention
-        gate = ops.se_mlp(ops.channel_mean(y), ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
+        gate = ops.se_gate(y, ca[1].weight, ca[1].bias, ca[3].weight, ca[3].bias)
         return ops.maxpool2x2(y, gate) if pool else ops.scale_residual(y, gate, None)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

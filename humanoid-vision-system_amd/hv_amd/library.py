@@ -194,8 +194,7 @@ def _(x, weight, bias, bn_weight, bn_bias, bn_mean, bn_var, stride=1, padding=0,
 @torch.library.custom_op("hv::se_gate", mutates_args=(), device_types="cuda")
 def se_gate(y: Tensor, identity: Optional[Tensor], w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor) -> Tensor:
     """y * sigmoid(W2 silu(W1 mean_hw(y) + b1) + b2) (+ identity); y NHWC."""
-    pooled = ops.channel_mean(y.contiguous())
-    gate = ops.se_mlp(pooled, w1.reshape(w1.shape[0], -1), b1, w2.reshape(w2.shape[0], -1), b2)
+    gate = ops.se_gate(y.contiguous(), w1.reshape(w1.shape[0], -1), b1, w2.reshape(w2.shape[0], -1), b2)
     return ops.scale_residual(y.contiguous(), gate, None if identity is None else identity.contiguous())
 
 

@@ -546,6 +546,23 @@ def se_mlp(pooled: Tensor, w1, b1, w2, b2) -> Tensor:
     return gate
 
 
+def se_gate(x: Tensor, w1, b1, w2, b2) -> Tensor:
+    """SE gate fp32 [n, c] of an NHWC map in one call (hv_se_gate): bitwise
+    se_mlp(channel_mean(x), ...) with one launch fewer."""
+    _contig(x, "x")
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    cr = w1.shape[0]
+    w1, b1, w2, b2 = map(f32, (w1, b1, w2, b2))
+    gate = torch.empty((n, c), device=x.device, dtype=torch.float32)
+    work = torch.empty(L.lib().hv_channel_mean_work_floats(n, hw, c), device=x.device, dtype=torch.float32)
+    hidden = torch.empty((n, cr), device=x.device, dtype=torch.float32) if n <= 4 else None
+    check(L.lib().hv_se_gate(dtype_code(x.dtype), x.data_ptr(), n, hw, c, cr, w1.data_ptr(), b1.data_ptr(),
+                             w2.data_ptr(), b2.data_ptr(), work.data_ptr(), ptr(hidden), gate.data_ptr(),
+                             stream_ptr()), "hv_se_gate")
+    return gate
+
+
 def scale_residual(x: Tensor, gate: Tensor, identity: Optional[Tensor]) -> Tensor:
     _contig(x, "x")
     n, c = x.shape[0], x.shape[-1]
@@ -942,7 +959,7 @@ def _install_sync_check():
         return
     mod = sys.modules[__name__]
     for name in ("gemm", "conv2d", "conv_weight_prep", "bn_fold", "cast", "row_stats", "layernorm", "rmsnorm",
-                 "sinkhorn", "mhc_prep", "nchw_to_nhwc", "maxpool2x2", "channel_mean", "se_mlp",
+                 "sinkhorn", "mhc_prep", "nchw_to_nhwc", "maxpool2x2", "channel_mean", "se_mlp", "se_gate",
                  "scale_residual", "upsample_add", "add_scaled", "add_rowvec", "interp_linear", "vit_tokens",
                  "attention", "gather_rows", "yolo_decode"):
         fn = getattr(mod, name)

@@ -348,6 +348,11 @@ int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const 
  * workgroups (one wave per output unit, coalesced weight rows) instead of one workgroup per image */
 int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
                const float* w2, const float* b2, float* hidden, float* gate, hv_stream_t stream);
+/* whole SE gate of an NHWC map: pool chunk sums then the MLP, which finishes the mean itself
+ * (one launch fewer than hv_channel_mean + hv_se_mlp2; bitwise equal to that pair with the same
+ * `hidden`).  work: hv_channel_mean_work_floats(n, hw, c) floats.  (vision_backbone.py:77-83) */
+int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr, const float* w1, const float* b1,
+               const float* w2, const float* b2, float* work, float* hidden, float* gate, hv_stream_t stream);
 /* y = x * gate[n, c] (+ identity)  (vision_backbone.py:126-132) */
 int hv_scale_residual(int dtype, const void* x, const float* gate, const void* identity,
                       int n, int hw, int c, void* y, hv_stream_t stream);
