@@ -467,11 +467,125 @@ __device__ __forceinline__ void epi_writeout_v(const hv_gemm_desc& d, int r0, in
   }
 }
 
+// Mode-2 (gradient) write-out with the aux rows loaded ONE PASS AHEAD (opt-in HV_GV_TRAIN_PF):
+// the aux load of pass p+1 is issued before the stores of pass p, so it is not queued behind
+// them (vmcnt retires in issue order) -- one extra 8-value row in registers instead of the
+// per-pass store round trip, and not the all-pass preload that spilled.  Same arithmetic and
+// order as epi_train8 + epi_writeout_v: bitwise equal.
+template <int BN, int NT, int SLAB, int RES>
+__device__ __forceinline__ void epi_writeout_m2pf(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
+  const bool c_bf = d.c_dtype == HV_BF16, a_bf = d.aux_dtype == HV_BF16;
+  constexpr int TPR = BN / 8, RPP = NT / TPR, NP = SLAB / RPP;
+  const int c8 = (threadIdx.x % TPR) * 8;
+  const int col = n0 + c8;
+  const bool vcol = col + 8 <= d.N;
+  const bool av = vcol && (d.ld_aux & 7) == 0 && ((((uintptr_t)d.aux) & 15) == 0);
+  const uint32_t sd_ = epi_seed(d);
+  auto aux_row = [&](int p, float (&z)[8]) {
+    const int row = min(r0 + p * RPP + (int)threadIdx.x / TPR, d.M - 1);
+    const long ai = (long)row * d.ld_aux + col;
+    if (av && a_bf) {
+      const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
+      const unsigned tw[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        z[2 * q] = __uint_as_float(tw[q] << 16);
+        z[2 * q + 1] = __uint_as_float(tw[q] & 0xffff0000u);
+      }
+    } else if (av) {
+      const float4 t0 = *reinterpret_cast<const float4*>((const float*)d.aux + ai);
+      const float4 t1 = *reinterpret_cast<const float4*>((const float*)d.aux + ai + 4);
+      z[0] = t0.x; z[1] = t0.y; z[2] = t0.z; z[3] = t0.w; z[4] = t1.x; z[5] = t1.y; z[6] = t1.z; z[7] = t1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        z[j] = col + j < d.N ? (a_bf ? bf2f(((const unsigned short*)d.aux)[ai + j]) : ((const float*)d.aux)[ai + j])
+                             : 0.f;
+    }
+  };
+  uint4 rb[RES == 1 ? NP : 1];
+  float4 rf[RES == 2 ? NP : 1][2];
+  if constexpr (RES != 0) {
+    if (vcol) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int row = min(r0 + p * RPP + (int)threadIdx.x / TPR, d.M - 1);
+        const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
+        if constexpr (RES == 1) {
+          rb[p] = *reinterpret_cast<const uint4*>((const unsigned short*)d.residual + rrow * d.ldr + col);
+        } else {
+          rf[p][0] = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col);
+          rf[p][1] = *reinterpret_cast<const float4*>((const float*)d.residual + rrow * d.ldr + col + 4);
+        }
+      }
+    }
+  }
+  float za[8], zb[8];
+  aux_row(0, za);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    float (&z)[8] = (p & 1) ? zb : za;
+    float (&zn)[8] = (p & 1) ? za : zb;
+    if (p + 1 < NP) aux_row(p + 1, zn);
+    const int lr = p * RPP + threadIdx.x / TPR;
+    const int row = r0 + lr;
+    if (row >= d.M || col >= d.N) continue;
+    const float4 lo = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4), hi = *epi_lds_chunk<BN / 4>(smem, lr, c8 / 4 + 1);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const unsigned long long idx0 = (unsigned long long)row * d.N + col;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+    if (vcol) {
+      if constexpr (RES == 1) {
+        const unsigned rw[4] = {rb[p].x, rb[p].y, rb[p].z, rb[p].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] += __uint_as_float(rw[q] << 16);
+          v[2 * q + 1] += __uint_as_float(rw[q] & 0xffff0000u);
+        }
+      } else if constexpr (RES == 2) {
+        v[0] += rf[p][0].x; v[1] += rf[p][0].y; v[2] += rf[p][0].z; v[3] += rf[p][0].w;
+        v[4] += rf[p][1].x; v[5] += rf[p][1].y; v[6] += rf[p][1].z; v[7] += rf[p][1].w;
+      }
+      if (c_bf) {
+        *reinterpret_cast<uint4*>((unsigned short*)d.C + (long)row * d.ldc + col) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+      } else {
+        float* o = (float*)d.C + (long)row * d.ldc + col;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+      const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (col + j >= d.N) break;
+        float x = v[j];
+        if (RES != 0)
+          x += d.r_dtype == HV_BF16 ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
+                                    : ((const float*)d.residual)[rrow * d.ldr + col + j];
+        const long o = (long)row * d.ldc + col + j;
+        if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
+        else ((float*)d.C)[o] = x;
+      }
+    }
+  }
+}
+
 template <int BN, int NT, int SLAB, bool TRAIN = false>
 __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int n0, unsigned char* smem) {
   const bool vec = (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
                    (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
   // coalesced write-out: thread -> (row, 8 columns); the vector path needs aligned C / residual
+  if constexpr (TRAIN) {
+    if (vec && d.epi_mode == 2 && (d.variant & HV_GV_TRAIN_PF)) {
+      if (!d.residual) epi_writeout_m2pf<BN, NT, SLAB, 0>(d, r0, n0, smem);
+      else if (d.r_dtype == HV_BF16) epi_writeout_m2pf<BN, NT, SLAB, 1>(d, r0, n0, smem);
+      else epi_writeout_m2pf<BN, NT, SLAB, 2>(d, r0, n0, smem);
+      return;
+    }
+  }
   if (!vec) epi_writeout_s<BN, NT, SLAB, TRAIN>(d, r0, n0, smem);
   else if (!d.residual) epi_writeout_v<BN, NT, SLAB, TRAIN, 0>(d, r0, n0, smem);
   else if (d.r_dtype == HV_BF16) epi_writeout_v<BN, NT, SLAB, TRAIN, 1>(d, r0, n0, smem);

@@ -508,10 +508,10 @@ __global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int 
 // one wave per hidden unit o, lanes across the input channels (coalesced weight-row reads), the
 // dots of up to NB images accumulated together and reduced by xor shuffles; stage 2 the same per
 // output channel over the hidden vector.  Fixed summation order: deterministic.
-template <int NB, int ACT, bool PART = false>
+template <int NB, int ACT>
 __global__ void __launch_bounds__(256) k_se_fc(const float* __restrict__ in, int n, int k, int nout,
                                                const float* __restrict__ w, const float* __restrict__ bias,
-                                               float* __restrict__ out, int nchunk = 0, float inv = 0.f) {
+                                               float* __restrict__ out) {
   const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int b0 = blockIdx.y * NB;
   if (o >= nout) return;
@@ -523,8 +523,7 @@ __global__ void __launch_bounds__(256) k_se_fc(const float* __restrict__ in, int
     const float wv = wr[i];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
-      if (b0 + j < n)
-        acc[j] += wv * (PART ? pooled_from_part(in, b0 + j, nchunk, k, i, inv) : in[(long)(b0 + j) * k + i]);
+      if (b0 + j < n) acc[j] += wv * in[(long)(b0 + j) * k + i];
   }
 #pragma unroll
   for (int j = 0; j < NB; ++j) acc[j] = wave_sum(acc[j]);
@@ -1034,8 +1033,9 @@ extern "C" int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float
 }
 
 // Whole SE gate of an NHWC map (vision_backbone.py:77-83, the channel_attention call of
-// ConvMHCLayer.forward): chunk sums of the pool, then the MLP finishing the mean from them.
-// Bitwise equal to hv_channel_mean followed by hv_se_mlp2 with the same `hidden` choice.
+// ConvMHCLayer.forward): chunk sums of the pool, then (n > 4) the per-image MLP finishing the mean
+// from them -- one launch fewer -- or (n <= 4) the final reduce + the batched MLP.  Bitwise equal
+// to hv_channel_mean followed by hv_se_mlp2 with the same `hidden` choice.
 extern "C" int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr, const float* w1,
                           const float* b1, const float* w2, const float* b2, float* work, float* hidden,
                           float* gate, hv_stream_t stream) {
@@ -1048,13 +1048,16 @@ extern "C" int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr
   hipStream_t s = (hipStream_t)stream;
   HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(nchunk, n), 256, 0, s>>>((const T*)x, hw, c, nchunk, work)));
   if (n <= 4 && hidden) {
+    // batched MLP: every hidden-unit wave needs the whole pooled vector, so the mean is finished
+    // once (into `gate`, free until the second stage writes it) -- finishing it per wave from the
+    // chunk sums cost ~(c / 64) * nchunk dependent L2 loads per lane
+    k_chan_final<<<dim3(hv_cdiv(c, 64), n), 256, 0, s>>>(work, n, nchunk, c, inv, gate);
     if (n == 1) {
-      k_se_fc<1, 0, true><<<hv_cdiv(cr, 4), 256, 0, s>>>(work, n, c, cr, w1, b1, hidden, nchunk, inv);
+      k_se_fc<1, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(gate, n, c, cr, w1, b1, hidden);
       k_se_fc<1, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
     } else {
-      k_se_fc<4, 0, true><<<dim3(hv_cdiv(cr, 4), hv_cdiv(n, 4)), 256, 0, s>>>(work, n, c, cr, w1, b1, hidden,
-                                                                              nchunk, inv);
-      k_se_fc<4, 1><<<dim3(hv_cdiv(c, 4), hv_cdiv(n, 4)), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
+      k_se_fc<4, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(gate, n, c, cr, w1, b1, hidden);
+      k_se_fc<4, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
     }
   } else {
     k_se_mlp<true><<<n, 256, (c + cr) * sizeof(float), s>>>(work, c, cr, w1, b1, w2, b2, gate, nchunk, inv);

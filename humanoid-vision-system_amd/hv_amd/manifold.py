@@ -145,7 +145,8 @@ def build_plan(m: "ManifoldHyperConnection", h_res: torch.Tensor, dtype: torch.d
 
 def mhc_apply(x2: torch.Tensor, p: MhcPlan, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token chain on x2 [T, D] (compute dtype).  Returns LN_post(...) (+ residual) [T, D]."""
-    if (options().use_fused_mhc and p.fold and x2.is_contiguous() and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype)
+    if (options().use_fused_mhc and p.fold and x2.is_contiguous()
+            and ops.mhc_fused_supported(p.D, p.Hd, x2.dtype, T=x2.shape[0])
             and (residual is None or residual.dtype == x2.dtype)):
         return ops.mhc_fused(x2, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post, residual)
     mean, rstd = ops.row_stats(x2, 1e-5)

@@ -277,8 +277,23 @@ def f32(t: Optional[Tensor]) -> Optional[Tensor]:
     return None if t is None else t.detach().float().contiguous()
 
 
-def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype, variant: Optional[int] = None) -> bool:
-    v = options().mhc_variant if variant is None else variant
+def _mhc_variant(D: int, T: Optional[int], variant: Optional[int]) -> int:
+    """D = 256 sites take the split-hidden fused kernel (HV_MV_SPLIT256) automatically only from
+    HVOptions.mhc256_min_tokens tokens: one 64-token group per workgroup, so small grids leave CUs
+    idle and the unfused chain (the ViT's grouped q / k / v GEMM1) wins -- per launch 0.421 vs
+    0.482 ms at T = 102,400, 0.124 vs 0.138 at 25,600, equal at 6,416 / 401; in-model with EVERY
+    D = 256 site fused: B=16 19.90 vs 19.18 ms, B=1 9.0 vs 7.05 ms (profiles/r04/mhc256_ab.txt)."""
+    o = options()
+    v = o.mhc_variant if variant is None else variant
+    if v == 0 and D == 256 and T is not None and T >= o.mhc256_min_tokens:
+        v = L.MV_SPLIT256
+    return v
+
+
+def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype, variant: Optional[int] = None,
+                        T: Optional[int] = None) -> bool:
+    """T: the site's token count (None = the token-count-independent answer)."""
+    v = _mhc_variant(D, T, variant)
     return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype), v))
 
 
@@ -298,7 +313,7 @@ def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optiona
     out = torch.empty_like(x)
     a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
                        b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), ptr(residual),
-                       out.data_ptr(), options().mhc_variant if variant is None else variant, 0)
+                       out.data_ptr(), _mhc_variant(D, T, variant), 0)
     check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
     return out
 
@@ -548,7 +563,9 @@ def se_mlp(pooled: Tensor, w1, b1, w2, b2) -> Tensor:
 
 def se_gate(x: Tensor, w1, b1, w2, b2) -> Tensor:
     """SE gate fp32 [n, c] of an NHWC map in one call (hv_se_gate): bitwise
-    se_mlp(channel_mean(x), ...) with one launch fewer."""
+    se_mlp(channel_mean(x), ...) with one launch fewer (HVOptions.fused_se_gate=False: that pair)."""
+    if not options().fused_se_gate:
+        return se_mlp(channel_mean(x), w1, b1, w2, b2)
     _contig(x, "x")
     n, c = x.shape[0], x.shape[-1]
     hw = x.numel() // (n * c)

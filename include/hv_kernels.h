@@ -172,6 +172,7 @@ typedef struct hv_gemm_desc {
                                       (measured +1.2 % train-step time at B=16, so opt-in) */
 #define HV_GV_DEEP8        0x40000 /* 64x64 tiles on the 8-stage ring (inference epilogues; measured no gain) */
 #define HV_GV_NO_DEEP8     0x80000 /* (kept for the A/B tools: the 8-stage ring is never automatic) */
+#define HV_GV_TRAIN_PF     0x100000 /* gradient epilogue (epi_mode 2) loads its aux rows one pass ahead of the stores */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;

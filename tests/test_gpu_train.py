@@ -969,14 +969,17 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
     from conftest import gemm_variant
     # staged (default) / fragment-layout epilogue, and the 256x256 ping-pong kernel with the
     # training epilogues (GV_TILE_256 forces it; the automatic choice takes it for long K and wide N)
-    for key, v in (("staged", 0), ("flat", _lib.GV_FLAT_TRAIN), ("pp256", _lib.GV_TILE_256)):
+    # ("pf": the gradient epilogue loading its aux rows one pass ahead, HV_GV_TRAIN_PF)
+    for key, v in (("staged", 0), ("flat", _lib.GV_FLAT_TRAIN), ("pp256", _lib.GV_TILE_256),
+                   ("pf", _lib.GV_TRAIN_PF)):
         if key == "pp256" and K % 64:
             continue
         with gemm_variant(v):
             pre = torch.empty(M, N, device=gpu_device, dtype=torch.bfloat16)
             y = T.gemm_train(a, b, mode=1, act=act, aux=pre, bias=bias, drop_p=0.2, seed=5, **kw)
             dpre = T.gemm_train(a, b, mode=2, act=act, aux=pre, drop_p=0.2, seed=5, residual=res)
-            outs[key] = (pre, y, dpre)
+            dpre0 = T.gemm_train(a, b, mode=2, act=act, aux=pre, drop_p=0.2, seed=5)
+            outs[key] = (pre, y, dpre, dpre0)
     for key in outs:
         for x0, x1 in zip(outs["staged"], outs[key]):
             assert torch.equal(x0, x1), key

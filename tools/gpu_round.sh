@@ -25,7 +25,7 @@ for step in "$@"; do
             timeout -s KILL 240 rocprofv3 --pmc $cs -d $OUT/mfma_p$i -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/mfma_p$i.log 2>&1 || { tail -30 $OUT/mfma_p$i.log; exit 1; }
           done
           python tools/pmc_mfma.py $OUT/pmc_mfma.json $OUT/mfma_p1 $OUT/mfma_p2 > $OUT/pmc_mfma.txt; head -50 $OUT/pmc_mfma.txt ;;
-    latprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/latprof -o run --output-format csv -- python tools/lat_prof.py > $OUT/latprof.log 2>&1 || { tail -30 $OUT/latprof.log; exit 1; } ; f=$(find $OUT/latprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 1 40 > $OUT/latprof_summary.txt; head -25 $OUT/latprof_summary.txt ;;
+    latprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/latprof -o run --output-format csv -- python tools/lat_prof.py > $OUT/latprof.log 2>&1 || { tail -30 $OUT/latprof.log; exit 1; } ; f=$(find $OUT/latprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 1 40 > $OUT/latprof_summary.txt; python tools/frame_kernels.py $OUT/latprof > $OUT/latprof_frame.txt; head -25 $OUT/latprof_frame.txt ;;
     trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trainprof -o run --output-format csv -- python tools/train_diag.py time 16 640 > $OUT/trainprof.log 2>&1 || { tail -30 $OUT/trainprof.log; exit 1; } ; f=$(find $OUT/trainprof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 6 45 > $OUT/trainprof_summary.txt; head -30 $OUT/trainprof_summary.txt ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
