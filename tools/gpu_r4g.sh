@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r4g; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_train.py -q --timeout 200 --timeout-method thread -k "se_ or staged_epilogue or seed_offset" > $OUT/tests_k.log 2>&1 || { tail -30 $OUT/tests_k.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_train.py tests/test_gpu_prep.py -q --timeout 200 --timeout-method thread -k "se_ or staged_epilogue or seed_offset or prep" > $OUT/tests_k.log 2>&1 || { tail -30 $OUT/tests_k.log; exit 1; }
 tail -2 $OUT/tests_k.log
 timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -q --timeout 200 --timeout-method thread > $OUT/tests_model.log 2>&1 || { tail -30 $OUT/tests_model.log; exit 1; }
 tail -2 $OUT/tests_model.log
@@ -20,3 +20,4 @@ for r in 1 2; do
   HV_GEMM_VARIANT=0x100000 timeout -k 10 300 python -u tools/train_diag.py time 16 640 > $OUT/train_pf_$r.txt 2>&1 || { tail -20 $OUT/train_pf_$r.txt; exit 1; }
   tail -1 $OUT/train_pf_$r.txt
 done
+bash tools/gpu_round.sh r4g profinf || exit 1
