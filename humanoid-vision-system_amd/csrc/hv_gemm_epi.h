@@ -467,7 +467,9 @@ __device__ __forceinline__ void epi_writeout_v(const hv_gemm_desc& d, int r0, in
   }
 }
 
-// Mode-2 (gradient) write-out with the aux rows loaded ONE PASS AHEAD (opt-in HV_GV_TRAIN_PF):
+// Mode-2 (gradient) write-out with the aux rows loaded ONE PASS AHEAD (default; HV_GV_TRAIN_NOPF
+// selects the per-pass form below -- base-640 B=16 training step 146.1 / 146.7 vs 148.6 / 149.2 ms
+// alternating, profiles/r04/train_pf_ab.txt):
 // the aux load of pass p+1 is issued before the stores of pass p, so it is not queued behind
 // them (vmcnt retires in issue order) -- one extra 8-value row in registers instead of the
 // per-pass store round trip, and not the all-pass preload that spilled.  Same arithmetic and
@@ -579,7 +581,7 @@ __device__ __forceinline__ void epi_writeout(const hv_gemm_desc& d, int r0, int 
                    (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
   // coalesced write-out: thread -> (row, 8 columns); the vector path needs aligned C / residual
   if constexpr (TRAIN) {
-    if (vec && d.epi_mode == 2 && (d.variant & HV_GV_TRAIN_PF)) {
+    if (vec && d.epi_mode == 2 && !(d.variant & HV_GV_TRAIN_NOPF)) {
       if (!d.residual) epi_writeout_m2pf<BN, NT, SLAB, 0>(d, r0, n0, smem);
       else if (d.r_dtype == HV_BF16) epi_writeout_m2pf<BN, NT, SLAB, 1>(d, r0, n0, smem);
       else epi_writeout_m2pf<BN, NT, SLAB, 2>(d, r0, n0, smem);

@@ -467,28 +467,16 @@ __global__ void __launch_bounds__(256) k_chan_final(const float* part, int n, in
     out[(long)b * c + ch] = ((red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192])) * inv;
 }
 
-// The pooled mean of channel ch of image b straight from k_chan_partial's chunk sums, in
-// k_chan_final's exact order (lane q = chunks q, q+4, ...; lanes combined pairwise), so the SE
-// gate computed from the partials is bitwise the gate of hv_channel_mean -> hv_se_mlp2.
-__device__ __forceinline__ float pooled_from_part(const float* part, int b, int nchunk, int c, int ch, float inv) {
-  float r[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* pp = part + (long)b * nchunk * c + ch;
-  for (int k = 0; k < nchunk; ++k) r[k & 3] += pp[(long)k * c];
-  return ((r[0] + r[1]) + (r[2] + r[3])) * inv;
-}
-
-// SE gate MLP (vision_backbone.py:77-83): one block per image.  PART: `pooled` is the
-// [n, nchunk, c] chunk-sum buffer of k_chan_partial (the mean is finished here: one launch fewer).
-template <bool PART>
+// SE gate MLP (vision_backbone.py:77-83): one block per image.  The block reads its pooled row
+// into LDS before writing its gate row, so `pooled` may alias `gate` (hv_se_gate).
 __global__ void __launch_bounds__(256) k_se_mlp(const float* pooled, int c, int cr, const float* w1,
                                                 const float* b1, const float* w2, const float* b2,
-                                                float* gate, int nchunk, float inv) {
+                                                float* gate) {
   extern __shared__ float sh[];
   float* p = sh;           // [c]
   float* h = sh + c;       // [cr]
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < c; i += blockDim.x)
-    p[i] = PART ? pooled_from_part(pooled, b, nchunk, c, i, inv) : pooled[(long)b * c + i];
+  for (int i = threadIdx.x; i < c; i += blockDim.x) p[i] = pooled[(long)b * c + i];
   __syncthreads();
   for (int o = threadIdx.x; o < cr; o += blockDim.x) {
     float s = b1[o];
@@ -1026,44 +1014,25 @@ extern "C" int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float
       k_se_fc<4, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
     }
   } else {
-    k_se_mlp<false><<<n, 256, (c + cr) * sizeof(float), s>>>(pooled, c, cr, w1, b1, w2, b2, gate, 0, 0.f);
+    k_se_mlp<<<n, 256, (c + cr) * sizeof(float), s>>>(pooled, c, cr, w1, b1, w2, b2, gate);
   }
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
 
-// Whole SE gate of an NHWC map (vision_backbone.py:77-83, the channel_attention call of
-// ConvMHCLayer.forward): chunk sums of the pool, then (n > 4) the per-image MLP finishing the mean
-// from them -- one launch fewer -- or (n <= 4) the final reduce + the batched MLP.  Bitwise equal
-// to hv_channel_mean followed by hv_se_mlp2 with the same `hidden` choice.
+// Whole SE gate of an NHWC map in one call (vision_backbone.py:77-83, the channel_attention call
+// of ConvMHCLayer.forward): chunk sums, the fixed-order final reduce into `gate` (used as the
+// pooled buffer), then the MLP in place -- the launches of hv_channel_mean + hv_se_mlp2, bitwise
+// equal to that pair.  (Finishing the mean inside the per-image MLP saved the reduce launch but
+// walked nchunk partials per channel serially: 24.5 vs 9.8 + 6.6 us per site, slower in-model,
+// profiles/r04/se_gate_fused_mean_rejected.txt.)
 extern "C" int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr, const float* w1,
                           const float* b1, const float* w2, const float* b2, float* work, float* hidden,
                           float* gate, hv_stream_t stream) {
   if (n <= 0 || hw <= 0 || c <= 0 || cr <= 0 || !work || !gate) return HV_EINVAL;
-  const int vec = dtype == HV_BF16 ? 8 : 4;
-  if (c % vec || c / vec > 256 || ((uintptr_t)x & 15)) return HV_EINVAL;
-  const int rows = cm_rows_per_chunk(c, vec);
-  const int nchunk = (hw + rows - 1) / rows;
-  const float inv = 1.0f / hw;
-  hipStream_t s = (hipStream_t)stream;
-  HV_DISPATCH(dtype, (k_chan_partial<T><<<dim3(nchunk, n), 256, 0, s>>>((const T*)x, hw, c, nchunk, work)));
-  if (n <= 4 && hidden) {
-    // batched MLP: every hidden-unit wave needs the whole pooled vector, so the mean is finished
-    // once (into `gate`, free until the second stage writes it) -- finishing it per wave from the
-    // chunk sums cost ~(c / 64) * nchunk dependent L2 loads per lane
-    k_chan_final<<<dim3(hv_cdiv(c, 64), n), 256, 0, s>>>(work, n, nchunk, c, inv, gate);
-    if (n == 1) {
-      k_se_fc<1, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(gate, n, c, cr, w1, b1, hidden);
-      k_se_fc<1, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
-    } else {
-      k_se_fc<4, 0><<<hv_cdiv(cr, 4), 256, 0, s>>>(gate, n, c, cr, w1, b1, hidden);
-      k_se_fc<4, 1><<<hv_cdiv(c, 4), 256, 0, s>>>(hidden, n, cr, c, w2, b2, gate);
-    }
-  } else {
-    k_se_mlp<true><<<n, 256, (c + cr) * sizeof(float), s>>>(work, c, cr, w1, b1, w2, b2, gate, nchunk, inv);
-  }
-  HV_CHECK_LAUNCH();
-  return HV_OK;
+  const int rc = hv_channel_mean(dtype, x, n, hw, c, gate, work, stream);
+  if (rc != HV_OK) return rc;
+  return hv_se_mlp2(gate, n, c, cr, w1, b1, w2, b2, hidden, gate, stream);
 }
 
 extern "C" int hv_scale_residual(int dtype, const void* x, const float* gate, const void* identity,

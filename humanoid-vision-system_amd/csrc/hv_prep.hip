@@ -292,10 +292,12 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
 
 // bf16 fold tile with 128-deep k-steps (K = Hd % 128 == 0: every site).  The 32-deep form above
 // is a chain of K/32 dependent global-load round trips per tile (4 MFMAs per wave between them:
-// 0.08 MFMA busy, 408 us per forward); here each thread keeps 2 x 32 fp32 values of the NEXT
-// k-step in flight (16 x 16-B loads), so a tile waits K/128 round trips.  Same k order and fp32
-// accumulation per output as one bf16 MFMA chain over k = 0..K-1: bitwise equal to the 32-deep
-// form (each 16x16x32 MFMA adds one 32-deep chunk in k order either way).
+// 0.08 MFMA busy, 408 us per forward); here each thread keeps 2 x 8 x 16 B of the NEXT k-step in
+// flight, so a tile waits K/128 round trips.  Load mapping: piece p = j * 256 + t of the
+// 64 rows x 32 16-B pieces of a k-step is (row p / 32, piece p % 32), so every load instruction
+// of a wave reads two whole 512-B row segments (a mapping with 128 contiguous bytes per lane
+// touched 64 cache lines per instruction and ran 6x slower).  Same k order and fp32 accumulation
+// per output as one bf16 MFMA chain over k = 0..K-1, like the 32-deep form.
 constexpr int FK = 128;
 constexpr int FRB = FK * 2 + 16;          // LDS row bytes: 128 bf16 + 16 B pad (conflict-free b128 reads)
 __device__ __forceinline__ void fold_tile_bf128(const hv_mhc_prep_entry& e, const Scratch& sc, int tile, char* lds) {
@@ -305,10 +307,12 @@ __device__ __forceinline__ void fold_tile_bf128(const hv_mhc_prep_entry& e, cons
   char* As = lds;
   char* Bs = lds + 64 * FRB;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int lr = t >> 2, lq = (t & 3) * 32;
-  const float* Ar = e.w1 + (long)(m0 + lr) * K + lq;
-  const bool bvalid = n0 + lr < D;
-  const float* Br = sc.gc + (long)(bvalid ? n0 + lr : 0) * K + lq;
+  const int pr = t >> 5, pc = (t & 31) * 4;         // row (+ 8 j) and k offset of this thread's pieces
+  const float* Ar = e.w1 + (long)(m0 + pr) * K + pc;
+  const float* Br = sc.gc + (long)(n0 + pr) * K + pc;
+  bool bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bv[j] = n0 + pr + 8 * j < D;
   f32x4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -317,26 +321,24 @@ __device__ __forceinline__ void fold_tile_bf128(const hv_mhc_prep_entry& e, cons
   float4 na[8], nb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    na[j] = *reinterpret_cast<const float4*>(Ar + 4 * j);
-    nb[j] = bvalid ? *reinterpret_cast<const float4*>(Br + 4 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    na[j] = *reinterpret_cast<const float4*>(Ar + (long)8 * j * K);
+    nb[j] = bv[j] ? *reinterpret_cast<const float4*>(Br + (long)8 * j * K) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const int fr = lane & 15, fg = lane >> 4;
   for (int k0 = 0; k0 < K; k0 += FK) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 a0 = na[2 * j], a1 = na[2 * j + 1], b0 = nb[2 * j], b1 = nb[2 * j + 1];
-      const u16x8 pa = {f2bf(a0.x), f2bf(a0.y), f2bf(a0.z), f2bf(a0.w), f2bf(a1.x), f2bf(a1.y), f2bf(a1.z), f2bf(a1.w)};
-      const u16x8 pb = {f2bf(b0.x), f2bf(b0.y), f2bf(b0.z), f2bf(b0.w), f2bf(b1.x), f2bf(b1.y), f2bf(b1.z), f2bf(b1.w)};
-      *reinterpret_cast<u16x8*>(As + lr * FRB + (lq + 8 * j) * 2) = pa;
-      *reinterpret_cast<u16x8*>(Bs + lr * FRB + (lq + 8 * j) * 2) = pb;
+    for (int j = 0; j < 8; ++j) {
+      const int off = (pr + 8 * j) * FRB + pc * 2;
+      *reinterpret_cast<uint2*>(As + off) = make_uint2(pack_bf16x2(na[j].x, na[j].y), pack_bf16x2(na[j].z, na[j].w));
+      *reinterpret_cast<uint2*>(Bs + off) = make_uint2(pack_bf16x2(nb[j].x, nb[j].y), pack_bf16x2(nb[j].z, nb[j].w));
     }
     __syncthreads();
     if (k0 + FK < K) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        na[j] = *reinterpret_cast<const float4*>(Ar + k0 + FK + 4 * j);
-        if (bvalid) nb[j] = *reinterpret_cast<const float4*>(Br + k0 + FK + 4 * j);
+        na[j] = *reinterpret_cast<const float4*>(Ar + (long)8 * j * K + k0 + FK);
+        if (bv[j]) nb[j] = *reinterpret_cast<const float4*>(Br + (long)8 * j * K + k0 + FK);
       }
     }
 #pragma unroll

@@ -21,7 +21,7 @@ GV_REGSTAGE, GV_NO_BIG, GV_BIG_ALWAYS, GV_NO_SMALL = 0x8, 0x10, 0x20, 0x40
 GV_TRAIN128, GV_FLAT_EPI, GV_FLAT_TRAIN, GV_SHALLOW = 0x80, 0x100, 0x200, 0x400
 GV_CONV_KTAIL, GV_NO_SMALLK, GV_SK_DIAG1, GV_SK_DIAG2 = 0x800, 0x1000, 0x2000, 0x4000
 GV_SK_RES3, GV_SK_RES4, GV_TRAIN_BIG, GV_DEEP8, GV_NO_DEEP8 = 0x8000, 0x10000, 0x20000, 0x40000, 0x80000
-GV_TRAIN_PF = 0x100000
+GV_TRAIN_NOPF = 0x100000
 MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_SHIFT = 1, 2, 5, 6, 0x100, 16
 MV_SPLIT256, MV_SPLITW = 0x200, 12
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10

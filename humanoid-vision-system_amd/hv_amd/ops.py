@@ -563,9 +563,7 @@ def se_mlp(pooled: Tensor, w1, b1, w2, b2) -> Tensor:
 
 def se_gate(x: Tensor, w1, b1, w2, b2) -> Tensor:
     """SE gate fp32 [n, c] of an NHWC map in one call (hv_se_gate): bitwise
-    se_mlp(channel_mean(x), ...) with one launch fewer (HVOptions.fused_se_gate=False: that pair)."""
-    if not options().fused_se_gate:
-        return se_mlp(channel_mean(x), w1, b1, w2, b2)
+    se_mlp(channel_mean(x), ...)."""
     _contig(x, "x")
     n, c = x.shape[0], x.shape[-1]
     hw = x.numel() // (n * c)

@@ -39,7 +39,6 @@ class HVOptions:
     splitk: bool = False              # split-K for small output grids: measured no gain
     gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
-    fused_se_gate: bool = True        # SE gate as hv_se_gate (pool + MLP, one launch fewer)
     mhc256_min_tokens: int = 25600    # D = 256 sites fused (split-hidden) from this many tokens (ops._mhc_variant)
 
     def replace(self, **kw) -> "HVOptions":

@@ -172,7 +172,8 @@ typedef struct hv_gemm_desc {
                                       (measured +1.2 % train-step time at B=16, so opt-in) */
 #define HV_GV_DEEP8        0x40000 /* 64x64 tiles on the 8-stage ring (inference epilogues; measured no gain) */
 #define HV_GV_NO_DEEP8     0x80000 /* (kept for the A/B tools: the 8-stage ring is never automatic) */
-#define HV_GV_TRAIN_PF     0x100000 /* gradient epilogue (epi_mode 2) loads its aux rows one pass ahead of the stores */
+#define HV_GV_TRAIN_NOPF   0x100000 /* gradient epilogue (epi_mode 2) loads each pass's aux rows after the previous
+                                      pass's stores (the pre-round-4 form; default: one pass ahead) */
 int hv_gemm(const hv_gemm_desc* d, hv_stream_t stream);
 /* ------------------------------------------------------------------------------------
  * Row statistics / normalisation (manifold_layers.py:250,267 LayerNorm eps 1e-5;
@@ -349,9 +350,9 @@ int hv_se_mlp(const float* pooled, int n, int c, int cr, const float* w1, const 
  * workgroups (one wave per output unit, coalesced weight rows) instead of one workgroup per image */
 int hv_se_mlp2(const float* pooled, int n, int c, int cr, const float* w1, const float* b1,
                const float* w2, const float* b2, float* hidden, float* gate, hv_stream_t stream);
-/* whole SE gate of an NHWC map: pool chunk sums then the MLP, which finishes the mean itself
- * (one launch fewer than hv_channel_mean + hv_se_mlp2; bitwise equal to that pair with the same
- * `hidden`).  work: hv_channel_mean_work_floats(n, hw, c) floats.  (vision_backbone.py:77-83) */
+/* whole SE gate of an NHWC map in one call: hv_channel_mean into `gate`, then hv_se_mlp2 in place
+ * (bitwise equal to that pair).  work: hv_channel_mean_work_floats(n, hw, c) floats; hidden as
+ * hv_se_mlp2.  (vision_backbone.py:77-83) */
 int hv_se_gate(int dtype, const void* x, int n, int hw, int c, int cr, const float* w1, const float* b1,
                const float* w2, const float* b2, float* work, float* hidden, float* gate, hv_stream_t stream);
 /* y = x * gate[n, c] (+ identity)  (vision_backbone.py:126-132) */

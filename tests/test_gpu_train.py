@@ -969,9 +969,10 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
     from conftest import gemm_variant
     # staged (default) / fragment-layout epilogue, and the 256x256 ping-pong kernel with the
     # training epilogues (GV_TILE_256 forces it; the automatic choice takes it for long K and wide N)
-    # ("pf": the gradient epilogue loading its aux rows one pass ahead, HV_GV_TRAIN_PF)
+    # ("nopf": the gradient epilogue loading each pass's aux rows after the previous pass's
+    # stores instead of one pass ahead, HV_GV_TRAIN_NOPF)
     for key, v in (("staged", 0), ("flat", _lib.GV_FLAT_TRAIN), ("pp256", _lib.GV_TILE_256),
-                   ("pf", _lib.GV_TRAIN_PF)):
+                   ("nopf", _lib.GV_TRAIN_NOPF)):
         if key == "pp256" and K % 64:
             continue
         with gemm_variant(v):
