@@ -154,77 +154,58 @@ __global__ void __launch_bounds__(256) k_colred(const ColRed r, int nblk, float*
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[v][c][j] = 0.f;
   if (rsub < rpi) {
-    // U rows per trip: all their loads are issued before any is consumed (the one-load-per-trip
-    // loop ran at load latency); the values are then accumulated in the original row order, so
-    // the sums are bitwise those of the one-row loop
-    constexpr int U = NCH == 1 ? 4 : (NCH == 2 ? 2 : 1);
-    constexpr bool HASB = MODE != CR_SUM && MODE != CR_SUMSQ;
-    const long step = (long)nblk * rpi;
-    for (long r0 = (long)blockIdx.x * rpi; r0 < r.rows; r0 += U * step) {
-      float a[U][NCH][4], b[U][NCH][4];
-      float rmu[U], rrs[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long row = r0 + u * step + rsub;
-        rmu[u] = 0.f;
-        rrs[u] = 1.f;
-        if (row >= r.rows) continue;
-        if constexpr (MODE == CR_ROWN) {
-          rmu[u] = r.mean ? r.mean[row] : 0.f;
-          rrs[u] = r.rstd[row];
-        }
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
-          if (ch >= cpr) continue;
-          const long o = base + row * r.cols + ch * 4;
-          ld4<TA>((const TA*)r.a, o, a[u][c]);
-          if constexpr (HASB) {
-            if (MODE != CR_DOT || r.b) ld4<TB>((const TB*)r.b, o, b[u][c]);
-          }
-        }
+    for (long r0 = (long)blockIdx.x * rpi; r0 < r.rows; r0 += (long)nblk * rpi) {
+      const long row = r0 + rsub;
+      if (row >= r.rows) break;
+      float rmu = 0.f, rrs = 1.f;
+      if constexpr (MODE == CR_ROWN) {
+        rmu = r.mean ? r.mean[row] : 0.f;
+        rrs = r.rstd[row];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long row = r0 + u * step + rsub;
-        if (row >= r.rows) break;
+      for (int c = 0; c < NCH; ++c) {
+        const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
+        if (ch >= cpr) continue;
+        const int col = ch * 4;
+        const long o = base + row * r.cols + col;
+        float a[4];
+        ld4<TA>((const TA*)r.a, o, a);
+        if constexpr (MODE == CR_SUM) {
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
-          if (ch >= cpr) continue;
-          const int col = ch * 4;
-          const long o = base + row * r.cols + col;
-          if constexpr (MODE == CR_SUM) {
+          for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
+        } else if constexpr (MODE == CR_SUMSQ) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j];
-          } else if constexpr (MODE == CR_SUMSQ) {
+          for (int j = 0; j < 4; ++j) { acc[0][c][j] += a[j]; acc[1][c][j] += a[j] * a[j]; }
+        } else if constexpr (MODE == CR_DOT) {
+          if (r.b) {
+            float b[4];
+            ld4<TB>((const TB*)r.b, o, b);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { acc[0][c][j] += a[u][c][j]; acc[1][c][j] += a[u][c][j] * a[u][c][j]; }
-          } else if constexpr (MODE == CR_DOT) {
-            if (r.b) {
+            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j] * b[j];
+          } else {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j] * b[u][c][j];
-            } else {
+            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
+          }
+        } else if constexpr (MODE == CR_BNBWD) {
+          float b[4];
+          ld4<TB>((const TB*)r.b, o, b);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j];
-            }
-          } else if constexpr (MODE == CR_BNBWD) {
+          for (int j = 0; j < 4; ++j) {
+            const int cc = col + j;
+            const float xh = (a[j] - r.mean[cc]) * r.rstd[cc];
+            const float g = b[j] * hv_act_grad(xh * (r.gamma ? r.gamma[cc] : 1.f) + (r.beta ? r.beta[cc] : 0.f), r.act);
+            acc[0][c][j] += g;
+            acc[1][c][j] += g * xh;
+          }
+        } else {  // CR_ROWN
+          float b[4];
+          ld4<TB>((const TB*)r.b, o, b);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int cc = col + j;
-              const float xh = (a[u][c][j] - r.mean[cc]) * r.rstd[cc];
-              const float g = b[u][c][j] * hv_act_grad(xh * (r.gamma ? r.gamma[cc] : 1.f) + (r.beta ? r.beta[cc] : 0.f), r.act);
-              acc[0][c][j] += g;
-              acc[1][c][j] += g * xh;
-            }
-          } else {  // CR_ROWN
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float xh = (a[u][c][j] - rmu[u]) * rrs[u];
-              const float g = b[u][c][j] * hv_drop_scale(hv_seed(r.seed, r.soff), (unsigned long long)(o + j), r.p);
-              acc[0][c][j] += g * xh;
-              acc[1][c][j] += g;
-            }
+          for (int j = 0; j < 4; ++j) {
+            const float xh = (a[j] - rmu) * rrs;
+            const float g = b[j] * hv_drop_scale(hv_seed(r.seed, r.soff), (unsigned long long)(o + j), r.p);
+            acc[0][c][j] += g * xh;
+            acc[1][c][j] += g;
           }
         }
       }
@@ -298,9 +279,7 @@ inline int colred_blocks(long rows, int cols, int imgs) {
   const int cpr = cols / 4;
   const int rpi = cpr <= 256 ? 256 / cpr : 1;
   long b = (rows + (long)rpi * 8 - 1) / ((long)rpi * 8);
-  // up to 1024 workgroups (4 per CU): with U rows of loads in flight per thread that keeps ~4 TB/s
-  // of requests outstanding; 512 left the pass at half that
-  const long cap = imgs > 1 ? (1024 / imgs > 8 ? 1024 / imgs : 8) : 1024;
+  const long cap = imgs > 1 ? (512 / imgs > 8 ? 512 / imgs : 8) : 512;
   b = b > cap ? cap : (b < 1 ? 1 : b);
   return (int)b;
 }
@@ -800,14 +779,18 @@ __global__ void __launch_bounds__(256) k_yolo_loss(const T* __restrict__ lg, con
 
 __global__ void k_yolo_final(const float* part, int nblk, const float* nobj, float lc, float lo, float ln, float lcl,
                              float* sums) {
-  if (threadIdx.x >= 4) return;
+  // lanes 0..3 of the one wave: component sums; the weighted total is formed from the lanes'
+  // registers (shuffles), not by reading back the other lanes' global stores
+  const int t = threadIdx.x;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * 4 + threadIdx.x];
+  if (t < 4)
+    for (int b = 0; b < nblk; ++b) s += part[(long)b * 4 + t];
   const float N = nobj[0];
-  sums[threadIdx.x] = N > 0.f ? s : 0.f;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sums[4] = N > 0.f ? (lc * sums[0] + lo * sums[1] + ln * sums[2] + lcl * sums[3]) / N : 0.f;
+  const float v = N > 0.f ? s : 0.f;
+  const float s0 = __shfl(v, 0), s1 = __shfl(v, 1), s2 = __shfl(v, 2), s3 = __shfl(v, 3);
+  if (t < 4) sums[t] = v;
+  if (t == 0) {
+    sums[4] = N > 0.f ? (lc * s0 + lo * s1 + ln * s2 + lcl * s3) / N : 0.f;
     sums[5] = N;
   }
 }

@@ -16,6 +16,11 @@ for p in (ROOT, PKG):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: full-size model cases")
+    # bisection knob: HV_TEST_GEMM_VARIANT=<HV_GV_* bits> runs every test's default options with
+    # that GEMM variant (training steps included -- they read runtime.DEFAULT_OPTIONS)
+    if os.environ.get("HV_TEST_GEMM_VARIANT"):
+        from hv_amd import runtime
+        runtime.DEFAULT_OPTIONS = runtime.HVOptions(gemm_variant=int(os.environ["HV_TEST_GEMM_VARIANT"], 0))
 
 
 def golden(name: str):
