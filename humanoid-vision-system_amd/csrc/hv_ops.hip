@@ -3,6 +3,8 @@
 // type (float or bf16 bits), arithmetic is fp32.
 #include "hv_common.h"
 
+#include <cstring>
+
 namespace {
 
 using bf = unsigned short;
@@ -1428,6 +1430,31 @@ extern "C" int hv_copy_segments(const hv_copy_segment* segs, int count, hv_strea
     if (cb.count == 0) continue;
     cb.block_start[cb.count] = blocks;
     k_copy_segments<<<(unsigned)blocks, 256, 0, s>>>(cb);
+    HV_CHECK_LAUNCH();
+  }
+  return HV_OK;
+}
+
+// Host bytes -> device through kernel arguments (2 KiB per launch): a captured graph records the
+// bytes by value in its kernel nodes, so a table upload inside a capture needs no pinned staging
+// buffer (pinning new host memory is refused while a stream captures) and nothing to keep alive.
+constexpr int kArgBytes = 2048;
+struct ArgBytes {
+  unsigned int w[kArgBytes / 4];
+};
+__global__ void __launch_bounds__(256) k_write_bytes(const ArgBytes a, int n, unsigned char* dst) {
+  for (int i = threadIdx.x; i < n; i += 256) dst[i] = (unsigned char)(a.w[i >> 2] >> (8 * (i & 3)));
+}
+
+extern "C" int hv_write_bytes(void* dst, const void* src, long long n, hv_stream_t stream) {
+  if (n < 0 || (n > 0 && (!dst || !src))) return HV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  for (long long off = 0; off < n; off += kArgBytes) {
+    const int m = (int)(n - off < kArgBytes ? n - off : kArgBytes);
+    ArgBytes a;
+    memset(&a, 0, sizeof(a));
+    memcpy(&a, (const unsigned char*)src + off, (size_t)m);
+    k_write_bytes<<<1, 256, 0, s>>>(a, m, (unsigned char*)dst + off);
     HV_CHECK_LAUNCH();
   }
   return HV_OK;

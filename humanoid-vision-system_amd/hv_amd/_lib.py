@@ -184,6 +184,7 @@ _SIGS = {
     "hv_attention_mfma": ([vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp], i32),
     "hv_gather_rows": ([i32, vp, i64, i32, i32, vp, vp], i32),
     "hv_copy_segments": ([vp, i32, vp], i32),
+    "hv_write_bytes": ([vp, vp, C.c_longlong, vp], i32),
     "hv_attention_general": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),

@@ -52,17 +52,27 @@ def keep_if_capturing(*objs) -> None:
 
 
 def upload_table(entries, device) -> Tensor:
-    """ctypes struct array -> device bytes, asynchronously (pinned staging + non_blocking copy
-    on the current stream): a table upload never synchronises the host with the GPU, so it can
-    sit inside a training forward/backward without draining the queue (or a graph capture:
-    see capture_keepalive)."""
-    host = torch.frombuffer(bytearray(bytes(entries)), dtype=torch.uint8)
-    if torch.device(device).type == "cuda":
-        host = host.pin_memory()
-    dev = host.to(device, non_blocking=True)
-    if torch.device(device).type == "cuda":
-        keep_if_capturing(host, dev)
-    return dev
+    """ctypes struct array -> device bytes, asynchronously: a table upload never synchronises the
+    host with the GPU, so it can sit inside a training forward/backward without draining the
+    queue.  Outside a capture: pinned staging + non_blocking copy on the current stream.  Inside
+    a graph capture (pinning new host memory is refused there): the bytes travel as kernel
+    arguments (hv_write_bytes), recorded by value in the graph."""
+    return upload_bytes(bytes(entries), device)
+
+
+def upload_bytes(data: bytes, device, dtype: torch.dtype = torch.uint8) -> Tensor:
+    """Host bytes -> a new device tensor of `dtype` (see upload_table)."""
+    host = torch.frombuffer(bytearray(data), dtype=dtype) if data else torch.empty(0, dtype=dtype)
+    if torch.device(device).type != "cuda":
+        return host.to(device)
+    if torch.cuda.is_current_stream_capturing():
+        dev = torch.empty(host.shape, dtype=dtype, device=device)
+        if host.numel():
+            check(L.lib().hv_write_bytes(dev.data_ptr(), host.data_ptr(), host.numel() * host.element_size(),
+                                         stream_ptr()), "hv_write_bytes")
+        return dev
+    host = host.pin_memory()
+    return host.to(device, non_blocking=True)
 
 
 def _contig(t: Tensor, name: str) -> Tensor:

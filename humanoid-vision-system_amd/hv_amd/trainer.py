@@ -244,14 +244,10 @@ class GradBuckets:
         n = len(self.params)
         key = tuple(self._received_local) + tuple(hooked)
         if key != self._flags_key:              # new local flags: one async upload (then cached)
+            from .ops import upload_bytes
             host = torch.tensor([int(r) for r in self._received_local] + [1 - int(h) for h in hooked],
                                 dtype=torch.int32)
-            if self.flat.is_cuda:
-                host = host.pin_memory()
-            self._flags_local = host.to(self.flat.device, non_blocking=True)
-            if self.flat.is_cuda:
-                from .ops import keep_if_capturing
-                keep_if_capturing(host)
+            self._flags_local = upload_bytes(host.numpy().tobytes(), self.flat.device, torch.int32)
             self._flags_key = key
         if self.world > 1:
             flags = self._flags_local.clone()
@@ -333,10 +329,9 @@ class FusedAdamW:
             return active
         key = tuple(bool(a) for a in active) if active is not None else (True,) * len(self.named)
         if self._active_cache[0] != key:
-            host = torch.tensor([int(a) for a in key], dtype=torch.int32).pin_memory()
-            self._active_cache = (key, host.to(self.device, non_blocking=True))
-            from .ops import keep_if_capturing
-            keep_if_capturing(host)
+            from .ops import upload_bytes
+            host = torch.tensor([int(a) for a in key], dtype=torch.int32)
+            self._active_cache = (key, upload_bytes(host.numpy().tobytes(), self.device, torch.int32))
         return self._active_cache[1]
 
     def step(self, clip: bool = True, active=None):
@@ -443,7 +438,17 @@ class HVTrainer:
         self.monitor_every = monitor_every
         self._set_monitor(monitor_every)
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-        self.grads = GradBuckets(named, bucket_mb << 20, group)
+        dev0 = named[0][1].device
+        # ONE stream for every step, eager or captured: the gradient hooks keep each parameter's
+        # AccumulateGrad node alive, and autograd runs that node (with the bucket flush hooked to
+        # it) on the stream that was current when the node was created.  Created on the default
+        # stream, a captured backward (on the capture stream) ran those accumulations and
+        # flushes on the default stream -- outside the graph -- and replays lost them (torch's
+        # "AccumulateGrad node's stream does not match" warning).  Hooks registered, eager steps
+        # run and the graph captured on self.stream: the nodes' stream is the capture stream.
+        self.stream = torch.cuda.Stream(device=dev0) if dev0.type == "cuda" else None
+        with self._on_stream():
+            self.grads = GradBuckets(named, bucket_mb << 20, group)
         self.opt = FusedAdamW(named, lr, weight_decay, betas, eps, (mhc_max_norm, max_grad_norm))
         self.world = self.grads.world
         self.group = group
@@ -461,6 +466,10 @@ class HVTrainer:
         self.replays = 0
         self.captures = 0
         self._g: Optional[Dict] = None
+
+    def _on_stream(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     def _set_monitor(self, every: int, reset: bool = False) -> None:
         for m in self._mhc:
@@ -529,6 +538,9 @@ class HVTrainer:
             self.seed_offset.add_(SEED_STRIDE)         # new dropout masks every step
             self.grads.zero()
             out = self.model(images, targets=targets, compute_loss=True)
+            # detached (a captured step's: refreshed by every replay); holding the attached
+            # outputs would keep this step's autograd graph alive into the next step
+            self.last_predictions = {k: v.detach() for k, v in out.get("predictions", {}).items()}
             loss = out["loss"]
             total = loss["total_loss"]
             (total * (1.0 / self.world) if self.world > 1 else total).backward()
@@ -568,12 +580,27 @@ class HVTrainer:
         # the capturing stream; the device-table uploads inside the step become graph memcpy
         # nodes whose pinned sources `keep` holds for the graph's lifetime
         with ops.capture_keepalive(keep):
-            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            with torch.cuda.graph(graph, stream=self.stream, capture_error_mode="thread_local"):
                 loss = self._body(static_x, static_t)
         self._g = {"graph": graph, "x": static_x, "t": static_t, "loss": loss, "keep": keep, "key": key}
         self.captures += 1
 
     def step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
+        """One training step, issued on the trainer's stream (ordered after the caller's current
+        stream's work, and the caller's stream waits for it before returning)."""
+        if self.stream is None:
+            return self._step(images, targets)
+        cur = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            loss = self._step(images, targets)
+        cur.wait_stream(self.stream)
+        for v in loss.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(cur)
+        return loss
+
+    def _step(self, images: Tensor, targets: List[Tensor]) -> Dict[str, Tensor]:
         self.model.train()
         if self._buf_flats and not self._buffers_still_flat():
             self._buf_flats = self._flatten_buffers()   # re-bind (the ranks do it in lock-step:

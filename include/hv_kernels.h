@@ -406,6 +406,10 @@ typedef struct hv_copy_segment {
   long long bytes;
 } hv_copy_segment;
 int hv_copy_segments(const hv_copy_segment* segs /* host array */, int count, hv_stream_t stream);
+/* n host bytes -> device `dst`, stream-ordered, carried in kernel arguments (2 KiB per launch):
+   usable inside a graph capture, where pinning host memory for an async copy is refused; the
+   host buffer may be reused as soon as the call returns. */
+int hv_write_bytes(void* dst, const void* src, long long n, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * YOLO decode (yolo_head.py:196-201 permute + YOLODecoder.forward :220-294, shims S4/S5).

@@ -703,3 +703,30 @@ def test_gpu_preprocess_pil_bit_exact(gpu_device, case):
     assert torch.equal(out.cpu(), ref)
     nh = ops.preprocess(bgr.to(gpu_device), oh, ow, dtype=torch.bfloat16, nhwc=True, resample="pil")
     assert torch.equal(nh.cpu(), ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("n", [0, 5, 2048, 5000])
+def test_write_bytes_eager_and_captured(gpu_device, n):
+    """hv_write_bytes (ops.upload_bytes inside a capture): host bytes reach the device through
+    kernel arguments, stream-ordered; captured, the graph replays the bytes recorded at capture
+    even after the host buffer is overwritten."""
+    from hv_amd import ops
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    t = ops.upload_bytes(data, gpu_device)
+    torch.cuda.synchronize()
+    assert bytes(t.cpu().numpy().tobytes()) == data
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    buf = bytearray(data)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            tc = ops.upload_bytes(bytes(buf), gpu_device)
+            out = tc.to(torch.int32) + 1
+    for i in range(len(buf)):
+        buf[i] = 0
+    g.replay()
+    torch.cuda.synchronize()
+    assert bytes(tc.cpu().numpy().tobytes()) == data
+    assert torch.equal(out.cpu(), torch.frombuffer(bytearray(data), dtype=torch.uint8).to(torch.int32) + 1) if n else True

@@ -14,6 +14,7 @@ from oracle import weights as W  # noqa: E402
 
 v = int(sys.argv[1], 0) if len(sys.argv) > 1 else 0
 prec = sys.argv[2] if len(sys.argv) > 2 else "bf16"
+me = int(sys.argv[3]) if len(sys.argv) > 3 else 4          # monitor_every of all three trainers
 runtime.DEFAULT_OPTIONS = runtime.HVOptions(gemm_variant=v)
 dev = torch.device("cuda")
 
@@ -29,8 +30,8 @@ def tiny():
 
 
 ms = [tiny(), tiny(), tiny()]
-trs = [HVTrainer(ms[0], lr=1e-3, monitor_every=4), HVTrainer(ms[1], lr=1e-3, monitor_every=4),
-       HVTrainer(ms[2], lr=1e-3, monitor_every=4, graph=True)]
+trs = [HVTrainer(ms[0], lr=1e-3, monitor_every=me), HVTrainer(ms[1], lr=1e-3, monitor_every=me),
+       HVTrainer(ms[2], lr=1e-3, monitor_every=me, graph=True)]
 gen = torch.Generator().manual_seed(5)
 B, S = 2, 96
 for step in range(4):
@@ -43,5 +44,10 @@ for step in range(4):
         bad = [n for (n, pa), (_, pb) in zip(ms[0].named_parameters(), ms[j].named_parameters())
                if not torch.equal(pa, pb)]
         same.append(f"{len(bad)} differ" + (f" (first {bad[0]})" if bad else ""))
-    print(f"variant {v:#x} {prec} step {step}: eager {ls[0]:.4f} eager2 {ls[1]:.4f} graph {ls[2]:.4f} | "
+    print(f"variant {v:#x} {prec} monitor_every {me} step {step}: eager {ls[0]:.4f} eager2 {ls[1]:.4f} graph {ls[2]:.4f} | "
           f"eager2: {same[0]} | graph: {same[1]}", flush=True)
+    pe, pg = trs[0].last_predictions, trs[2].last_predictions
+    diffs = {k: float((pe[k].float() - pg[k].float()).abs().max()) for k in pe}
+    hist = [n for (n, ba), (_, bb) in zip(ms[0].named_buffers(), ms[2].named_buffers())
+            if "convergence_history" in n and not torch.equal(ba, bb)]
+    print(f"   predictions max|eager - graph| {diffs}; Sinkhorn histories differing: {len(hist)}", flush=True)
