@@ -714,6 +714,19 @@ __global__ void k_scatter_rows(const T* dy, long stride, int n, int c, T* dx) {
 // ------------------------------------------------------------------ YOLO loss
 // object count: block partial counts added atomically (integer-valued floats < 2^24: exact in
 // any order, so deterministic)
+// Small fills / copies as kernels, not hipMemsetAsync / hipMemcpyAsync: inside a captured
+// training step these become kernel nodes ordered like every other launch (the memset-node
+// form of the object-count reset left the first replay's YOLO loss normalised by a wrong
+// count on some runs -- tools/train_bisect.py: identical predictions, total 2002.99 vs 1700.07).
+__global__ void k_fill_f32(float* p, int n, float v) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+__global__ void k_copy_f32(const float* __restrict__ src, float* __restrict__ dst, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
 __global__ void __launch_bounds__(256) k_yolo_count(const float* targets, long cells, int P, float* nobj) {
   __shared__ float scratch[16];
   float s = 0.f;
@@ -1088,8 +1101,9 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
     else if (dy_dtype == HV_F32) rc = colred_run<unsigned short, float, CR_ROWN>(r, 1, work, sums, 0, s);
     else rc = colred_run<unsigned short, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
     if (rc) return rc;
-    if (dgamma) HV_CHECK(hipMemcpyAsync(dgamma, sums, cols * sizeof(float), hipMemcpyDeviceToDevice, s));
-    if (dbeta) HV_CHECK(hipMemcpyAsync(dbeta, sums + cols, cols * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (dgamma) k_copy_f32<<<hv_cdiv(cols, 256), 256, 0, s>>>(sums, dgamma, cols);
+    if (dbeta) k_copy_f32<<<hv_cdiv(cols, 256), 256, 0, s>>>(sums + cols, dbeta, cols);
+    HV_CHECK_LAUNCH();
   }
   return HV_OK;
 }
@@ -1202,7 +1216,7 @@ extern "C" int hv_yolo_loss(int dtype, const void* logits, const float* targets,
   float* nobj = work;
   float* part = work + 8;
   const unsigned nblk = hv_cdiv(cells, 256);
-  HV_CHECK(hipMemsetAsync(nobj, 0, sizeof(float), s));
+  k_fill_f32<<<1, 256, 0, s>>>(nobj, 1, 0.f);
   k_yolo_count<<<(unsigned)((cells + 255) / 256 < 1024 ? (cells + 255) / 256 : 1024), 256, 0, s>>>(targets, cells, P, nobj);
 #define YL_LAUNCH(T, TD) k_yolo_loss<T, TD><<<nblk, 256, 0, s>>>((const T*)logits, targets, n, h, w, A, P, l_coord, \
       l_obj, l_noobj, l_cls, nobj, (TD*)dlogits, part)
