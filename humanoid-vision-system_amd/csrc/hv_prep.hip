@@ -290,89 +290,9 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
     }
 }
 
-// bf16 fold tile with 128-deep k-steps (K = Hd % 128 == 0: every site).  The 32-deep form above
-// is a chain of K/32 dependent global-load round trips per tile (4 MFMAs per wave between them:
-// 0.08 MFMA busy, 408 us per forward); here each thread keeps 2 x 8 x 16 B of the NEXT k-step in
-// flight, so a tile waits K/128 round trips.  Load mapping: piece p = j * 256 + t of the
-// 64 rows x 32 16-B pieces of a k-step is (row p / 32, piece p % 32), so every load instruction
-// of a wave reads two whole 512-B row segments (a mapping with 128 contiguous bytes per lane
-// touched 64 cache lines per instruction and ran 6x slower).  Same k order and fp32 accumulation
-// per output as one bf16 MFMA chain over k = 0..K-1, like the 32-deep form.
-constexpr int FK = 128;
-constexpr int FRB = FK * 2 + 16;          // LDS row bytes: 128 bf16 + 16 B pad (conflict-free b128 reads)
-__device__ __forceinline__ void fold_tile_bf128(const hv_mhc_prep_entry& e, const Scratch& sc, int tile, char* lds) {
-  const int D = e.D, K = e.Hd;
-  const int ntn = (D + 63) / 64;
-  const int m0 = (tile / ntn) * 64, n0 = (tile % ntn) * 64;
-  char* As = lds;
-  char* Bs = lds + 64 * FRB;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-  const int pr = t >> 5, pc = (t & 31) * 4;         // row (+ 8 j) and k offset of this thread's pieces
-  const float* Ar = e.w1 + (long)(m0 + pr) * K + pc;
-  const float* Br = sc.gc + (long)(n0 + pr) * K + pc;
-  bool bv[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bv[j] = n0 + pr + 8 * j < D;
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 na[8], nb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    na[j] = *reinterpret_cast<const float4*>(Ar + (long)8 * j * K);
-    nb[j] = bv[j] ? *reinterpret_cast<const float4*>(Br + (long)8 * j * K) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  const int fr = lane & 15, fg = lane >> 4;
-  for (int k0 = 0; k0 < K; k0 += FK) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int off = (pr + 8 * j) * FRB + pc * 2;
-      *reinterpret_cast<uint2*>(As + off) = make_uint2(pack_bf16x2(na[j].x, na[j].y), pack_bf16x2(na[j].z, na[j].w));
-      *reinterpret_cast<uint2*>(Bs + off) = make_uint2(pack_bf16x2(nb[j].x, nb[j].y), pack_bf16x2(nb[j].z, nb[j].w));
-    }
-    __syncthreads();
-    if (k0 + FK < K) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        na[j] = *reinterpret_cast<const float4*>(Ar + (long)8 * j * K + k0 + FK);
-        if (bv[j]) nb[j] = *reinterpret_cast<const float4*>(Br + (long)8 * j * K + k0 + FK);
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < FK / 32; ++ks) {
-      uint4 fa[2], fb[2];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) fa[a] = *reinterpret_cast<const uint4*>(As + (wr * 32 + a * 16 + fr) * FRB + ks * 64 + fg * 16);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) fb[c] = *reinterpret_cast<const uint4*>(Bs + (wc * 32 + c * 16 + fr) * FRB + ks * 64 + fg * 16);
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-          acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[a]),
-                                                              __builtin_bit_cast(bf16x8, fb[c]), acc[a][c], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int col = n0 + wc * 32 + c * 16 + (lane & 15);
-      if (col >= D) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = m0 + wr * 32 + a * 16 + (lane >> 4) * 4 + j;
-        Elem<unsigned short>::store((unsigned short*)e.a1, (long)row * D + col, acc[a][c][j]);
-      }
-    }
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict__ tab, int count) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * FRB];
+  __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 144];
   // the fold tiles of one 64-row block of W1 (one per 64 columns of D) are consecutive logical
   // blocks: on one XCD they read those W1 rows from HBM once (W1 is the dominant operand, 390 MB
   // per forward over all sites; dealt round-robin it was re-fetched by every XCD's L2)
@@ -383,12 +303,6 @@ __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict
   const Scratch sc = carve(e);
   const int b = bx - e.blk[2];
   if (b < s.fold) {
-    if constexpr (std::is_same<T, unsigned short>::value) {
-      if (e.Hd % FK == 0) {
-        fold_tile_bf128(e, sc, b, lds);
-        return;
-      }
-    }
     fold_tile<T>(e, sc, b, lds);
     return;
   }

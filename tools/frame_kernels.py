@@ -26,7 +26,7 @@ print(f"launches per frame {len(frame)}; GPU span {span:.1f} us; summed kernel t
 hist = collections.Counter()
 tsum = collections.defaultdict(float)
 for s, e, n in frame:
-    k = n.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+    k = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
     hist[k] += 1
     tsum[k] += (e - s) / 1e3
 for k, c in sorted(hist.items(), key=lambda kv: -tsum[kv[0]]):
