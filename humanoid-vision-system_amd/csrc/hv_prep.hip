@@ -65,14 +65,6 @@ __device__ inline int find_entry(const E* t, int count, int b) {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// XCD-local workgroup order: the hardware deals consecutive workgroups round-robin over the 8
-// XCDs; this bijection gives each XCD a CONTIGUOUS range of logical block indices, so
-// neighbouring tiles (which share operand rows) run on one XCD and meet in its L2
-__device__ __forceinline__ int xcd_local(int bid, int G) {
-  const int xcd = bid & 7, q = G >> 3, r = G & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
 // ------------------------------------------------------------------ phase 1
 __global__ void __launch_bounds__(256) k_pg1(const hv_mhc_prep_entry* __restrict__ tab, int count) {
   __shared__ float red[2][4][PT];
@@ -293,10 +285,10 @@ __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scra
 template <typename T>
 __global__ void __launch_bounds__(256) k_pg3(const hv_mhc_prep_entry* __restrict__ tab, int count) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 64 * 144];
-  // the fold tiles of one 64-row block of W1 (one per 64 columns of D) are consecutive logical
-  // blocks: on one XCD they read those W1 rows from HBM once (W1 is the dominant operand, 390 MB
-  // per forward over all sites; dealt round-robin it was re-fetched by every XCD's L2)
-  const int bx = xcd_local(blockIdx.x, gridDim.x);
+  // hardware order: an XCD-local remap (each XCD a contiguous range of tiles, so the tiles of
+  // one W1 row block share an L2) measured SLOWER, 577 vs 408 us per forward -- the round-robin
+  // deal spreads each row block's tiles over all eight XCDs' HBM request queues at once
+  const int bx = blockIdx.x;
   const int ei = find_entry<hv_mhc_prep_entry, 2>(tab, count, bx);
   const hv_mhc_prep_entry& e = tab[ei];
   const PrepSizes s = prep_sizes(e.D, e.Hd, e.fold);
