@@ -29,10 +29,8 @@ __device__ __forceinline__ v4i16 tr_read(const unsigned char* p) {
 }
 
 // BGATHER: 0 dense B, 1 conv im2col with 16-B channel chunks, 2 conv im2col scalar
-// three workgroups per CU (the two-step register prefetch otherwise took the 128x128 tile to 172
-// VGPR+AGPR and two per CU); the per-element conv gather keeps two (it spills at three)
 template <typename T, int BM, int BN, int BGATHER>
-__global__ void __launch_bounds__(256, (BGATHER == 2 ? 2 : 3)) gemm_tn_kernel(const hv_wgrad_desc d, int p_chunk) {
+__global__ void __launch_bounds__(256) gemm_tn_kernel(const hv_wgrad_desc d, int p_chunk) {
   constexpr int KSTEP = TnTr<T>::KSTEP, EPC = TnTr<T>::EPC;
   constexpr int APITCH = BM * (int)sizeof(T) + 32;
   constexpr int BPITCH = BN * (int)sizeof(T) + 32;
@@ -56,9 +54,7 @@ __global__ void __launch_bounds__(256, (BGATHER == 2 ? 2 : 3)) gemm_tn_kernel(co
   const long pend = min((long)d.P, pbeg + p_chunk);
   const int nk = (int)((pend - pbeg + KSTEP - 1) / KSTEP);
 
-  // two register sets: k-step kt+2's global loads are issued while kt computes and kt+1 waits
-  // in the other set (one step ahead, each k-step waited a whole load round trip)
-  uint4 ra[2][ACH], rb[2][BCH];
+  uint4 ra[ACH], rb[BCH];
 
   auto load_b_chunk = [&](long p, int col) -> uint4 {
     if (p >= pend || col >= d.N2) return make_uint4(0, 0, 0, 0);
@@ -94,33 +90,33 @@ __global__ void __launch_bounds__(256, (BGATHER == 2 ? 2 : 3)) gemm_tn_kernel(co
     }
   };
 
-  auto gload = [&](int kt, uint4 (&xa)[ACH], uint4 (&xb)[BCH]) {
+  auto gload = [&](int kt) {
     const long p0 = pbeg + (long)kt * KSTEP;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + 256 * i;
       const int r = c / ACPR, col = n10 + (c % ACPR) * EPC;
       const long p = p0 + r;
-      xa[i] = (p < pend && col < d.N1) ? *reinterpret_cast<const uint4*>((const T*)d.A + p * d.lda + col)
+      ra[i] = (p < pend && col < d.N1) ? *reinterpret_cast<const uint4*>((const T*)d.A + p * d.lda + col)
                                        : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + 256 * i;
       const int r = c / BCPR, col = n20 + (c % BCPR) * EPC;
-      xb[i] = load_b_chunk(p0 + r, col);
+      rb[i] = load_b_chunk(p0 + r, col);
     }
   };
-  auto sstore = [&](int buf, const uint4 (&xa)[ACH], const uint4 (&xb)[BCH]) {
+  auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + 256 * i;
-      *reinterpret_cast<uint4*>(As + (buf * KSTEP + c / ACPR) * APITCH + (c % ACPR) * 16) = xa[i];
+      *reinterpret_cast<uint4*>(As + (buf * KSTEP + c / ACPR) * APITCH + (c % ACPR) * 16) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + 256 * i;
-      *reinterpret_cast<uint4*>(Bs + (buf * KSTEP + c / BCPR) * BPITCH + (c % BCPR) * 16) = xb[i];
+      *reinterpret_cast<uint4*>(Bs + (buf * KSTEP + c / BCPR) * BPITCH + (c % BCPR) * 16) = rb[i];
     }
   };
 
@@ -131,19 +127,14 @@ __global__ void __launch_bounds__(256, (BGATHER == 2 ? 2 : 3)) gemm_tn_kernel(co
     for (int b = 0; b < RN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    gload(0, ra[0], rb[0]);
-    if (nk > 1) gload(1, ra[1], rb[1]);
-    sstore(0, ra[0], rb[0]);
+    gload(0);
+    sstore(0);
   }
   __syncthreads();
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pq = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    // register set (kt & 1) held step kt (already in LDS): refill it with step kt+2
-    if (kt + 2 < nk) {
-      if (buf == 0) gload(kt + 2, ra[0], rb[0]);
-      else gload(kt + 2, ra[1], rb[1]);
-    }
+    if (kt + 1 < nk) gload(kt + 1);
     const unsigned char* sa = As + buf * KSTEP * APITCH;
     const unsigned char* sb = Bs + buf * KSTEP * BPITCH;
     if constexpr (IS_BF16) {
@@ -185,10 +176,7 @@ __global__ void __launch_bounds__(256, (BGATHER == 2 ? 2 : 3)) gemm_tn_kernel(co
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[b], fa[a], acc[a][b], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) {
-      if (buf == 0) sstore(1, ra[1], rb[1]);
-      else sstore(0, ra[0], rb[0]);
-    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
 
