@@ -233,7 +233,10 @@ TnPlan plan_tn(int P, int N1, int N2, int kstep) {
   t.bn = N2 >= 128 ? 128 : 64;
   const long tiles = (long)hv_cdiv(N1, t.bm) * hv_cdiv(N2, t.bn);
   const long ksteps = (P + kstep - 1) / kstep;
-  long s = (1024 + tiles - 1) / tiles;                 // aim for >= 1024 workgroups
+  // aim for >= 512 workgroups: 1024 split the pixels twice as finely and doubled the fp32
+  // partial traffic + reduce; base-640 B=16 training step 146.5 / 146.4 vs 150.3 / 149.5 ms
+  // (profiles/r04/wgrad_split_ab.txt)
+  long s = (512 + tiles - 1) / tiles;
   s = s < 1 ? 1 : s;
   const long max_s = ksteps / 4 > 0 ? ksteps / 4 : 1; // each split keeps >= 4 k-steps
   s = s > max_s ? max_s : s;

@@ -43,7 +43,10 @@ out = m(x, targets=tg, compute_loss=True)
 out["loss"]["total_loss"].backward()
 local = tr.grads.flat.clone()
 tr.grads.world = hooks_world
-tr.grads._hooks = [p.register_post_accumulate_grad_hook(tr.grads._on_grad) for p in tr.grads.params]
+with tr._on_stream():                     # the trainer's hooks live on its stream (HVTrainer.__init__)
+    g = tr.grads
+    g._hooks = [p.register_hook(g._flag_hook(i)) for i, p in enumerate(g.params)]
+    g._hooks += [p.register_post_accumulate_grad_hook(g._on_grad) for p in g.params]
 torch.manual_seed(7)
 for step in range(2):
     loss = tr.step(x, tg)
