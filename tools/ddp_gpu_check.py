@@ -41,7 +41,13 @@ for h in tr.grads._hooks:
     h.remove()
 out = m(x, targets=tg, compute_loss=True)
 out["loss"]["total_loss"].backward()
-local = tr.grads.flat.clone()
+# the local gradients in the flat buffer's layout (zero() leaves param.grad None, so without the
+# hooks the backward stored them in param.grad, not in the flat views)
+local = torch.zeros_like(tr.grads.flat)
+for p in tr.grads.params:
+    if p.grad is not None:
+        o = tr.grads.offsets[id(p)]
+        local[o:o + p.numel()] = p.grad.detach().float().reshape(-1)
 tr.grads.world = hooks_world
 with tr._on_stream():                     # the trainer's hooks live on its stream (HVTrainer.__init__)
     g = tr.grads
