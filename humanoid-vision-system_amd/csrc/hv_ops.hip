@@ -1262,8 +1262,11 @@ __global__ void __launch_bounds__(256) k_attention_row(const T* __restrict__ q, 
 }
 
 // ---- batched byte-range copies (hv_copy_segments): 16 KiB per block, segment found by binary
-// search over the block prefix table passed by value
-constexpr int kCopyMax = 64;
+// search over the block prefix table passed by value.  24 ranges per launch keep the by-value
+// table under 1 KiB: with 64 (2.1 KiB of kernel arguments) a rocprofv3 --pmc run of a training
+// step crashed inside the launch (SIGSEGV at a mapping boundary in the profiler-intercepted
+// dispatch path; unprofiled runs were unaffected)
+constexpr int kCopyMax = 24;
 constexpr long long kCopyChunk = 16384;
 struct CopyBatch {
   int count;
@@ -1435,10 +1438,10 @@ extern "C" int hv_copy_segments(const hv_copy_segment* segs, int count, hv_strea
   return HV_OK;
 }
 
-// Host bytes -> device through kernel arguments (2 KiB per launch): a captured graph records the
+// Host bytes -> device through kernel arguments (1 KiB per launch): a captured graph records the
 // bytes by value in its kernel nodes, so a table upload inside a capture needs no pinned staging
 // buffer (pinning new host memory is refused while a stream captures) and nothing to keep alive.
-constexpr int kArgBytes = 2048;
+constexpr int kArgBytes = 1024;                  // kernel-argument bytes per launch (see kCopyMax)
 struct ArgBytes {
   unsigned int w[kArgBytes / 4];
 };

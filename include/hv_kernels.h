@@ -397,7 +397,7 @@ int hv_attention_general(int dtype, const void* q, const void* k, const void* v,
                          const unsigned char* key_padding_mask, void* out, float* weights, int n,
                          int Lq, int Lk, int heads, int hd, float sm_scale, hv_stream_t stream);
 
-/* Batched device-to-device copy of `count` byte ranges in one launch per 64 ranges (the
+/* Batched device-to-device copy of `count` byte ranges in one launch per 24 ranges (the
    engine's owned copies of a graph replay's outputs: InferenceEngine.infer returns fresh
    tensors per call, engine.py:251-317, while a replay rewrites the captured buffers). */
 typedef struct hv_copy_segment {
@@ -406,7 +406,7 @@ typedef struct hv_copy_segment {
   long long bytes;
 } hv_copy_segment;
 int hv_copy_segments(const hv_copy_segment* segs /* host array */, int count, hv_stream_t stream);
-/* n host bytes -> device `dst`, stream-ordered, carried in kernel arguments (2 KiB per launch):
+/* n host bytes -> device `dst`, stream-ordered, carried in kernel arguments (1 KiB per launch):
    usable inside a graph capture, where pinning host memory for an async copy is refused; the
    host buffer may be reused as soon as the call returns. */
 int hv_write_bytes(void* dst, const void* src, long long n, hv_stream_t stream);
