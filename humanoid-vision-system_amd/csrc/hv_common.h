@@ -84,6 +84,18 @@ __device__ __forceinline__ float hv_act_grad(float z, int act) {
   }
 }
 
+// Derivative of hv_gelu_fast, the GELU a bf16 training forward applies (its backward then
+// differentiates the function it ran): with s = 1 / (1 + 2^(x p(x^2))),
+// d/dx [x s] = s - x s (1 - s) ln2 (p + 2 x^2 p'(x^2))  (p' = 0 where x^2 is clamped)
+__device__ __forceinline__ float hv_gelu_grad_fast(float x) {
+  const float x2r = x * x;
+  const float x2 = fminf(x2r, 64.f);
+  const float p = fmaf(fmaf(1.0142630839702301e-3f, x2, -0.10677572552514955f), x2, -2.3011213415186913f);
+  const float dp = x2r < 64.f ? fmaf(2.0285261679404602e-3f, x2, -0.10677572552514955f) : 0.f;
+  const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * p));
+  return sg - x * sg * (1.f - sg) * 0.6931471805599453f * fmaf(2.f * x2, dp, p);
+}
+
 // Dropout keep mask shared by every training kernel: element idx of a tensor dropped with
 // probability p under `seed` (counter-based, so the backward regenerates it instead of storing).
 __device__ __forceinline__ uint32_t hv_hash32(uint32_t h) {

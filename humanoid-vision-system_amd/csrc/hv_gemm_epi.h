@@ -21,6 +21,17 @@ __device__ __forceinline__ uint32_t epi_seed(const hv_gemm_desc& d) {
   return d.drop_p > 0.f ? hv_seed(d.drop_seed, d.seed_offset) : 0u;
 }
 
+// Training activations: bf16 outputs take the fast GELU (|err| <= 2.6e-5, far below bf16
+// resolution) and its exact derivative in the backward, as the inference epilogue does -- the
+// erf form and its derivative were ~60 VALU instructions per element of the write-bound
+// training GEMMs; fp32 (parity) outputs keep the exact erf GELU.
+__device__ __forceinline__ float epi_train_act(const hv_gemm_desc& d, float z) {
+  return (d.act == HV_ACT_GELU && d.c_dtype == HV_BF16) ? hv_gelu_fast(z) : hv_act(z, d.act);
+}
+__device__ __forceinline__ float epi_train_act_grad(const hv_gemm_desc& d, float z) {
+  return (d.act == HV_ACT_GELU && d.c_dtype == HV_BF16) ? hv_gelu_grad_fast(z) : hv_act_grad(z, d.act);
+}
+
 __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 acc, int row, int col, const f32x4 sc,
                                            const f32x4 bi, const f32x4 cs, float mean, float rstd, bool ln_epi) {
   f32x4 v;
@@ -60,7 +71,7 @@ __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 ac
     }
     const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
+    for (int j = 0; j < 4; ++j) v[j] = epi_train_act(d, z[j]) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
   } else {
     if (vec) {
       if (aux_bf) {
@@ -80,7 +91,7 @@ __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 ac
     const uint32_t sd_ = epi_seed(d);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      v[j] = acc[j] * d.alpha * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+      v[j] = acc[j] * d.alpha * hv_drop_scale(sd_, idx0 + j, d.drop_p) * epi_train_act_grad(d, z[j]);
   }
   return v;
 }
@@ -333,7 +344,7 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
     }
     const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = hv_act(z[j], d.act) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
+    for (int j = 0; j < 8; ++j) v[j] = epi_train_act(d, z[j]) * hv_drop_scale(sd_, idx0 + j, d.drop_p);
   } else {
     if (av && aux_bf) {
       const uint4 t = *reinterpret_cast<const uint4*>((const unsigned short*)d.aux + ai);
@@ -355,7 +366,7 @@ __device__ __forceinline__ void epi_train8(const hv_gemm_desc& d, float (&v)[8],
     }
     const uint32_t sd_ = epi_seed(d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * epi_train_act_grad(d, z[j]);
   }
 }
 
@@ -536,7 +547,7 @@ __device__ __forceinline__ void epi_writeout_m2pf(const hv_gemm_desc& d, int r0,
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const unsigned long long idx0 = (unsigned long long)row * d.N + col;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * hv_act_grad(z[j], d.act);
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * hv_drop_scale(sd_, idx0 + j, d.drop_p) * epi_train_act_grad(d, z[j]);
     if (vcol) {
       if constexpr (RES == 1) {
         const unsigned rw[4] = {rb[p].x, rb[p].y, rb[p].z, rb[p].w};

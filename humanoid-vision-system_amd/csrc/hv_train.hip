@@ -537,7 +537,9 @@ __global__ void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ pre, l
                           uint32_t seed, const unsigned int* soff, T* dpre) {
   seed = hv_seed(seed, soff);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    st<T>(dpre, i, ld<T>(dy, i) * hv_drop_scale(seed, (unsigned long long)i, p) * hv_act_grad(ld<T>(pre, i), act));
+    st<T>(dpre, i, ld<T>(dy, i) * hv_drop_scale(seed, (unsigned long long)i, p) *
+                       ((sizeof(T) == 2 && act == HV_ACT_GELU) ? hv_gelu_grad_fast(ld<T>(pre, i))
+                                                                : hv_act_grad(ld<T>(pre, i), act)));
 }
 
 template <typename T>
