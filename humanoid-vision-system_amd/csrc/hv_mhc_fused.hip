@@ -1038,21 +1038,47 @@ int launch2(const hv_mhc_fused_args* a, hipStream_t s) {
 
 }  // namespace
 
+extern "C" int hv_mhc_tok_supported(int D, int Hd);
+int hv_mhc_tok_launch(const hv_mhc_fused_args* a, int n, hipStream_t s);
+
 extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant) {
   if (dtype != HV_BF16) return 0;
+  if (variant & HV_MV_TOK) return hv_mhc_tok_supported(D, Hd);
   return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
          (D == 256 && Hd == 512 && (variant & (HV_MV_WIDE | HV_MV_SPLIT256)));
 }
 
-extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
-  if (!a || a->T <= 0) return HV_EINVAL;
+static int mhc_args_ok(const hv_mhc_fused_args* a) {
+  if (!a || a->T <= 0 || !a->x || !a->a1t || !a->c1 || !a->w2 || !a->b2 || !a->wct || !a->g_post || !a->b_post ||
+      !a->out)
+    return HV_EINVAL;
   if (!hv_mhc_fused_supported(a->D, a->Hd, a->dtype, a->variant)) return HV_EUNSUPPORTED;
-  const int shape = a->variant & HV_MV_SHAPE_MASK;
   const uintptr_t al = (uintptr_t)a->x | (uintptr_t)a->a1t | (uintptr_t)a->w2 | (uintptr_t)a->wct |
                        (uintptr_t)a->out | (uintptr_t)a->c1 | (uintptr_t)a->b2 | (uintptr_t)a->g_post |
                        (uintptr_t)a->b_post | (uintptr_t)a->residual;
   if (al & 15) return HV_EUNSUPPORTED;
+  return HV_OK;
+}
+
+extern "C" int hv_mhc_fused_group(const hv_mhc_fused_args* a, int n, hv_stream_t stream) {
+  if (!a || n < 1 || n > 3) return HV_EINVAL;
+  for (int i = 0; i < n; ++i) {
+    const int e = mhc_args_ok(a + i);
+    if (e != HV_OK) return e;
+    if (a[i].D != a[0].D || a[i].Hd != a[0].Hd || a[i].T != a[0].T || a[i].dtype != a[0].dtype ||
+        a[i].variant != a[0].variant)
+      return HV_EINVAL;
+  }
+  if (!(a[0].variant & HV_MV_TOK)) return HV_EUNSUPPORTED;
+  return hv_mhc_tok_launch(a, n, (hipStream_t)stream);
+}
+
+extern "C" int hv_mhc_fused(const hv_mhc_fused_args* a, hv_stream_t stream) {
+  const int e = mhc_args_ok(a);
+  if (e != HV_OK) return e;
+  const int shape = a->variant & HV_MV_SHAPE_MASK;
   hipStream_t s = (hipStream_t)stream;
+  if (a->variant & HV_MV_TOK) return hv_mhc_tok_launch(a, 1, s);
   // default for D = 32 / 64: the software-pipelined per-wave kernel with unmerged fragment reads
   // (tools/mhc_ab.py, gpurun_out r3 mhcpipe3: D=64 T=1.6M 0.849 vs 0.979 ms, T=409,600 0.220 vs
   // 0.265; D=32 T=1.6M 0.321 vs 0.346; in-model graph 19.94 vs 20.26 ms/step, bitwise equal).

@@ -25,6 +25,7 @@ GV_TRAIN_NOPF = 0x100000
 MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_SHIFT = 1, 2, 5, 6, 0x100, 16
 MV_SPLIT256, MV_SPLITW = 0x200, 12
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
+MV_TOK, MV_TOK16 = 0x400, 0x800
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
 ABI_VERSION = 2          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
@@ -142,6 +143,7 @@ _SIGS = {
     "hv_wprep_group": ([vp, i32, i32, vp], i32),
     "hv_mhc_fused_supported": ([i32, i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
+    "hv_mhc_fused_group": ([vp, i32, vp], i32),
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),

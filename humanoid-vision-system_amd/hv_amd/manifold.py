@@ -346,6 +346,16 @@ class MultiHeadManifoldAttention(nn.Module):
         L = x.shape[0] // n
         ctx = current()
         opts = options()
+        if opts.use_fused_mhc and not self.training:
+            # q / k / v read the same x: one grouped launch of the token-tile fused kernel
+            qp = self.q_proj
+            gv = ops.mhc_group_variant(qp.input_dim, qp.hidden_dim, x.shape[0], 3, x.dtype)
+            if gv:
+                plans = [m.plan() for m in (self.q_proj, self.k_proj, self.v_proj)]
+                if all(p.fold for p in plans):
+                    q, k, v = (t.view(n, L, -1) for t in ops.mhc_fused_group(x, plans, gv))
+                    o = ops.attention(q, k, v, self.num_heads)
+                    return self.out_proj.forward_tokens(o.view(n * L, -1))
         grp = ctx.plans.get(("group", id(self))) if (ctx is not None and opts.group_qkv) else None
         # a fused one-launch chain per projection beats sharing GEMM1 across q / k / v
         fused = opts.use_fused_mhc and ops.mhc_fused_supported(self.q_proj.input_dim, self.q_proj.hidden_dim, x.dtype)

@@ -287,7 +287,7 @@ def f32(t: Optional[Tensor]) -> Optional[Tensor]:
     return None if t is None else t.detach().float().contiguous()
 
 
-def _mhc_variant(D: int, T: Optional[int], variant: Optional[int]) -> int:
+def _mhc_variant(D: int, T: Optional[int], variant: Optional[int], Hd: Optional[int] = None, nsites: int = 1) -> int:
     """D = 256 sites take the split-hidden fused kernel (HV_MV_SPLIT256) automatically only from
     HVOptions.mhc256_min_tokens tokens: one 64-token group per workgroup, so small grids leave CUs
     idle and the unfused chain (the ViT's grouped q / k / v GEMM1) wins -- per launch 0.421 vs
@@ -295,15 +295,37 @@ def _mhc_variant(D: int, T: Optional[int], variant: Optional[int]) -> int:
     D = 256 site fused: B=16 19.90 vs 19.18 ms, B=1 9.0 vs 7.05 ms (profiles/r04/mhc256_ab.txt)."""
     o = options()
     v = o.mhc_variant if variant is None else variant
+    if v == 0 and T is not None and o.mhc_tok:
+        v = _tok_variant(D, Hd, T, nsites)
     if v == 0 and D == 256 and T is not None and T >= o.mhc256_min_tokens:
         v = L.MV_SPLIT256
+    return v
+
+
+# Token-tile kernel (hv_mhc_tok.hip) policy, from the per-launch A/B (tools/mhc_tok_ab.py,
+# profiles/r05/mhc_tok_ab.txt): (D, Hd) -> largest token count it takes.  (256, 512): 23 us at
+# T = 401 / 33 at 6,416 / 116 at 25,600 vs the chain's 59 / 62 / 136 and the split-hidden kernel's
+# 124 at 25,600; (128, 512): 26 vs 58-60 us at 6,400, but the split-hidden kernel wins from 25,600
+# (64 vs 94 us); (256, 1024) ties the chain at 1,600 and loses at 6,400: not taken.  Every
+# workgroup streams all of a site's weights, so 16-token tiles (twice the workgroups) win while
+# the grid fits the 256 CUs in one round, 32-token tiles (half the weight traffic per token) after.
+TOK_MAX_T = {(128, 512): 12800, (256, 512): 51200}
+TOK_CUS = 256
+
+
+def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
+    if Hd is None or T > TOK_MAX_T.get((D, Hd), -1):
+        return 0
+    v = L.MV_TOK
+    if -(-T // 16) * nsites <= TOK_CUS:
+        v |= L.MV_TOK16
     return v
 
 
 def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype, variant: Optional[int] = None,
                         T: Optional[int] = None) -> bool:
     """T: the site's token count (None = the token-count-independent answer)."""
-    v = _mhc_variant(D, T, variant)
+    v = _mhc_variant(D, T, variant, Hd)
     return dtype in (torch.float32, torch.bfloat16) and bool(L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype), v))
 
 
@@ -323,9 +345,40 @@ def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optiona
     out = torch.empty_like(x)
     a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
                        b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), ptr(residual),
-                       out.data_ptr(), _mhc_variant(D, T, variant), 0)
+                       out.data_ptr(), _mhc_variant(D, T, variant, Hd), 0)
     check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
     return out
+
+
+def mhc_group_variant(D: int, Hd: int, T: int, n: int, dtype: torch.dtype, variant: Optional[int] = None) -> int:
+    """HV_MV_* of a grouped launch of n sites (0: no grouped fused kernel for this shape)."""
+    if dtype != torch.bfloat16:
+        return 0
+    v = _mhc_variant(D, T, variant, Hd, n)
+    if not v & L.MV_TOK or not L.lib().hv_mhc_fused_supported(D, Hd, dtype_code(dtype), v):
+        return 0
+    return v
+
+
+def mhc_fused_group(x: Tensor, plans, variant: int) -> list:
+    """n <= 3 mHC chains on the SAME x [T, D] (q / k / v) in one launch (hv_mhc_fused_group);
+    plans: manifold.MhcPlan (folded), variant from mhc_group_variant."""
+    _contig(x, "x")
+    T, D = x.shape
+    n = len(plans)
+    arr = (L.MhcFusedArgs * n)()
+    outs = []
+    for i, p in enumerate(plans):
+        Hd = p.w2.shape[0]
+        if p.b1.shape != (2 * Hd, D) or p.w2.shape != (Hd, 2 * Hd) or p.wct.shape != (D, D + Hd) or not p.fold:
+            raise ValueError("mhc_fused_group: coefficient shapes do not match x")
+        o = torch.empty_like(x)
+        outs.append(o)
+        arr[i] = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), p.b1.data_ptr(), p.c1.data_ptr(),
+                                p.w2.data_ptr(), p.bias2.data_ptr(), p.wct.data_ptr(), p.g_post.data_ptr(),
+                                p.b_post.data_ptr(), None, o.data_ptr(), variant, 0)
+    check(L.lib().hv_mhc_fused_group(arr, n, stream_ptr()), f"hv_mhc_fused_group D={D} n={n}")
+    return outs
 
 
 def gemv(w: Tensor, x: Tensor, b: Optional[Tensor] = None) -> Tensor:

@@ -40,6 +40,7 @@ class HVOptions:
     gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
     mhc256_min_tokens: int = 25600    # D = 256 sites fused (split-hidden) from this many tokens (ops._mhc_variant)
+    mhc_tok: bool = True              # token-tile fused kernel for small-T sites (HV_MV_TOK, ops._mhc_variant)
 
     def replace(self, **kw) -> "HVOptions":
         return dataclasses.replace(self, **kw)
@@ -90,6 +91,38 @@ _TRAIN = _TrainState()
 def set_train_state(opts: Optional[HVOptions] = None, seed_offset: Optional[torch.Tensor] = None) -> None:
     _TRAIN.opts = opts if opts is not None else DEFAULT_OPTIONS
     _TRAIN.seed_offset = seed_offset
+
+
+def carry_train_state(namespace: dict) -> None:
+    """Every torch.autograd.Function class in `namespace` (a module's globals()) records the
+    training state of its forward (the model's HVOptions, the dropout seed-offset word) and runs
+    its backward under that state, so the backward -- on autograd's worker thread, after
+    system_forward has returned and restored _TRAIN -- launches with the forward's kernel variants
+    and seeds, and no model's options outlive its forward in the process-level _TRAIN."""
+    for cls in list(namespace.values()):
+        if not (isinstance(cls, type) and issubclass(cls, torch.autograd.Function)) or cls is torch.autograd.Function:
+            continue
+        if getattr(cls, "_hv_carries_state", False):
+            continue
+        fwd, bwd = cls.forward, cls.backward
+
+        def forward(ctx, *a, _fwd=fwd, **k):
+            ctx.hv_train_state = (_TRAIN.opts, _TRAIN.seed_offset)
+            return _fwd(ctx, *a, **k)
+
+        def backward(ctx, *g, _bwd=bwd):
+            st = getattr(ctx, "hv_train_state", None)
+            if st is None:
+                return _bwd(ctx, *g)
+            prev = (_TRAIN.opts, _TRAIN.seed_offset)
+            _TRAIN.opts, _TRAIN.seed_offset = st
+            try:
+                return _bwd(ctx, *g)
+            finally:
+                _TRAIN.opts, _TRAIN.seed_offset = prev
+
+        cls.forward, cls.backward = staticmethod(forward), staticmethod(backward)
+        cls._hv_carries_state = True
 
 
 def seed_offset_ptr() -> Optional[int]:

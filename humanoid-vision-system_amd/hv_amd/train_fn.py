@@ -454,3 +454,8 @@ class YoloLossFn(torch.autograd.Function):
     def backward(ctx, g, _gs):
         (dl,) = ctx.saved_tensors
         return dl * g.to(dl.dtype), None, None, None
+
+
+from .runtime import carry_train_state  # noqa: E402
+
+carry_train_state(globals())

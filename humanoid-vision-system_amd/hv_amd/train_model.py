@@ -274,9 +274,18 @@ def system_forward(model, x: torch.Tensor, targets=None, task: str = "detection"
                    compute_loss: bool = False) -> Dict[str, Any]:
     """HybridVisionSystem.forward(x, targets, task, compute_loss) with model.training True.
     The model's HVOptions (kernel variants) apply to this forward and its backward
-    (runtime._TRAIN: the backward runs on autograd's worker thread, outside any RunCtx)."""
+    (runtime._TRAIN during the forward; runtime.carry_train_state hands them to the backward, which
+    runs on autograd's worker thread outside any RunCtx)."""
     from .runtime import _TRAIN, module_options
-    _TRAIN.opts = module_options(model)
+    prev = _TRAIN.opts
+    _TRAIN.opts = module_options(model)     # this forward only: every Function carries it into its backward
+    try:
+        return _system_forward(model, x, targets, task, compute_loss)
+    finally:
+        _TRAIN.opts = prev
+
+
+def _system_forward(model, x: torch.Tensor, targets, task: str, compute_loss: bool) -> Dict[str, Any]:
     dt = PRECISIONS[model.hv_precision]
     H = _hres_table(model)
     xin = to_nhwc(x.detach(), dt)
@@ -436,3 +445,8 @@ def yolo_loss_api(loss_fn, predictions: Dict[str, torch.Tensor], targets) -> Dic
         B, A, h, w, P = p.shape
         logits[s] = p.permute(0, 2, 3, 1, 4).reshape(B, h, w, A * P).contiguous()
     return yolo_loss(loss_fn, logits, targets, A)
+
+
+from .runtime import carry_train_state  # noqa: E402
+
+carry_train_state(globals())

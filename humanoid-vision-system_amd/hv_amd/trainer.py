@@ -563,9 +563,17 @@ class HVTrainer:
         return loss
 
     def _graph_key(self, images: Tensor, targets: List[Tensor]):
+        """Everything a captured step bakes in: shapes, parameter storage, precision, the kernel
+        variants (the model's HVOptions) and the optimizer hyper-parameters the captured clip +
+        AdamW launches carry by value -- changing opt.lr (a scheduler), loading an optimizer state
+        or model.set_options() re-captures instead of replaying stale values."""
+        from .runtime import module_options
+        o = self.opt
         return (tuple(images.shape), images.dtype, tuple(tuple(t.shape) for t in targets),
                 tuple(p.data_ptr() for p in self.grads.params), self.model.hv_precision
-                if hasattr(self.model, "hv_precision") else None)
+                if hasattr(self.model, "hv_precision") else None, module_options(self.model),
+                float(o.lr), float(o.wd), tuple(float(b) for b in o.betas), float(o.eps),
+                tuple(float(m) for m in o.max_norms))
 
     def _capture(self, images: Tensor, targets: List[Tensor], key) -> None:
         from . import ops
@@ -579,9 +587,11 @@ class HVTrainer:
         # thread_local: the autograd engine's worker thread issues the backward's launches onto
         # the capturing stream; the device-table uploads inside the step become graph memcpy
         # nodes whose pinned sources `keep` holds for the graph's lifetime
+        steps = self.opt.step_count
         with ops.capture_keepalive(keep):
             with torch.cuda.graph(graph, stream=self.stream, capture_error_mode="thread_local"):
                 loss = self._body(static_x, static_t)
+        self.opt.step_count = steps            # the capture ran step()'s host side; no step happened
         self._g = {"graph": graph, "x": static_x, "t": static_t, "loss": loss, "keep": keep, "key": key}
         self.captures += 1
 

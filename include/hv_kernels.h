@@ -242,10 +242,18 @@ typedef struct hv_mhc_fused_args {
                                     chunk loop waits for the A1^T half of the next-next chunk only */
 #define HV_MV_WIDE        0x100  /* also run (256, 512) fused, per-wave kernel (slower than the GEMM chain; tests) */
 #define HV_MV_SPLIT256    0x200  /* (256, 512) on the split-hidden kernel */
+#define HV_MV_TOK         0x400  /* token-tile kernel (hv_mhc_tok.hip): 32 (or 16) tokens per workgroup,
+                                    weights streamed L2 -> registers; (D, Hd) in {(128, 512), (256, 512),
+                                    (256, 1024)} -- small token counts (ViT, B=1) */
+#define HV_MV_TOK16       0x800  /* with HV_MV_TOK: 16-token tiles (Hd = 1024 always uses 16) */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
 int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant);
 int hv_mhc_fused(const hv_mhc_fused_args* args, hv_stream_t stream);
+/* n <= 3 sites with equal (dtype, D, Hd, T, variant) in ONE launch of the token-tile kernel (the
+   attention's q / k / v projections, which read the same x: MultiHeadManifoldAttention.forward,
+   manifold_layers.py:386-398); variant must include HV_MV_TOK */
+int hv_mhc_fused_group(const hv_mhc_fused_args* sites, int n, hv_stream_t stream);
 
 /* y[N] = W[N, K] x[K] + b  (fp32; folded mHC bias c1 = W1 u + b1) */
 int hv_gemv(const float* W, const float* x, const float* b, int N, int K, float* y, hv_stream_t stream);

@@ -57,6 +57,21 @@ def mhc_input(D: int, e: int) -> torch.Tensor:
     return torch.randn(64, D, generator=gen_seed(D, e, 11))
 
 
+# mHC fixtures at the token counts that make the automatic kernel policy (hv_amd/ops.py
+# _mhc_variant) pick each large-T kernel: (256, 2) at 25,601 -> token-tile (32-token tiles), at
+# 102,401 -> split-hidden; (128, 4) at 25,601 -> split-hidden; (256, 4) at 25,601 -> the chain.
+# x is regenerated from its seed (not stored); y64 is stored on a row subsample.
+MHC_LARGE_CASES = [(256, 2, 25601), (256, 2, 102401), (128, 4, 25601), (256, 4, 25601)]
+
+
+def mhc_input_large(D: int, e: int, T: int) -> torch.Tensor:
+    return torch.randn(T, D, generator=gen_seed(D, e, T, 14))
+
+
+def mhc_large_rows(T: int) -> torch.Tensor:
+    return torch.cat([torch.arange(0, T, 97), torch.arange(T - 5, T)])
+
+
 def mhc_cotangent(D: int, e: int) -> torch.Tensor:
     return torch.randn(64, D, generator=gen_seed(D, e, 12))
 

@@ -28,8 +28,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, REF)
 
 from oracle import weights as W  # noqa: E402
-from oracle.cases import (MHC_CASES, MODEL_CASES, SK_CASES, STAB_CASES, gen_seed,  # noqa: E402
-                          mhc_input, sinkhorn_raw, stab_inputs)
+from oracle.cases import (MHC_CASES, MHC_LARGE_CASES, MODEL_CASES, SK_CASES, STAB_CASES, gen_seed,  # noqa: E402
+                          mhc_input, mhc_input_large, mhc_large_rows, sinkhorn_raw, stab_inputs)
 
 _TINY = {"on": False}
 
@@ -235,6 +235,23 @@ def gen_mhc(ml):
             save(f"mhc_{fam}_D{D}_e{e}", x=x, y=y, y64=y64.float(), gx=x.grad,
                  g_hres=ghres, g_hpre_sum=m.H_pre_raw.grad.abs().sum(),
                  g_w1_sum=m.mlp[0].weight.grad.abs().sum())
+
+
+def gen_mhc_large(ml):
+    """mHC at the token counts where the automatic policy selects each large-T kernel
+    (cases.MHC_LARGE_CASES): the reference's fp64 forward on a row subsample (the chain is
+    per-token), plus the input checksum the test verifies its regenerated x against."""
+    print("G2b mhc large-T")
+    for fam in ("wc", "init"):
+        for D, e, T in MHC_LARGE_CASES:
+            x = mhc_input_large(D, e, T)
+            rows = mhc_large_rows(T)
+            with torch.no_grad():
+                m64 = ml.ManifoldHyperConnection(D, expansion_rate=e).double().eval()
+                W.load_formula_weights(m64, fam)
+                y64 = torch.cat([m64(x[i:i + 8192].double()) for i in range(0, T, 8192)])
+            save(f"mhc_{fam}_D{D}_e{e}_T{T}", rows=rows, y64=y64[rows].float(), x_sum=x.double().sum(),
+                 x_abs_sum=x.double().abs().sum(), T=T)
 
 
 # ------------------------------------------------------------------ G3 blocks
@@ -566,6 +583,8 @@ def main():
         gen_stability(ml)
     if "mhc" in parts:
         gen_mhc(ml)
+    if "mhc" in parts or "mhclarge" in parts:
+        gen_mhc_large(ml)
     if "blocks" in parts:
         gen_blocks(ml, vb, ve, yh)
     if "model" in parts:

@@ -17,6 +17,9 @@ from oracle import weights as W
 pytestmark = pytest.mark.gpu
 
 
+MHC_BF16_BOUND = 1.5e-2     # 3x HIP's measured bf16 mHC level vs the reference fp64 run
+
+
 def rel_l2(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
@@ -47,9 +50,10 @@ def test_mhc_bf16_agreement(gpu_device, fam, D, e):
     """bf16 mode held to the reference's OWN bf16 error: the reference under its autocast policy
     (S8, oracle/autocast_emu.py: bf16 matmuls/linears, fp32 LayerNorm -- manifold_layers.py:186,
     248) is `err_vs_f64` rel-L2 from its fp64 run on the same input (fixture *_bf16ref); the HIP
-    bf16 mHC must be within 2x that.  The well-conditioned family also keeps the absolute bound
-    5e-2 (centred coefficients keep HIP at the bf16 level; the reference's un-centred
-    H_res + H_post sum loses 0.02-0.12 there and 0.18-1.2 at init)."""
+    bf16 mHC must be within 2x that AND within MHC_BF16_BOUND = 1.5e-2 rel-L2, 3x HIP's own
+    measured level (0.003 init / 0.005 wc: the centred coefficients keep HIP at the bf16 level,
+    while the reference's un-centred H_res + H_post sum loses 0.02-0.12 on wc and 0.18-1.2 at
+    init, so a 2x-reference bound alone would pass a 100x regression)."""
     from conftest import record_parity
     from hv_amd import ManifoldHyperConnection
     g = golden(f"mhc_{fam}_D{D}_e{e}")
@@ -60,10 +64,88 @@ def test_mhc_bf16_agreement(gpu_device, fam, D, e):
     y = m(cases.mhc_input(D, e).to(gpu_device)).float().cpu().numpy()
     err, ref = rel_l2(y, g["y64"]), float(gb["err_vs_f64"])
     record_parity(f"mhc_bf16_{fam}_D{D}_e{e}", {"hip_bf16_vs_f64": err, "ref_bf16_vs_f64": ref,
-                                                 "ratio": err / ref, "bound_ratio": 2.0})
+                                                 "ratio": err / ref, "bound_ratio": 2.0, "bound_abs": MHC_BF16_BOUND})
     assert err <= 2.0 * ref, (err, ref)
-    if fam == "wc":
-        assert err < 5e-2
+    assert err <= MHC_BF16_BOUND, err
+
+
+def _mhc_variants(D, e):
+    """Every kernel that can run the (D, e) site, by the HV_MV_* bits that force it."""
+    from hv_amd import _lib as L
+    v = {"chain": None}
+    if D in (32, 64):
+        v.update({"pipe": L.MV_WIDE, "pipe_merge": L.MV_WIDE | L.MV_PIPE, "perwave": L.MV_WIDE | L.MV_PERWAVE,
+                  "perwave8": L.MV_WIDE | L.MV_ONE_GROUP8})
+    if (D, e) == (128, 4):
+        v.update({"split_hidden": L.MV_WIDE, "split_hidden_w": L.MV_WIDE | L.MV_SPLITW,
+                  "perwave": L.MV_WIDE | L.MV_PERWAVE128})
+    if (D, e) == (256, 2):
+        v.update({"split_hidden": L.MV_SPLIT256, "split_hidden_w": L.MV_SPLIT256 | L.MV_SPLITW,
+                  "perwave8": L.MV_WIDE})
+    if (D, e) in ((128, 4), (256, 2), (256, 4)):
+        v.update({"tok32": L.MV_TOK, "tok16": L.MV_TOK | L.MV_TOK16})
+    return v
+
+
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e", cases.MHC_CASES)
+def test_mhc_bf16_fixture_every_variant(gpu_device, fam, D, e):
+    """Each fused kernel FORCED (whatever the token-count policy would pick) on the reference's mHC
+    fixture, held to MHC_BF16_BOUND vs the reference fp64 run -- so a kernel the policy selects only
+    at large T still meets the reference, not only the HIP chain.  Per-variant errors go to
+    gpurun_out/parity/mhc_variants_<fam>_D<D>_e<e>.json (summary: profiles/r05/parity/)."""
+    from hv_amd import ManifoldHyperConnection, ops
+    g = golden(f"mhc_{fam}_D{D}_e{e}")
+    gb = golden(f"mhc_{fam}_D{D}_e{e}_bf16ref")
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
+    W.load_formula_weights(m, fam)
+    m = m.to(gpu_device).eval()
+    x = cases.mhc_input(D, e).to(gpu_device).to(torch.bfloat16)
+    rec = {"ref_bf16_vs_f64": float(gb["err_vs_f64"]), "bound": MHC_BF16_BOUND}
+    for name, v in _mhc_variants(D, e).items():
+        with torch.no_grad():
+            ops.launch_counts(reset=True)
+            if v is None:
+                with run_options(use_fused_mhc=False):
+                    y = m.forward_tokens(x)
+            else:
+                with run_options(mhc_variant=v):
+                    y = m.forward_tokens(x)
+            fused = ops.launch_counts()["mhc_fused"]
+        assert fused == (0 if v is None else 1), (name, fused)
+        err = rel_l2(y.float().cpu().numpy(), g["y64"])
+        rec[name] = {"hip_bf16_vs_f64": err, "ratio_to_ref_bf16": err / rec["ref_bf16_vs_f64"]}
+        assert err <= MHC_BF16_BOUND, (name, err)
+    record_parity(f"mhc_variants_{fam}_D{D}_e{e}", rec)
+
+
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e,T", cases.MHC_LARGE_CASES)
+def test_mhc_bf16_large_T_reference(gpu_device, fam, D, e, T):
+    """The automatic kernel policy at the token counts that select each large-T kernel
+    ((256, 2): token-tile 32 at 25,601, split-hidden at 102,401; (128, 4): split-hidden; (256, 4):
+    the chain) against the reference's fp64 run (row subsample of fixture mhc_<fam>_D_e_T)."""
+    from hv_amd import ManifoldHyperConnection, _lib, ops
+    g = golden(f"mhc_{fam}_D{D}_e{e}_T{T}")
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
+    W.load_formula_weights(m, fam)
+    m = m.to(gpu_device).eval()
+    x = cases.mhc_input_large(D, e, T).to(gpu_device).to(torch.bfloat16)
+    expect = {(256, 2, 25601): _lib.MV_TOK, (256, 2, 102401): _lib.MV_SPLIT256, (128, 4, 25601): 0,
+              (256, 4, 25601): None}[(D, e, T)]
+    v = ops._mhc_variant(D, T, None, D * e)
+    if expect is None:
+        assert not ops.mhc_fused_supported(D, D * e, torch.bfloat16, T=T)
+    else:
+        assert v == expect, hex(v)
+    with torch.no_grad():
+        ops.launch_counts(reset=True)
+        y = m(x)
+        assert ops.launch_counts()["mhc_fused"] == (0 if expect is None else 1)
+    rows = torch.from_numpy(g["rows"]).to(gpu_device)
+    err = rel_l2(y[rows].float().cpu().numpy(), g["y64"])
+    record_parity(f"mhc_large_{fam}_D{D}_e{e}_T{T}", {"variant": v, "hip_bf16_vs_f64": err, "bound": MHC_BF16_BOUND})
+    assert err <= MHC_BF16_BOUND, err
 
 
 @pytest.mark.parametrize("D,e,T,with_res", [(32, 4, 64, False), (32, 4, 1000, False), (64, 4, 64, False),
@@ -85,6 +167,57 @@ def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, e, T, with_res):
             y0 = m.forward_tokens(x, residual=res).float().cpu().numpy()
     assert rel_l2(y1, y0) < 1e-2
     assert np.abs(y1 - y0).max() < 0.1
+
+
+@pytest.mark.parametrize("tile", [16, 32])
+@pytest.mark.parametrize("D,e,T,with_res", [(256, 2, 401, False), (256, 2, 401, True), (256, 2, 6416, True),
+                                             (256, 2, 130, False), (256, 2, 7, True), (128, 4, 1000, False),
+                                             (128, 4, 6400, True), (256, 4, 1600, True), (256, 4, 77, False)])
+def test_mhc_tok_kernel_matches_unfused_chain(gpu_device, tile, D, e, T, with_res):
+    """Token-tile fused kernel (HV_MV_TOK, csrc/hv_mhc_tok.hip: 16 / 32 tokens per workgroup,
+    weights streamed L2 -> LDS transposer -> MFMA) vs the unfused bf16 chain, ragged T included.
+    Hd = 1024 always runs 16-token tiles."""
+    from hv_amd import ManifoldHyperConnection, _lib
+    m = ManifoldHyperConnection(D, expansion_rate=e, use_mixed_precision=True)
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    g = torch.Generator().manual_seed(T + D)
+    x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
+    res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
+    v = _lib.MV_TOK | (_lib.MV_TOK16 if tile == 16 else 0)
+    from hv_amd import ops
+    with torch.no_grad():
+        ops.launch_counts(reset=True)
+        with run_options(mhc_variant=v):
+            y1 = m.forward_tokens(x, residual=res).float().cpu().numpy()
+        assert ops.launch_counts()["mhc_fused"] == 1
+        with run_options(use_fused_mhc=False):
+            y0 = m.forward_tokens(x, residual=res).float().cpu().numpy()
+    assert rel_l2(y1, y0) < 1e-2
+    assert np.abs(y1 - y0).max() < 0.1
+
+
+@pytest.mark.parametrize("T", [401, 6416, 33])
+def test_mhc_tok_group_equals_single_launches(gpu_device, T):
+    """hv_mhc_fused_group: q / k / v (three sites on one x) in ONE launch give the same bits as
+    three single launches of the token-tile kernel, and the attention block takes that path."""
+    from hv_amd import ManifoldHyperConnection, _lib, ops
+    from hv_amd.runtime import HVOptions, RunCtx, use_ctx
+    ms = []
+    for i in range(3):
+        m = ManifoldHyperConnection(256, expansion_rate=2)
+        W.load_formula_weights(m, "wc" if i != 1 else "init")
+        ms.append(m.to(gpu_device).eval())
+    x = torch.randn(T, 256, generator=torch.Generator().manual_seed(T)).to(torch.bfloat16).to(gpu_device)
+    with torch.no_grad():
+        for v in (_lib.MV_TOK, _lib.MV_TOK | _lib.MV_TOK16):
+            with use_ctx(RunCtx(dtype=torch.bfloat16, opts=HVOptions(mhc_variant=v))):
+                plans = [m.plan() for m in ms]
+                outs = ops.mhc_fused_group(x, plans, v)
+                singles = [ops.mhc_fused(x, p.b1, p.c1, p.w2, p.bias2, p.wct, p.g_post, p.b_post, variant=v)
+                           for p in plans]
+            for a, b in zip(outs, singles):
+                assert torch.equal(a, b)
 
 
 def test_convmhc_and_blocks_fp32(gpu_device):
@@ -180,7 +313,8 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
       * at 640 they are ALSO held to the reference's own bf16 numerics (fixture
         model_base_wc_640_b2_bf16ref: the reference under CUDA autocast's bf16 policy, S8):
         logits (vs fp64), boxes (vs the reference fp32 run) and final features no worse than
-        the reference's own bf16 error (ratio <= 1.0; measured ~0.25-0.35), class agreement no
+        the reference's own bf16 error (ratio <= 0.5; measured 0.24-0.27, final features 0.09),
+        class agreement no
         lower;
       * the fp32 HIP path on the same batch meets the fp32 contract on those images (atol 1e-3),
         and on EVERY image of the batch the bf16 step stays near the fp32 step: logits rel-L2
@@ -235,7 +369,7 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
             anchor[f"scale_{s}"] = {"logits_hip": round(e_log, 5), "logits_ref_bf16": round(r_log, 5),
                                     "logits_ratio": round(e_log / r_log, 4), "boxes_hip": round(e_box, 5),
                                     "boxes_ref_bf16": round(r_box, 5), "boxes_ratio": round(e_box / r_box, 4)}
-            assert e_log <= 1.0 * r_log and e_box <= 1.0 * r_box, (s, anchor[f"scale_{s}"])
+            assert e_log <= 0.5 * r_log and e_box <= 0.5 * r_box, (s, anchor[f"scale_{s}"])
         ci = b16["cls"][f"scale_{s}"][:nref]
         sure = g[f"margin{s}"] >= 1e-2
         if sure.any():
@@ -248,9 +382,9 @@ def test_timed_step_graph_matches_reference(gpu_device, S, B, fixture, nref):
         r_fin = float(gb["final_err_vs_f64"])
         anchor["final_features"] = {"hip": round(e_fin, 5), "ref_bf16": round(r_fin, 5), "ratio": round(e_fin / r_fin, 4)}
         anchor["class_agreement_ref_bf16"] = [round(float(a), 5) for a in gb["class_agreement_margin_1e-2"]]
-        anchor["bound"] = "HIP bf16 error <= 1.0x the reference's own bf16 error (S8) on every output"
+        anchor["bound"] = "HIP bf16 error <= 0.5x the reference's own bf16 error (S8) on every output"
         rec["vs_reference_bf16"] = anchor
-        assert e_fin <= 1.0 * r_fin, anchor
+        assert e_fin <= 0.5 * r_fin, anchor
         assert min(agree) >= min(gb["class_agreement_margin_1e-2"]), (agree, anchor)
     m32 = _build("base", "wc", "fp32", gpu_device)
     with torch.no_grad():
@@ -592,7 +726,8 @@ def test_mhc_fused_split_hidden_d256_and_splitw(gpu_device, D, e, T, with_res):
     g = torch.Generator().manual_seed(T + D)
     x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
     res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
-    v = _lib.MV_SPLIT256 if D == 256 else 0
+    # forced: the automatic policy takes the token-tile kernel at these D = 128 token counts
+    v = _lib.MV_SPLIT256 if D == 256 else _lib.MV_WIDE
     with torch.no_grad():
         with run_options(mhc_variant=v):
             ops.launch_counts(reset=True)

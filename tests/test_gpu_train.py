@@ -877,6 +877,33 @@ def test_trainer_graph_dropout_masks_change_per_replay(gpu_device):
     assert res[False][1] == res[False][2] == res[False][3]
 
 
+def test_trainer_graph_recaptures_on_hyperparameter_change(gpu_device):
+    """A captured step carries lr / weight decay / betas / eps / clip norms and the model's kernel
+    variants by value: changing opt.lr between replays (a scheduler), or model.set_options(),
+    must re-capture -- with lr = wd = 0 after the change the parameters stay bit-identical, which
+    a stale replay at lr = 1e-3 would not give.  step_count counts steps, not captures."""
+    from hv_amd.targets import synthetic_targets
+    from hv_amd.trainer import HVTrainer
+    m, _ = _tiny_model(gpu_device, "bf16")
+    tr = HVTrainer(m, lr=1e-3, monitor_every=0, graph=True)
+    B, S = 2, 96
+    x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(9)).to(gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=9)]
+    for _ in range(3):
+        tr.step(x, tg)
+    assert tr.captures == 1 and tr.replays == 2 and tr.opt.step_count == 3
+    tr.opt.lr, tr.opt.wd = 0.0, 0.0
+    before = [p.detach().clone() for p in m.parameters()]
+    tr.step(x, tg)
+    torch.cuda.synchronize()
+    assert tr.captures == 2 and tr.opt.step_count == 4
+    for a, p in zip(before, m.parameters()):
+        assert torch.equal(a, p)
+    m.set_options(use_fused_mhc=False)
+    tr.step(x, tg)
+    assert tr.captures == 3 and tr.opt.step_count == 5
+
+
 def test_trainer_skips_parameters_without_gradient(gpu_device):
     """final_fusion / output_projection feed no loss term, so their gradients stay None in the
     reference and torch.optim / ManifoldAwareOptimizer (optimizer.py:144) skip them: no weight

@@ -59,6 +59,23 @@ def test_mhc_oracle_matches_reference(fam, D, e):
     np.testing.assert_allclose(y64.float().numpy(), g["y64"], rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("fam", ["wc", "init"])
+@pytest.mark.parametrize("D,e,T", cases.MHC_LARGE_CASES)
+def test_mhc_oracle_matches_reference_large_T(fam, D, e, T):
+    """The large-T fixtures (the kernel-policy thresholds): the regenerated input matches the
+    one the reference ran on (checksums), and the oracle's fp64 chain on the stored row subsample
+    reproduces the reference's fp64 rows (the chain is per token)."""
+    g = golden(f"mhc_{fam}_D{D}_e{e}_T{T}")
+    x = cases.mhc_input_large(D, e, T)
+    assert int(g["T"]) == T
+    assert float(x.double().sum()) == float(g["x_sum"]) and float(x.double().abs().sum()) == float(g["x_abs_sum"])
+    rows = torch.from_numpy(g["rows"])
+    assert torch.equal(rows, cases.mhc_large_rows(T))
+    sd64 = O.cast_state_dict(_mhc_sd(D, e, fam), torch.float64)
+    y64 = O.mhc(sd64, "", x[rows].double(), 20)
+    np.testing.assert_allclose(y64.float().numpy(), g["y64"], rtol=0, atol=2e-5)
+
+
 def _module_sd(names_shapes, fam):
     return {n: W.make_tensor(n, s, fam) for n, s in names_shapes}
 
