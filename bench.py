@@ -170,22 +170,26 @@ def pmc_child(a):
     torch.cuda.synchronize()
 
 
-def cpu_baseline(model_cpu_sd, size, threads, batch=16):
+def cpu_baseline(model_cpu_sd, size, threads, batch=4, iters=3):
     """Oracle (CPU restatement of the reference path) on the host cores: a bounded sample of the
-    SAME workload as the GPU line -- one batch of `batch` images (config B: 16) -- after a
-    single-image warmup."""
+    SAME workload as the GPU line (640x640 fp32 forward, same weights) -- `iters` timed batches of
+    `batch` images after a 1-image warmup (>= 3 timed iterations after a warmup),
+    the median batch giving the rate; about 15-20 s of CPU work on 16 cores."""
     from oracle import hv_oracle as O
     torch.set_num_threads(threads)
     x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(1))
+    ts = []
     with torch.no_grad():
         O.system_forward(model_cpu_sd, x[:1], O.BASE)      # warmup
-        t0 = time.perf_counter()
-        O.system_forward(model_cpu_sd, x, O.BASE)
-        dt = time.perf_counter() - t0
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            O.system_forward(model_cpu_sd, x, O.BASE)
+            ts.append(time.perf_counter() - t0)
+    dt = sorted(ts)[len(ts) // 2]
     return {"value": round(batch / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"one batch of {batch} {size}x{size} images (config B's batch), fp32 forward of the "
-                      f"oracle (oracle/hv_oracle.py), same random-init weights, after a 1-image warmup; "
-                      f"{dt:.1f} s"}
+            "sample": f"{iters} timed batches of {batch} {size}x{size} images after a 1-image warmup, median "
+                      f"batch {dt:.2f} s (all: {', '.join(f'{t:.2f}' for t in ts)} s); fp32 forward of the "
+                      f"oracle (oracle/hv_oracle.py), same random-init weights as the GPU line"}
 
 
 def _sync_time(world, dev, fn):

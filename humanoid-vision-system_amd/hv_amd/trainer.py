@@ -452,9 +452,12 @@ class HVTrainer:
         self.opt = FusedAdamW(named, lr, weight_decay, betas, eps, (mhc_max_norm, max_grad_norm))
         self.world = self.grads.world
         self.group = group
-        # DDP averaging: the loss is scaled by 1/world before the backward (exact for power-of-two
-        # worlds), so the bucket all-reduces sum with no division pass over the gradients
-        self.grads.prescaled = self.world > 1
+        # DDP averaging.  Power-of-two worlds: the loss is scaled by 1/world before the backward
+        # (exact: a power-of-two scale commutes with every rounding), so the bucket all-reduces
+        # sum with no division pass over the gradients.  Other worlds: each bucket is divided by
+        # the world right before its all-reduce, as torch DDP's allreduce hook does (a 1/3 loss
+        # scale would round differently from DDP's averaging)
+        self.grads.prescaled = self.world > 1 and (self.world & (self.world - 1)) == 0
         self.broadcast_buffers = broadcast_buffers and self.world > 1
         if self.world > 1:                         # DDP construction: replicas start identical
             self._broadcast(list(model.parameters()) + list(model.buffers()))
@@ -543,7 +546,7 @@ class HVTrainer:
             self.last_predictions = {k: v.detach() for k, v in out.get("predictions", {}).items()}
             loss = out["loss"]
             total = loss["total_loss"]
-            (total * (1.0 / self.world) if self.world > 1 else total).backward()
+            (total * (1.0 / self.world) if self.grads.prescaled else total).backward()
             self.grads.finish()
             self.opt.step(clip=True, active=self.grads.active_dev)
         finally:

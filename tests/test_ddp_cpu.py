@@ -159,13 +159,17 @@ def _trainer_worker(rank, world, port, q):
             res.append({"grads": {n: p.grad.detach().clone().numpy() for n, p in net.named_parameters()},
                         "bufs": {n: b.detach().clone().numpy() for n, b in net.named_buffers()},
                         "x": x.numpy(), "t": tgt.numpy()})
-        q.put((rank, init, bufs0, res, calls, [n for n, _ in tr.opt.named]))
+        q.put((rank, init, bufs0, res, calls, [n for n, _ in tr.opt.named], tr.grads.prescaled))
     finally:
         dist.destroy_process_group()
 
 
-def test_hvtrainer_ddp_broadcast_and_average():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_hvtrainer_ddp_broadcast_and_average(world):
+    """HVTrainer over gloo: construction broadcast, per-step buffer broadcast, averaged gradients
+    (== the mean of the per-rank gradients), received-gradient flags.  World 3: the 1/world loss
+    pre-scale is exact only for power-of-two worlds, so there each bucket is divided by the world
+    before its sum, as torch DDP's allreduce hook does -- the averages match DDP's rounding."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -176,14 +180,16 @@ def test_hvtrainer_ddp_broadcast_and_average():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, init0, buf0, res0, calls0, names), (_, init1, buf1, res1, calls1, _) = results
+    init0, buf0, names = results[0][1], results[0][2], results[0][5]
+    for r in results:
+        assert r[6] == (world & (world - 1) == 0)             # loss pre-scale only for 2^k worlds
     torch.manual_seed(0)
     ref_init = {n: p.detach().numpy() for n, p in TrainNet().named_parameters()}
-    for n in ref_init:                                    # construction: rank 0's parameters
-        torch.testing.assert_close(torch.from_numpy(init0[n]), torch.from_numpy(ref_init[n]))
-        torch.testing.assert_close(torch.from_numpy(init1[n]), torch.from_numpy(ref_init[n]))
-    for n in buf0:                                        # construction: rank 0's buffers
-        torch.testing.assert_close(torch.from_numpy(buf1[n]), torch.from_numpy(buf0[n]))
+    for r in results:
+        for n in ref_init:                                # construction: rank 0's parameters
+            torch.testing.assert_close(torch.from_numpy(r[1][n]), torch.from_numpy(ref_init[n]))
+        for n in buf0:                                    # construction: rank 0's buffers
+            torch.testing.assert_close(torch.from_numpy(r[2][n]), torch.from_numpy(buf0[n]))
     # reference: one replica on rank 0's state, each rank's batch with rank 0's buffers
     ref = TrainNet()
     ref.load_state_dict({**{k: torch.from_numpy(v) for k, v in init0.items()},
@@ -191,22 +197,25 @@ def test_hvtrainer_ddp_broadcast_and_average():
     ref.train()
     for step in range(2):
         start = {k: v.clone() for k, v in ref.state_dict().items()}
-        gsum, bufs = None, []
-        for r, res in ((0, res0), (1, res1)):
+        gs, bufs = [], []
+        for r in results:
             ref.load_state_dict(start)
             ref.zero_grad()
-            out = ref(torch.from_numpy(res[step]["x"]), torch.from_numpy(res[step]["t"]))
+            out = ref(torch.from_numpy(r[3][step]["x"]), torch.from_numpy(r[3][step]["t"]))
             out["loss"]["total_loss"].backward()
-            g = {n: (p.grad.clone() if p.grad is not None else torch.zeros_like(p)) for n, p in ref.named_parameters()}
-            gsum = g if gsum is None else {n: gsum[n] + g[n] for n in g}
+            gs.append({n: (p.grad.clone() if p.grad is not None else torch.zeros_like(p))
+                       for n, p in ref.named_parameters()})
             bufs.append({k: v.clone() for k, v in ref.named_buffers()})
-        for r, res in ((0, res0), (1, res1)):
-            for n, gv in res[step]["grads"].items():
-                torch.testing.assert_close(torch.from_numpy(gv), gsum[n] / 2, rtol=1e-5, atol=1e-6)
-            for n, bv in res[step]["bufs"].items():        # per-replica BN update from rank 0's stats
-                torch.testing.assert_close(torch.from_numpy(bv), bufs[r][n], rtol=1e-5, atol=1e-6)
+        # DDP's average: every rank's gradient divided by the world, then summed in rank order
+        avg = {n: sum(g[n] / world for g in gs) for n in gs[0]}
+        for ri, r in enumerate(results):
+            for n, gv in r[3][step]["grads"].items():
+                torch.testing.assert_close(torch.from_numpy(gv), avg[n], rtol=1e-5, atol=1e-6)
+            for n, bv in r[3][step]["bufs"].items():       # per-replica BN update from rank 0's stats
+                torch.testing.assert_close(torch.from_numpy(bv), bufs[ri][n], rtol=1e-5, atol=1e-6)
         ref.load_state_dict({**start, **{k: v for k, v in bufs[0].items()}})
-    for calls in (calls0, calls1):                         # optimizer sees which params got no grad
+    for r in results:                                      # optimizer sees which params got no grad
+        calls = r[4]
         assert len(calls) == 2
         for act in calls:
             assert dict(zip(names, act)) == {n: not n.startswith("unused.") for n in names}
