@@ -28,8 +28,11 @@ __device__ __forceinline__ uint32_t epi_seed(const hv_gemm_desc& d) {
 __device__ __forceinline__ float epi_train_act(const hv_gemm_desc& d, float z) {
   return (d.act == HV_ACT_GELU && d.c_dtype == HV_BF16) ? hv_gelu_fast(z) : hv_act(z, d.act);
 }
+// the backward differentiates the GELU its forward ran: that forward wrote its output in the dtype
+// of the stored pre-activation (aux, every mode-1 caller), which is not necessarily the dtype of
+// this launch's dX (c_dtype) -- the form is keyed on aux_dtype, as k_act_bwd keys on the pre-act
 __device__ __forceinline__ float epi_train_act_grad(const hv_gemm_desc& d, float z) {
-  return (d.act == HV_ACT_GELU && d.c_dtype == HV_BF16) ? hv_gelu_grad_fast(z) : hv_act_grad(z, d.act);
+  return (d.act == HV_ACT_GELU && d.aux_dtype == HV_BF16) ? hv_gelu_grad_fast(z) : hv_act_grad(z, d.act);
 }
 
 __device__ __forceinline__ f32x4 epi_train(const hv_gemm_desc& d, const f32x4 acc, int row, int col, const f32x4 sc,

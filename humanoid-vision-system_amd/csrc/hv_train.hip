@@ -56,6 +56,38 @@ __global__ void k_transpose_cast(const float* __restrict__ x, int rows, int cols
   }
 }
 
+// grouped transpose / cast (hv_transpose_group): 32x32 tiles of every entry of a device table;
+// a block finds its entry by binary search over the entries' first blocks
+__global__ void __launch_bounds__(256) k_transpose_group(const hv_transpose_entry* __restrict__ tab, int count) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.x;
+  int lo = 0, hi = count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].blk <= b) lo = mid; else hi = mid - 1;
+  }
+  const hv_transpose_entry& e = tab[lo];
+  const int tcols = (e.cols + 31) / 32, t = b - e.blk;
+  const int bx = (t % tcols) * 32, by = (t / tcols) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  if (!e.transpose) {
+    for (int r = ty; r < 32; r += 8) {
+      const int row = by + r, col = bx + tx;
+      if (row < e.rows && col < e.cols) st_dt(e.y, e.y_dtype, (long)row * e.cols + col, ld_dt(e.x, e.x_dtype, (long)row * e.cols + col));
+    }
+    return;
+  }
+  for (int r = ty; r < 32; r += 8) {
+    const int row = by + r, col = bx + tx;
+    tile[r][tx] = (row < e.rows && col < e.cols) ? ld_dt(e.x, e.x_dtype, (long)row * e.cols + col) : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int orow = bx + r, ocol = by + tx;                 // y[cols][rows]
+    if (orow < e.cols && ocol < e.rows) st_dt(e.y, e.y_dtype, (long)orow * e.rows + ocol, tile[tx][r]);
+  }
+}
+
 __global__ void k_conv_grad_reorder(const float* __restrict__ g, int cout, int cin, int k, float* y) {
   const long total = (long)cout * cin * k * k;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -154,58 +186,77 @@ __global__ void __launch_bounds__(256) k_colred(const ColRed r, int nblk, float*
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[v][c][j] = 0.f;
   if (rsub < rpi) {
-    for (long r0 = (long)blockIdx.x * rpi; r0 < r.rows; r0 += (long)nblk * rpi) {
-      const long row = r0 + rsub;
-      if (row >= r.rows) break;
-      float rmu = 0.f, rrs = 1.f;
-      if constexpr (MODE == CR_ROWN) {
-        rmu = r.mean ? r.mean[row] : 0.f;
-        rrs = r.rstd[row];
+    // U rows per trip: all their loads are issued before any is consumed (the one-load-per-trip
+    // loop ran at load latency); the values are then accumulated in the original row order, so
+    // the sums are bitwise those of the one-row loop
+    constexpr int U = NCH == 1 ? 4 : (NCH == 2 ? 2 : 1);
+    constexpr bool HASB = MODE != CR_SUM && MODE != CR_SUMSQ;
+    const long step = (long)nblk * rpi;
+    for (long r0 = (long)blockIdx.x * rpi; r0 < r.rows; r0 += U * step) {
+      float a[U][NCH][4], b[U][NCH][4];
+      float rmu[U], rrs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long row = r0 + u * step + rsub;
+        rmu[u] = 0.f;
+        rrs[u] = 1.f;
+        if (row >= r.rows) continue;
+        if constexpr (MODE == CR_ROWN) {
+          rmu[u] = r.mean ? r.mean[row] : 0.f;
+          rrs[u] = r.rstd[row];
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
+          if (ch >= cpr) continue;
+          const long o = base + row * r.cols + ch * 4;
+          ld4<TA>((const TA*)r.a, o, a[u][c]);
+          if constexpr (HASB) {
+            if (MODE != CR_DOT || r.b) ld4<TB>((const TB*)r.b, o, b[u][c]);
+          }
+        }
       }
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
-        if (ch >= cpr) continue;
-        const int col = ch * 4;
-        const long o = base + row * r.cols + col;
-        float a[4];
-        ld4<TA>((const TA*)r.a, o, a);
-        if constexpr (MODE == CR_SUM) {
+      for (int u = 0; u < U; ++u) {
+        const long row = r0 + u * step + rsub;
+        if (row >= r.rows) break;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
-        } else if constexpr (MODE == CR_SUMSQ) {
+        for (int c = 0; c < NCH; ++c) {
+          const int ch = cpr <= 256 ? tid % cpr : tid + 256 * c;
+          if (ch >= cpr) continue;
+          const int col = ch * 4;
+          const long o = base + row * r.cols + col;
+          if constexpr (MODE == CR_SUM) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { acc[0][c][j] += a[j]; acc[1][c][j] += a[j] * a[j]; }
-        } else if constexpr (MODE == CR_DOT) {
-          if (r.b) {
-            float b[4];
-            ld4<TB>((const TB*)r.b, o, b);
+            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j];
+          } else if constexpr (MODE == CR_SUMSQ) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j] * b[j];
-          } else {
+            for (int j = 0; j < 4; ++j) { acc[0][c][j] += a[u][c][j]; acc[1][c][j] += a[u][c][j] * a[u][c][j]; }
+          } else if constexpr (MODE == CR_DOT) {
+            if (r.b) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[0][c][j] += a[j];
-          }
-        } else if constexpr (MODE == CR_BNBWD) {
-          float b[4];
-          ld4<TB>((const TB*)r.b, o, b);
+              for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j] * b[u][c][j];
+            } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int cc = col + j;
-            const float xh = (a[j] - r.mean[cc]) * r.rstd[cc];
-            const float g = b[j] * hv_act_grad(xh * (r.gamma ? r.gamma[cc] : 1.f) + (r.beta ? r.beta[cc] : 0.f), r.act);
-            acc[0][c][j] += g;
-            acc[1][c][j] += g * xh;
-          }
-        } else {  // CR_ROWN
-          float b[4];
-          ld4<TB>((const TB*)r.b, o, b);
+              for (int j = 0; j < 4; ++j) acc[0][c][j] += a[u][c][j];
+            }
+          } else if constexpr (MODE == CR_BNBWD) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float xh = (a[j] - rmu) * rrs;
-            const float g = b[j] * hv_drop_scale(hv_seed(r.seed, r.soff), (unsigned long long)(o + j), r.p);
-            acc[0][c][j] += g * xh;
-            acc[1][c][j] += g;
+            for (int j = 0; j < 4; ++j) {
+              const int cc = col + j;
+              const float xh = (a[u][c][j] - r.mean[cc]) * r.rstd[cc];
+              const float g = b[u][c][j] * hv_act_grad(xh * (r.gamma ? r.gamma[cc] : 1.f) + (r.beta ? r.beta[cc] : 0.f), r.act);
+              acc[0][c][j] += g;
+              acc[1][c][j] += g * xh;
+            }
+          } else {  // CR_ROWN
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float xh = (a[u][c][j] - rmu[u]) * rrs[u];
+              const float g = b[u][c][j] * hv_drop_scale(hv_seed(r.seed, r.soff), (unsigned long long)(o + j), r.p);
+              acc[0][c][j] += g * xh;
+              acc[1][c][j] += g;
+            }
           }
         }
       }
@@ -964,6 +1015,17 @@ extern "C" int hv_transpose_cast(const float* x, int rows, int cols, int y_dtype
   if (!x || !y || rows <= 0 || cols <= 0) return HV_EINVAL;
   dim3 grid(hv_cdiv(cols, 32), hv_cdiv(rows, 32));
   k_transpose_cast<<<grid, 256, 0, (hipStream_t)stream>>>(x, rows, cols, y_dtype, y);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_transpose_blocks(int rows, int cols) {
+  return (rows <= 0 || cols <= 0) ? 0 : (int)(hv_cdiv(rows, 32) * hv_cdiv(cols, 32));
+}
+
+extern "C" int hv_transpose_group(const hv_transpose_entry* tab, int count, int total_blocks, hv_stream_t stream) {
+  if (!tab || count <= 0 || total_blocks <= 0) return HV_EINVAL;
+  k_transpose_group<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

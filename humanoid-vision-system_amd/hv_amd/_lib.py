@@ -128,6 +128,11 @@ class MhcPrepEntry(C.Structure):
                 ("D", i32), ("Hd", i32), ("fold", i32), ("pad_", i32), ("blk", i32 * 4)]
 
 
+class TransposeEntry(C.Structure):
+    _fields_ = [("x", vp), ("y", vp), ("rows", i32), ("cols", i32), ("x_dtype", i32), ("y_dtype", i32),
+                ("transpose", i32), ("blk", i32)]
+
+
 class WprepEntry(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("gamma", vp), ("beta", vp), ("mean", vp), ("var", vp),
                 ("cbias", vp), ("scale_out", vp), ("bias_out", vp), ("n", i64),
@@ -144,6 +149,8 @@ _SIGS = {
     "hv_mhc_fused_supported": ([i32, i32, i32, i32], i32),
     "hv_mhc_fused": ([vp, vp], i32),
     "hv_mhc_fused_group": ([vp, i32, vp], i32),
+    "hv_transpose_blocks": ([i32, i32], i32),
+    "hv_transpose_group": ([vp, i32, i32, vp], i32),
     "hv_diag_launch_counts": ([vp], None),
     "hv_diag_reset_counts": ([], None),
     "hv_abi_version": ([], i32),

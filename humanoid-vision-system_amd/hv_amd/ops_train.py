@@ -172,8 +172,17 @@ def transpose_cast(x: Tensor, dtype: torch.dtype) -> Tensor:
     return y
 
 
-def conv_grad_reorder(g: Tensor, cout: int, cin: int, k: int) -> Tensor:
-    y = torch.empty((cout, cin, k, k), device=g.device, dtype=torch.float32)
+def grad_out(p: Tensor) -> Optional[Tensor]:
+    """Destination for parameter p's gradient: a fresh view of the trainer's flat gradient buffer
+    the first time p's gradient is produced in a step (trainer.GradBuckets: autograd then stores that
+    view as p.grad and no bucket copy runs), else None (no trainer, or a second contribution, which
+    autograd accumulates into the first)."""
+    claim = getattr(p, "_hv_grad_claim", None)
+    return None if claim is None else claim()
+
+
+def conv_grad_reorder(g: Tensor, cout: int, cin: int, k: int, out: Optional[Tensor] = None) -> Tensor:
+    y = out if out is not None else torch.empty((cout, cin, k, k), device=g.device, dtype=torch.float32)
     check(L.lib().hv_conv_grad_reorder(_contig(g, "g").data_ptr(), cout, cin, k, y.data_ptr(), stream_ptr()),
           "hv_conv_grad_reorder")
     return y

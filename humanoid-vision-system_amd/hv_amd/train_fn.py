@@ -81,7 +81,8 @@ class ConvFn(torch.autograd.Function):
             wt = T.dgrad_weight(wpad, dpre.dtype, flip)
             dx = T.conv_dgrad(dpre, wt, k, s, p, in_hw, flipped=flip)
         if _need(ctx, 1):
-            dw = T.conv_grad_reorder(T.conv_wgrad(dpre, x, k, s, p), cp, cin, k)[:cout]
+            dst = T.grad_out(weight) if cp == cout else None
+            dw = T.conv_grad_reorder(T.conv_wgrad(dpre, x, k, s, p), cp, cin, k, out=dst)[:cout]
         if _need(ctx, 2):
             db = T.colsum(dpre)[:cout]
         return dx, dw, db, dgamma, dbeta, None, None, None
@@ -126,7 +127,7 @@ class LinearFn(torch.autograd.Function):
         if _need(ctx, 0):
             dx = ops.gemm(g, T.transpose_cast(weight, dt))
         if _need(ctx, 1):
-            dw = T.wgrad(g, x)
+            dw = T.wgrad(g, x, out=T.grad_out(weight))
         if _need(ctx, 2):
             db = T.colsum(g)
         return dx, dw, db, None, None, None, None
@@ -178,16 +179,23 @@ class MhcFn(torch.autograd.Function):
     gradients down to H_pre_raw / H_post_raw / H_res)."""
 
     @staticmethod
-    def forward(ctx, x, H_res, H_pre_raw, H_post_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post, m, seeds):
+    def forward(ctx, x, H_res, H_pre_raw, H_post_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post, m, seeds,
+                coef=None):
         dt = x.dtype
         D, Hd = m.input_dim, m.hidden_dim
         p1, p2, p3 = m.mlp[2].p, m.mlp[5].p, m.dropout.p
         s1, s2, s3 = seeds
         with torch.no_grad():
-            gc, u, wct, A1, c1 = _mhc_coefficients(m, H_res, W1, b1, dt)
-            a1t = T.transpose_cast(A1, dt)                  # [2Hd, D]
-            w2 = ops.cast(f32(W2), dt)
-            wct_dt = ops.cast(wct, dt)                      # [D, D+Hd]
+            if coef is not None:                            # grouped prep of the whole model (train_prep)
+                gc = u = wct = A1 = None
+                a1t, c1, w2, wct_dt = coef.a1t, coef.c1, coef.w2, coef.wct
+                ctx.coef, ctx.coef_gen = coef, coef.gen
+            else:
+                gc, u, wct, A1, c1 = _mhc_coefficients(m, H_res, W1, b1, dt)
+                a1t = T.transpose_cast(A1, dt)              # [2Hd, D]
+                w2 = ops.cast(f32(W2), dt)
+                wct_dt = ops.cast(wct, dt)                  # [D, D+Hd]
+                ctx.coef = None
             z, mean, rstd = T.rownorm_train(T.LN, x, 1e-5)
             pre1 = torch.empty((x.shape[0], 2 * Hd), device=x.device, dtype=dt)
             h1 = T.gemm_train(z, a1t, mode=1, act="gelu", aux=pre1, bias=c1, drop_p=p1, seed=s1)
@@ -211,40 +219,50 @@ class MhcFn(torch.autograd.Function):
         dt = x.dtype
         dy = dy.contiguous()
         # LN_post (+ output dropout)
+        co = ctx.coef
+        if co is not None and co.gen != ctx.coef_gen:
+            raise RuntimeError("MhcFn.backward: the grouped training coefficients were recomputed by a later "
+                               "forward before this backward (one forward per backward)")
         dyc, dg_post, db_post = T.rownorm_backward(T.LN, yc, dy, mean2, rstd2, g_post, p3, s3, dx_dtype=dt)
-        wc = T.transpose_cast(wct, dt)                     # [D+Hd, D] (rows = input index)
+        wc = co.wc if co is not None else T.transpose_cast(wct, dt)     # [D+Hd, D] (rows = input index)
         dwc_x = T.wgrad(x, dyc)                            # [D, D]
         dwc_h = T.wgrad(h2, dyc)                           # [Hd, D]
         dx_res = ops.gemm(dyc, wc[:D])                     # [T, D]
         dpre2 = T.gemm_train(dyc, wc[D:], mode=2, act="gelu", aux=pre2, drop_p=p2, seed=s2)
-        dW2 = T.wgrad(dpre2, h1)                           # [Hd, 2Hd]
+        dW2 = T.wgrad(dpre2, h1, out=T.grad_out(W2))       # [Hd, 2Hd]
         db2 = T.colsum(dpre2)
-        w2t = T.transpose_cast(W2, dt)                     # [2Hd, Hd]
+        w2t = co.w2t if co is not None else T.transpose_cast(W2, dt)    # [2Hd, Hd]
         dpre1 = T.gemm_train(dpre2, w2t, mode=2, act="gelu", aux=pre1, drop_p=p1, seed=s1)
         dA1t = T.wgrad(dpre1, z)                           # [2Hd, D]
         dc1 = T.colsum(dpre1)
-        dz = ops.gemm(dpre1, ops.cast(A1, dt))             # [T, D]
+        dz = ops.gemm(dpre1, co.a1 if co is not None else ops.cast(A1, dt))   # [T, D]
         dx, _, _ = T.rownorm_backward(T.LN, x, dz, mean, rstd, None, dx_dtype=dt, dx_add=dx_res,
                                       param_grads=False)
         # ---- coefficient backward (parameter-sized fp32)
         w1 = f32(W1)
         pdt = torch.bfloat16 if dt == torch.bfloat16 else torch.float32   # parameter-side GEMM operands
-        dW1 = ops.gemm(ops.cast(dA1t, pdt), T.transpose_cast(gc, pdt), out_dtype=torch.float32)  # dA1t Gc
+        if co is not None:
+            gct, w1t, u = co.gct, co.w1t, co.u
+        else:
+            gct, w1t = T.transpose_cast(gc, pdt), T.transpose_cast(w1, torch.float32)
+        dW1 = ops.gemm(ops.cast(dA1t, pdt), gct, out_dtype=torch.float32)  # dA1t Gc
         dW1 += torch.outer(dc1, u)
         db1 = dc1
         dGc = T.wgrad(dA1t, w1)                            # [D, Hd] = dA1t^T W1
-        du = ops.gemv(T.transpose_cast(w1, torch.float32), dc1)   # [Hd] = W1^T dc1 (hv_gemv)
+        du = ops.gemv(w1t, dc1)                            # [Hd] = W1^T dc1 (hv_gemv)
         dH_pre_raw, dg_pre, db_pre, dH_res, dH_post_raw = T.mhc_param_backward(
             dGc, du, H_pre_raw, g_pre, b_pre, dwc_x, dwc_h, H_post_raw)
         return (dx, dH_res, dH_pre_raw, dH_post_raw, dg_pre, db_pre, dW1, db1, dW2, db2, dg_post, db_post,
-                None, None)
+                None, None, None)
 
 
-def mhc(m, x: Tensor, H_res: Tensor) -> Tensor:
+def mhc(m, x: Tensor, H_res: Tensor, coef=None) -> Tensor:
+    """coef: the site's train_prep.TrainCoef when the model's coefficients were prepared in one
+    grouped pass (train_model.system_forward), else None (per-site preparation)."""
     seeds = tuple(next_seed() if pp > 0 else 0 for pp in (m.mlp[2].p, m.mlp[5].p, m.dropout.p))
     y = MhcFn.apply(x, H_res, m.H_pre_raw, m.H_post_raw, m.norm_pre.weight, m.norm_pre.bias,
                     m.mlp[0].weight, m.mlp[0].bias, m.mlp[3].weight, m.mlp[3].bias,
-                    m.norm_post.weight, m.norm_post.bias, m, seeds)
+                    m.norm_post.weight, m.norm_post.bias, m, seeds, coef)
     if m.training:                                   # a4: manifold_layers.py:275-276 (throttled)
         cnt = getattr(m, "_mon_count", 0)
         m._mon_count = cnt + 1

@@ -23,14 +23,43 @@ from .manifold import flush_stability
 from .runtime import PRECISIONS
 
 
-def _hres_table(model) -> Dict[int, torch.Tensor]:
+class HTable(dict):
+    """id(mHC) -> its differentiable H_res (this forward's grouped Sinkhorn output); `coefs` holds
+    the sites' grouped training coefficients (train_prep.TrainCoef) when they were prepared."""
+    coefs: Dict[int, Any] = {}
+
+
+def _hres_table(model) -> HTable:
+    """Grouped differentiable Sinkhorn of all 76 sites + (model.hv_train_group_prep, default on)
+    the grouped training coefficient prep of train_prep.TrainPrep over its outputs.  The Sinkhorn
+    group and the prep program are cached on the model while the parameter storage is unchanged,
+    so their buffers (and a captured training graph's pointers) stay put."""
+    from .train_prep import TrainPrep
     mods = model._mhc_modules
     raws = [m.H_res_raw for m in mods]
-    group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
-                              raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
-                              hists=[m.sinkhorn.convergence_history for m in mods])
+    dt = PRECISIONS[model.hv_precision]
+    cache = model.__dict__.setdefault("_train_prep_cache", {})
+    key = (tuple(r.data_ptr() for r in raws), tuple(m.sinkhorn.convergence_history.data_ptr() for m in mods))
+    group = cache.get("sk") if cache.get("sk_key") == key else None
+    if group is None:
+        group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
+                                  raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
+                                  hists=[m.sinkhorn.convergence_history for m in mods])
+        cache["sk"], cache["sk_key"], cache["prep"] = group, key, None
     outs = TF.SinkhornGroupFn.apply(group, *raws)
-    return {id(m): h for m, h in zip(mods, outs)}
+    H = HTable({id(m): h for m, h in zip(mods, outs)})
+    H.coefs = {}
+    if getattr(model, "hv_train_group_prep", True):
+        prep = cache.get("prep")
+        if prep is None or not prep.valid_for(mods, outs, dt):
+            prep = cache["prep"] = TrainPrep(mods, [o.detach() for o in outs], dt)
+        H.coefs = prep.run()
+    return H
+
+
+def _mhc(m, x: torch.Tensor, H) -> torch.Tensor:
+    """TF.mhc with the site's grouped coefficients when the table carries them."""
+    return TF.mhc(m, x, H[id(m)], getattr(H, "coefs", {}).get(id(m)))
 
 
 def module_H(module) -> Dict[int, torch.Tensor]:
@@ -55,7 +84,7 @@ def nhwc_in(x: torch.Tensor, dtype) -> torch.Tensor:
 
 def _tok(m, x: torch.Tensor, H) -> torch.Tensor:
     n, h, w, c = x.shape
-    return TF.mhc(m, x.reshape(-1, c), H[id(m)]).view(n, h, w, c)
+    return _mhc(m, x.reshape(-1, c), H).view(n, h, w, c)
 
 
 def _dropout2d(x: torch.Tensor, p: float) -> torch.Tensor:
@@ -142,25 +171,25 @@ def _positions(pe: torch.Tensor, tokens: int) -> torch.Tensor:
 def attention(a, x, n, H):
     """MultiHeadManifoldAttention.forward (manifold_layers.py:386-434) on x [n*L, D]."""
     L = x.shape[0] // n
-    q = TF.mhc(a.q_proj, x, H[id(a.q_proj)]).view(n, L, -1)
-    k = TF.mhc(a.k_proj, x, H[id(a.k_proj)]).view(n, L, -1)
-    v = TF.mhc(a.v_proj, x, H[id(a.v_proj)]).view(n, L, -1)
+    q = _mhc(a.q_proj, x, H).view(n, L, -1)
+    k = _mhc(a.k_proj, x, H).view(n, L, -1)
+    v = _mhc(a.v_proj, x, H).view(n, L, -1)
     p = a.dropout.p
     o = TF.AttentionFn.apply(q, k, v, a.num_heads, p, TF.next_seed() if p > 0 else 0)
-    return TF.mhc(a.out_proj, o.reshape(n * L, -1), H[id(a.out_proj)])
+    return _mhc(a.out_proj, o.reshape(n * L, -1), H)
 
 
 def encoder_block(blk, x, n, H):
     """TransformerEncoderBlock.forward (vit_encoder_decoder.py:174-210)."""
     h = TF.RMSNormFn.apply(x, blk.norm1.scale, blk.norm1.eps)
     a = attention(blk.attention, h, n, H)
-    a = TF.mhc(blk.residual_mhc1, a, H[id(blk.residual_mhc1)])
+    a = _mhc(blk.residual_mhc1, a, H)
     p = blk.dropout.p
     x = TF.DropAddFn.apply(x, a, p, TF.next_seed() if p > 0 else 0)
     h = TF.RMSNormFn.apply(x, blk.norm2.scale, blk.norm2.eps)
     h = TF.linear(h, blk.mlp[0], act="gelu", p=blk.mlp[2].p)
     h = TF.linear(h, blk.mlp[3], act="none", p=blk.mlp[4].p)
-    h = TF.mhc(blk.residual_mhc2, h, H[id(blk.residual_mhc2)])
+    h = _mhc(blk.residual_mhc2, h, H)
     return TF.DropAddFn.apply(x, h, p, TF.next_seed() if p > 0 else 0)
 
 
@@ -170,7 +199,7 @@ def vit_encoder(enc, x, H, features=None, head: bool = True):
     pe = enc.patch_embed
     t = TF.conv(x, pe.projection)
     n, h, w, d = t.shape
-    t = TF.mhc(pe.mhc_enhance, t.reshape(-1, d), H[id(pe.mhc_enhance)]).view(n, h * w, d)
+    t = _mhc(pe.mhc_enhance, t.reshape(-1, d), H).view(n, h * w, d)
     pos = _positions(pe.position_embeddings, h * w)
     z = TF.VitAssembleFn.apply(t, pe.cls_token, pos)
     L = h * w + 1

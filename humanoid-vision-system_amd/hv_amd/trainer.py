@@ -114,6 +114,23 @@ class GradBuckets:
         # gradient itself in a tensor hook; bucket readiness is counted in the post-accumulate hook
         self._hooks = [p.register_hook(self._flag_hook(i)) for i, p in enumerate(self.params)]
         self._hooks += [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        # zero-copy gradients: the largest producers (weight-gradient GEMMs, ops_train.grad_out)
+        # write their first contribution of a step straight into the parameter's flat view, which
+        # autograd then stores as .grad -- the bucket flush skips it (no hv_copy_segments bytes)
+        self._claimed = [False] * len(self.params)
+        for i, p in enumerate(self.params):
+            p._hv_grad_claim = self._claimer(i)
+
+    def _claimer(self, idx: int):
+        off, p = self.offsets[id(self.params[idx])], self.params[idx]
+        n, shape = p.numel(), tuple(p.shape)
+
+        def claim():
+            if self._claimed[idx]:
+                return None
+            self._claimed[idx] = True
+            return self.flat[off:off + n].view(shape)       # a fresh view object (autograd may steal it)
+        return claim
 
     def _flag_hook(self, idx: int):
         def hook(g):
@@ -189,6 +206,7 @@ class GradBuckets:
         self.flat.zero_()
         for p in self.params:
             p.grad = None
+        self._claimed = [False] * len(self.params)
         self._received_local = [False] * len(self.params)
         self._received_host = None
         self._ready = [set() for _ in self.buckets]

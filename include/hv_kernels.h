@@ -512,6 +512,17 @@ int hv_dgrad_weight_prep(const float* w, int cout, int cin, int k, int flip, int
                          hv_stream_t stream);
 /* y[cols, rows] = x[rows, cols]^T  (fp32 -> y_dtype) */
 int hv_transpose_cast(const float* x, int rows, int cols, int y_dtype, void* y, hv_stream_t stream);
+/* Grouped transposes / casts of parameter-sized matrices in ONE launch (the training step's
+   per-forward operand layouts of every mHC site: A1, Wc, W2^T, Gc^T, W1^T, the W2 cast).  Entry:
+   x [rows, cols] (x_dtype) -> y [cols, rows] when transpose, else [rows, cols] (y_dtype); blk = the
+   entry's first block (exclusive prefix of hv_transpose_blocks over the table). */
+typedef struct hv_transpose_entry {
+  const void* x;
+  void* y;
+  int rows, cols, x_dtype, y_dtype, transpose, blk;
+} hv_transpose_entry;
+int hv_transpose_blocks(int rows, int cols);
+int hv_transpose_group(const hv_transpose_entry* tab, int count, int total_blocks, hv_stream_t stream);
 /* conv weight gradient [cout, (kh, kw, cin)] -> parameter layout [cout, cin, kh, kw] (fp32) */
 int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, float* y, hv_stream_t stream);
 /* out[c] (+)= sum_r x[r, c]  (bias gradients); deterministic two-pass */

@@ -480,6 +480,42 @@ def _tiny_model(gpu_device, precision="fp32"):
     return m, sd
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_grouped_train_prep_matches_per_site(gpu_device, precision):
+    """The grouped training coefficient prep (train_prep.TrainPrep: prep group + ONE transpose group
+    launch for all sites) gives the loss and every parameter gradient of the per-site preparation
+    (model.hv_train_group_prep = False), dropout off: bitwise-close in fp32 (the same fp32 products,
+    other launch boundaries), within bf16 rounding of the fold GEMM in bf16; a second forward before
+    the first backward is refused."""
+    from hv_amd.targets import synthetic_targets
+    res = {}
+    for grouped in (True, False):
+        m, _ = _tiny_model(gpu_device, precision)
+        m.hv_train_group_prep = grouped
+        B, S = 2, 64
+        x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(3)).to(gpu_device)
+        tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=4)]
+        out = m(x, targets=tg, compute_loss=True)
+        out["loss"]["total_loss"].backward()
+        torch.cuda.synchronize()
+        res[grouped] = (float(out["loss"]["total_loss"]),
+                        {n: p.grad.detach().float().cpu() for n, p in m.named_parameters() if p.grad is not None})
+    (l1, g1), (l0, g0) = res[True], res[False]
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    assert abs(l1 - l0) <= tol * abs(l0), (l1, l0)
+    assert g1.keys() == g0.keys()
+    for n in g0:
+        d = (g1[n] - g0[n]).norm().item()
+        assert d <= tol * g0[n].norm().item() + 1e-6, (n, d, g0[n].norm().item())
+    m, _ = _tiny_model(gpu_device, precision)
+    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(3)).to(gpu_device)
+    tg = [t.to(gpu_device) for t in synthetic_targets(2, 64, seed=4)]
+    first = m(x, targets=tg, compute_loss=True)["loss"]["total_loss"]
+    m(x, targets=tg, compute_loss=True)
+    with pytest.raises(RuntimeError, match="one forward per backward"):
+        first.backward()
+
+
 def test_tiny_train_step_grads_match_oracle(gpu_device):
     """Loss and every parameter gradient of one tiny-config training step (BN batch stats,
     dropout off) vs autograd of the oracle in fp64.  This configuration is ill-conditioned
