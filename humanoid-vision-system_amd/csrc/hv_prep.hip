@@ -332,6 +332,7 @@ __global__ void __launch_bounds__(256) k_pg4(const hv_mhc_prep_entry* __restrict
 // ------------------------------------------------------------------ weight prep group
 constexpr int WP_CAST_CHUNK = 4096;   // elements per block (cast)
 constexpr int WP_CONV_ROWS = 4;       // output channels per block (conv), one wave each
+constexpr int WP_MAX_TAPS = 9;        // staged reorder: kernels up to 3x3
 
 template <typename T>
 __device__ __forceinline__ void wp_cast(const hv_wprep_entry& e, int b) {
@@ -361,7 +362,7 @@ __device__ __forceinline__ void wp_cast(const hv_wprep_entry& e, int b) {
 }
 
 template <typename T>
-__device__ __forceinline__ void wp_conv(const hv_wprep_entry& e, int b) {
+__device__ __forceinline__ void wp_conv(const hv_wprep_entry& e, int b, float* lds) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int co = b * WP_CONV_ROWS + w;
   if (co >= e.n) return;
@@ -371,9 +372,37 @@ __device__ __forceinline__ void wp_conv(const hv_wprep_entry& e, int b) {
     if (e.scale_out) e.scale_out[co] = sc;
     if (e.bias_out) e.bias_out[co] = e.gamma ? e.beta[co] + (cb - e.mean[co]) * sc : cb;
   }
-  const int cin = e.cin, k = e.k, kk = k * k * cin;
+  const int cin = e.cin, k = e.k, kt = k * k, kk = kt * cin;
   const float* wr = e.src + (long)co * kk;
   T* yr = (T*)e.dst + (long)co * e.ldk;
+  if (cin % 64 == 0 && kt <= WP_MAX_TAPS && (((uintptr_t)wr) & 15) == 0) {
+    // 64 input channels per trip: their kt taps are one contiguous source run (64 * kt floats),
+    // loaded with 16-byte coalesced loads into this wave's LDS slice, then written out tap by
+    // tap as 64 consecutive outputs.  The element loop below issues one 4-byte load per lane
+    // and waits for it before the store (the store may alias the source for the compiler):
+    // latency-bound at a few bytes in flight per wave
+    float* sl = lds + (threadIdx.x >> 6) * (64 * WP_MAX_TAPS);
+    const int n4 = 16 * kt;
+    for (int c0 = 0; c0 < cin; c0 += 64) {
+      const float4* s4 = reinterpret_cast<const float4*>(wr + (long)c0 * kt);
+      float4 v[(64 * WP_MAX_TAPS / 4 + 63) / 64];
+#pragma unroll
+      for (int q = 0; q < (64 * WP_MAX_TAPS / 4 + 63) / 64; ++q)
+        if (lane + 64 * q < n4) v[q] = s4[lane + 64 * q];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < (64 * WP_MAX_TAPS / 4 + 63) / 64; ++q)
+        if (lane + 64 * q < n4) *reinterpret_cast<float4*>(sl + 4 * (lane + 64 * q)) = v[q];
+      // one wave's LDS operations complete in order: its own slice needs no barrier
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int t = 0; t < kt; ++t) Elem<T>::store(yr, (long)t * cin + c0 + lane, sl[lane * kt + t]);
+      __builtin_amdgcn_wave_barrier();
+    }
+    for (int i = kk + lane; i < e.ldk; i += 64) Elem<T>::store(yr, i, 0.f);
+    return;
+  }
   for (int i = lane; i < e.ldk; i += 64) {
     float v = 0.f;
     if (i < kk) {
@@ -394,12 +423,13 @@ __device__ inline int find_wp(const hv_wprep_entry* t, int count, int b) {
 }
 
 __global__ void __launch_bounds__(256) k_wprep(const hv_wprep_entry* __restrict__ tab, int count) {
+  __shared__ __attribute__((aligned(16))) float lds[WP_CONV_ROWS * 64 * WP_MAX_TAPS];
   const hv_wprep_entry& e = tab[find_wp(tab, count, blockIdx.x)];
   const int b = blockIdx.x - e.blk;
   if (e.kind == 0) {
     if (e.dtype == HV_BF16) wp_cast<unsigned short>(e, b); else wp_cast<float>(e, b);
   } else {
-    if (e.dtype == HV_BF16) wp_conv<unsigned short>(e, b); else wp_conv<float>(e, b);
+    if (e.dtype == HV_BF16) wp_conv<unsigned short>(e, b, lds); else wp_conv<float>(e, b, lds);
   }
 }
 

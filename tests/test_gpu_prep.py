@@ -52,7 +52,9 @@ def test_weight_prep_group_matches_per_layer(gpu_device, dtype):
     g = torch.Generator().manual_seed(5)
     m = ManifoldHyperConnection(32, expansion_rate=4).to(gpu_device).eval()
     convs = []
-    for cin, cout, k, bias, with_bn in [(3, 32, 3, False, True), (64, 128, 1, True, False), (96, 40, 3, True, True)]:
+    # cin % 64 == 0 takes the LDS-staged reorder (1x1 and 3x3), the others the element loop
+    for cin, cout, k, bias, with_bn in [(3, 32, 3, False, True), (64, 128, 1, True, False), (96, 40, 3, True, True),
+                                        (128, 24, 3, False, True), (192, 17, 3, True, False)]:
         c = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
         bn = nn.BatchNorm2d(cout) if with_bn else None
         with torch.no_grad():
