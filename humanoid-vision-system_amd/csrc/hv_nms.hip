@@ -165,6 +165,12 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_final(int nscales, float io
     scores[(long)b * max_det + k] = sscores[src];
     labels[(long)b * max_det + k] = slabels[src];
   }
+  // rows past `count` are zero, so the fixed-size outputs are a function of the inputs alone
+  for (int k = kept + threadIdx.x; k < max_det; k += blockDim.x) {
+    for (int j = 0; j < 4; ++j) boxes[((long)b * max_det + k) * 4 + j] = 0.f;
+    scores[(long)b * max_det + k] = 0.f;
+    labels[(long)b * max_det + k] = 0;
+  }
   if (threadIdx.x == 0) count[b] = kept;
 }
 

@@ -14,7 +14,7 @@ import torch.nn as nn
 from . import ops
 from .layers import conv_prep, ctx_scope, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection
-from .runtime import current, options, require_cuda, resolve_dtype
+from .runtime import Branches, current, options, require_cuda, resolve_dtype
 
 # Direct stem conv (hv_conv_stem: bf16 = LDS-staged input tile + one MFMA k-step per 16 pixels)
 # instead of the NCHW->NHWC pass + implicit GEMM (237 us at B=16 640^2).  Same-box A/B
@@ -180,7 +180,8 @@ class HybridVisionBackbone(nn.Module):
         if verbose:
             print(f"Backbone initialized with channels: {self.output_channels}")
 
-    def forward_nhwc(self, x: Optional[torch.Tensor], image: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    def forward_nhwc(self, x: Optional[torch.Tensor], image: Optional[torch.Tensor] = None,
+                     branches: Optional[Branches] = None) -> Dict[str, torch.Tensor]:
         """x: NHWC input; or image: the NCHW fp32 batch, whose first conv then runs as the direct
         stem kernel (falls back to the NHWC conversion + implicit GEMM when not applicable)."""
         layers = list(self.stem)[:3]
@@ -201,10 +202,6 @@ class HybridVisionBackbone(nn.Module):
         for i, lyr in enumerate(layers):
             x = lyr.forward_nhwc(x, pool=lyr is self.stem[2])     # stem[3] MaxPool2d fused into stem[2]
         raw = {"stem": x}
-        for i, st in enumerate(self.stages):
-            for lyr in st:
-                x = lyr.forward_nhwc(x)
-            raw[f"stage_{i + 1}"] = x
 
         def enh(mod, f):
             if isinstance(mod, nn.Identity):
@@ -212,10 +209,22 @@ class HybridVisionBackbone(nn.Module):
             n, h, w, c = f.shape
             return mod.forward_tokens(f.view(-1, c)).view(n, h, w, c)
 
-        return {"scale_small": enh(self.enhance_small, raw["stage_2"]),
-                "scale_medium": enh(self.enhance_medium, raw["stage_3"]),
-                "scale_large": enh(self.enhance_large, raw["stage_4"]),
-                "raw_features": raw}
+        # the small / medium scale enhancements read stage outputs the later stages only read too:
+        # with branches they run on side streams beside stages 3-4 (joined before returning)
+        br = branches if branches is not None else Branches(False)
+        out = {}
+        for i, st in enumerate(self.stages):
+            for lyr in st:
+                x = lyr.forward_nhwc(x)
+            raw[f"stage_{i + 1}"] = x
+            if i == 1:
+                out["scale_small"] = br.fork(lambda f=x: enh(self.enhance_small, f))
+            elif i == 2:
+                out["scale_medium"] = br.fork(lambda f=x: enh(self.enhance_medium, f))
+        out["scale_large"] = enh(self.enhance_large, raw["stage_4"])
+        br.join()
+        out["raw_features"] = raw
+        return out
 
     def forward(self, x: torch.Tensor) -> Dict[str, torch.Tensor]:
         require_cuda(x, "HybridVisionBackbone")

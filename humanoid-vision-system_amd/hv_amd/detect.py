@@ -13,7 +13,7 @@ from . import ops
 from .backbone import HybridVisionBackbone
 from .layers import ctx_scope, linear_prep, run_conv, to_nchw_view, to_nhwc
 from .manifold import ManifoldHyperConnection, prepare_plans
-from .runtime import HVOptions, RunCtx, VersionWatch, current, module_options, require_cuda, use_ctx, PRECISIONS
+from .runtime import Branches, HVOptions, RunCtx, VersionWatch, current, module_options, require_cuda, use_ctx, PRECISIONS
 from .vit import HybridVisionEncoder
 
 # side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HVOptions.prep_overlap); on
@@ -65,17 +65,26 @@ class FeaturePyramidNetwork(nn.Module):
         x = run_conv(x, r[3], r[4], "relu", self)
         return _tokens(self.mhc_fusions[i], x)
 
-    def forward_nhwc(self, feats: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    def forward_nhwc(self, feats: Dict[str, torch.Tensor], emit=None) -> Dict[str, torch.Tensor]:
+        """emit(key, tensor): called as soon as each fused scale is computed (top-down, large
+        first), so a consumer (the detection head on a side stream) can start on it while the
+        pyramid continues."""
         pl = run_conv(feats["scale_large"], self.lateral_convs[2], None, "none", self)
         pm = run_conv(feats["scale_medium"], self.lateral_convs[1], None, "none", self)
         ps = run_conv(feats["scale_small"], self.lateral_convs[0], None, "none", self)
+        out = {}
+
+        def put(key, t):
+            out[key] = t
+            if emit is not None:
+                emit(key, t)
         rl = self._refine(2, pl)
-        out = {"fused_large": run_conv(rl, self.output_convs[2], None, "none", self)}
+        put("fused_large", run_conv(rl, self.output_convs[2], None, "none", self))
         rm = self._refine(1, ops.upsample_add(pm, rl))
-        out["fused_medium"] = run_conv(rm, self.output_convs[1], None, "none", self)
+        put("fused_medium", run_conv(rm, self.output_convs[1], None, "none", self))
         rs = self._refine(0, ops.upsample_add(ps, rm))
-        out["fused_small"] = run_conv(rs, self.output_convs[0], None, "none", self)
-        return out
+        put("fused_small", run_conv(rs, self.output_convs[0], None, "none", self))
+        return {k: out[k] for k in ("fused_large", "fused_medium", "fused_small")}
 
     def forward(self, features: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         if self.training:
@@ -211,14 +220,22 @@ class YOLODetectionHead(nn.Module):
     def forward_nhwc(self, feats: Dict[str, torch.Tensor], detections: Optional[Dict[str, torch.Tensor]] = None):
         """detections: if a dict is given, it is filled with the per-scale decoded detections
         tensors (HybridVisionSystem's 'detections' output key)."""
+        res = {s: self.scale_nhwc(s, feats[key], detections is not None)
+               for s, key in enumerate(("scale_small", "scale_medium", "scale_large")) if key in feats}
+        return self.collect(res, detections)
+
+    def scale_nhwc(self, s: int, x: torch.Tensor, want_detections: bool):
+        """One scale's prediction head + decode: (pred, decoded dict)."""
+        lg = self.pred_heads[s].logits_nhwc(x)
+        awh = self.anchor_generator.anchors[s].reshape(self.num_anchors, 4)[:, 2:4].contiguous()
+        dec, pred = ops.yolo_decode(lg, self.num_anchors, self.num_classes, awh, detections=want_detections)
+        return pred, dec
+
+    @staticmethod
+    def collect(res: Dict[int, Tuple], detections: Optional[Dict[str, torch.Tensor]]):
         preds, decoded = {}, {}
-        for s, key in enumerate(("scale_small", "scale_medium", "scale_large")):
-            if key not in feats:
-                continue
-            lg = self.pred_heads[s].logits_nhwc(feats[key])
-            awh = self.anchor_generator.anchors[s].reshape(self.num_anchors, 4)[:, 2:4].contiguous()
-            dec, pred = ops.yolo_decode(lg, self.num_anchors, self.num_classes, awh,
-                                        detections=detections is not None)
+        for s in sorted(res):
+            pred, dec = res[s]
             if detections is not None:
                 detections[DETECTION_KEYS[s]] = dec.pop("detections")
             preds[f"scale_{s}"] = pred
@@ -469,25 +486,37 @@ class HybridVisionSystem(nn.Module):
         require_cuda(x, "HybridVisionSystem")
         ctx = self._ctx()
         with torch.no_grad(), use_ctx(ctx):
+            # independent parts on side streams (runtime.Branches): base 640 bf16 B=16 graph step
+            # 17.37 vs 17.85 ms; at B=1 the cross-stream edges cost more than the overlap wins
+            # (frozen p50 4.61 vs 4.46 ms; profiles/r05/branches_ab.txt)
+            br = Branches(x.shape[0] >= ctx.opts.branch_min_batch)
             if x.dtype == torch.float32 and x.is_contiguous():
-                bb = self.backbone.forward_nhwc(None, image=x)     # direct stem conv from NCHW
+                bb = self.backbone.forward_nhwc(None, image=x, branches=br)   # direct stem conv from NCHW
             else:
-                bb = self.backbone.forward_nhwc(to_nhwc(x, ctx.dtype))
+                bb = self.backbone.forward_nhwc(to_nhwc(x, ctx.dtype), branches=br)
             outputs: Dict[str, Any] = {}
             if self.use_vit:
                 vit = self.vit_encoder.forward_nhwc(bb["scale_large"])
                 bb["scale_large"] = ops.add_scaled(bb["scale_large"], vit, 0.5)
                 outputs["vit_features"] = to_nchw_view(vit)
-            fused = self.feature_fusion.forward_nhwc(bb)
+            head_res: Dict[int, Tuple] = {}
+            emit = None
             if task == "detection":
-                det_in = {"scale_small": fused["fused_small"], "scale_medium": fused["fused_medium"],
-                          "scale_large": fused["fused_large"]}
+                # each scale's head starts on a side stream as soon as the pyramid has produced it
+                scale_of = {"fused_small": 0, "fused_medium": 1, "fused_large": 2}
+
+                def emit(key, t):
+                    s = scale_of[key]
+                    head_res[s] = br.fork(lambda: self.detection_head.scale_nhwc(s, t, True))
+            fused = self.feature_fusion.forward_nhwc(bb, emit)
+            if task == "detection":
                 dets: Dict[str, torch.Tensor] = {}
-                preds, decoded = self.detection_head.forward_nhwc(det_in, dets)
+                preds, decoded = self.detection_head.collect(head_res, dets)
                 outputs["predictions"] = preds
                 outputs["decoded"] = decoded
                 outputs["detections"] = dets
                 if compute_loss and targets is not None:
+                    br.join()
                     outputs["loss"] = self.detection_head.loss_fn(preds, targets)
             final = self._final_features(fused)
             if task == "features":
@@ -498,6 +527,7 @@ class HybridVisionSystem(nn.Module):
             outputs["backbone_features"] = bbv
             outputs["fused_features"] = {k: to_nchw_view(v) for k, v in fused.items()}
             outputs["final_features"] = final
+            br.join()                          # every branch's results are on the forward's stream
         ctx.join_prep()                        # side-stream prep joined even if no mHC ran
         return outputs, ctx
 

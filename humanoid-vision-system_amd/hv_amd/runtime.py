@@ -41,6 +41,7 @@ class HVOptions:
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
     mhc256_min_tokens: int = 25600    # D = 256 sites fused (split-hidden) from this many tokens (ops._mhc_variant)
     mhc_tok: bool = True              # token-tile fused kernel for small-T sites (HV_MV_TOK, ops._mhc_variant)
+    branch_min_batch: int = 8         # independent branches on side streams from this batch (Branches)
 
     def replace(self, **kw) -> "HVOptions":
         return dataclasses.replace(self, **kw)
@@ -72,6 +73,52 @@ class RunCtx:
 
 def current() -> Optional[RunCtx]:
     return _CTX.get()
+
+
+class Branches:
+    """Independent parts of one eval forward on side streams: the three detection heads (each
+    starts as soon as the pyramid has produced its scale) and the small / medium scale
+    enhancements of the backbone beside stages 3-4.  Their launches leave CUs idle in their tails
+    (and the 20x20 heads use tens of workgroups), so overlapping parts that share no data fills
+    the chip better.  fork(fn) runs fn on a side stream that first waits for everything issued so
+    far on the forward's stream; join() makes the forward's stream wait for every forked branch.
+    Results of a branch may be read on the forward's stream only after join().  Side streams are
+    kept per (device, forward stream), so concurrent forwards on different streams never share
+    one; a graph captured over the forward records each fork / join as graph edges.
+    Disabled (fork = call), the forward is the single-stream one."""
+    _STREAMS: Dict[tuple, list] = {}
+
+    def __init__(self, enabled: bool):
+        self.main = torch.cuda.current_stream() if enabled else None
+        self.pending: list = []
+        self.used = 0
+
+    def _side(self) -> "torch.cuda.Stream":
+        key = (self.main.device.index, self.main.cuda_stream)
+        pool = Branches._STREAMS.setdefault(key, [])
+        if self.used == len(pool):
+            pool.append(torch.cuda.Stream(device=self.main.device))
+        s = pool[self.used]
+        self.used += 1
+        return s
+
+    def fork(self, fn):
+        if self.main is None:
+            return fn()
+        s = self._side()
+        s.wait_stream(self.main)
+        with torch.cuda.stream(s):
+            out = fn()
+            done = torch.cuda.Event()
+            done.record(s)
+        self.pending.append(done)
+        return out
+
+    def join(self) -> None:
+        for ev in self.pending:
+            self.main.wait_event(ev)
+        self.pending.clear()
+        self.used = 0           # the side streams' later work is ordered after this join
 
 
 class _TrainState:

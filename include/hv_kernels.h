@@ -441,7 +441,8 @@ int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, in
  * non_max_suppression (yolo_head.py:571-731) for a whole batch in two launches.
  * Per (image, scale): class_score > conf_thr, greedy NMS (keep IoU < iou_thr, best first,
  * at most max_det, up to 8192 candidates per image and scale); then per image the same NMS
- * over the concatenated per-scale survivors.  Outputs [batch, max_det] (+ count[batch]).
+ * over the concatenated per-scale survivors.  Outputs [batch, max_det] (+ count[batch]);
+ * rows at and past count[b] are written as zeros.
  * ------------------------------------------------------------------------------------ */
 typedef struct hv_nms_scale {
   const float* boxes;          /* [batch, cells, 4] xyxy (decoder output [B, A, H, W, 4]) */

@@ -12,6 +12,9 @@ from hv_amd import HybridVisionSystem  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 torch.manual_seed(0)
 m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False}).cuda().eval()
+if os.environ.get("HV_OPTS"):      # e.g. HV_OPTS="branch_min_batch=1,mhc_tok=False"
+    import ast
+    m.set_options(**{k: ast.literal_eval(v) for k, v in (kv.split("=") for kv in os.environ["HV_OPTS"].split(","))})
 m.freeze(True)
 x = torch.randn(1, 3, 640, 640, device="cuda")
 with torch.no_grad():
