@@ -11,6 +11,10 @@ for i in $(seq $R); do
     timeout -k 10 200 python -u tools/quick_bench.py "[$o]" >> $OUT/ab.txt 2>> $OUT/ab.err || exit 1
     echo -n "[$o]: " >> $OUT/ab.txt
     timeout -k 10 200 python -u tools/lat_prof.py 200 >> $OUT/ab.txt 2>> $OUT/ab.err || exit 1
+    if [ -n "$AB_RECOMPUTE" ]; then
+      echo -n "[$o]: " >> $OUT/ab.txt
+      HV_LAT_RECOMPUTE=1 timeout -k 10 200 python -u tools/lat_prof.py 200 >> $OUT/ab.txt 2>> $OUT/ab.err || exit 1
+    fi
   done
 done
 unset HV_OPTS

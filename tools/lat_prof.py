@@ -15,7 +15,7 @@ m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False
 if os.environ.get("HV_OPTS"):      # e.g. HV_OPTS="branch_min_batch=1,mhc_tok=False"
     import ast
     m.set_options(**{k: ast.literal_eval(v) for k, v in (kv.split("=") for kv in os.environ["HV_OPTS"].split(","))})
-m.freeze(True)
+m.freeze(not os.environ.get("HV_LAT_RECOMPUTE"))     # HV_LAT_RECOMPUTE=1: prep re-run per frame
 x = torch.randn(1, 3, 640, 640, device="cuda")
 with torch.no_grad():
     m(x)
@@ -30,4 +30,4 @@ with torch.no_grad():
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
 ts.sort()
-print(f"frozen B=1 p50 {ts[len(ts) // 2]:.3f} ms over {reps}")
+print(f"{'recompute' if os.environ.get('HV_LAT_RECOMPUTE') else 'frozen'} B=1 p50 {ts[len(ts) // 2]:.3f} ms over {reps}")
