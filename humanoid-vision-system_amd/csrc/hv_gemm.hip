@@ -356,6 +356,16 @@ extern "C" int hv_gemm(const hv_gemm_desc* dp, hv_stream_t stream) {
   if (d.ldb % epc) return HV_EUNSUPPORTED;
   if (((uintptr_t)d.A | (uintptr_t)d.B) & 15) return HV_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+  if (d.colsum_part) {
+    // only the LDS-DMA kernel's staged gradient epilogue (epi_writeout_m2pf) sums the columns:
+    // every other path refuses the call instead of silently leaving the partials unwritten
+    const bool ok = d.epi_mode == 2 && d.dtype == HV_BF16 && !d.conv_transposed && d.splitk <= 1 &&
+                    !(d.variant & (HV_GV_REGSTAGE | HV_GV_FLAT_TRAIN | HV_GV_TRAIN_NOPF | HV_GV_TRAIN_BIG)) &&
+                    (d.variant & HV_GV_TILE_MASK) <= 4 && !(d.conv_k == 3 && d.conv_c == 32) &&
+                    (((uintptr_t)d.C) & 15) == 0 && d.ldc % 8 == 0 &&
+                    (!d.residual || ((((uintptr_t)d.residual) & 15) == 0 && d.ldr % 8 == 0));
+    return ok ? hv_gemm_glds(d, s) : HV_EUNSUPPORTED;
+  }
   if (!(d.variant & HV_GV_REGSTAGE)) {
     if (d.conv_k == 3 && d.conv_c == 32) {               // halo-tiled 3x3 conv, Cin = 32 (hv_stem.hip)
       const int rc = hv_conv3x3_c32(d, s);

@@ -536,6 +536,10 @@ __device__ __forceinline__ void epi_writeout_m2pf(const hv_gemm_desc& d, int r0,
       }
     }
   }
+  // colsum_part: column sums of C as stored over this tile's rows (per-thread, then over the RPP
+  // threads of a column group through LDS); the branch is uniform (a kernel argument)
+  const bool want_cs = d.colsum_part != nullptr;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float za[8], zb[8];
   aux_row(0, za);
 #pragma unroll
@@ -564,13 +568,24 @@ __device__ __forceinline__ void epi_writeout_m2pf(const hv_gemm_desc& d, int r0,
         v[4] += rf[p][1].x; v[5] += rf[p][1].y; v[6] += rf[p][1].z; v[7] += rf[p][1].w;
       }
       if (c_bf) {
-        *reinterpret_cast<uint4*>((unsigned short*)d.C + (long)row * d.ldc + col) =
-            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                       pack_bf16x2(v[6], v[7]));
+        const uint4 pk = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                                    pack_bf16x2(v[6], v[7]));
+        *reinterpret_cast<uint4*>((unsigned short*)d.C + (long)row * d.ldc + col) = pk;
+        if (want_cs) {
+          const unsigned pw[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            csum[2 * q] += __uint_as_float(pw[q] << 16);
+            csum[2 * q + 1] += __uint_as_float(pw[q] & 0xffff0000u);
+          }
+        }
       } else {
         float* o = (float*)d.C + (long)row * d.ldc + col;
         *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        if (want_cs)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) csum[j] += v[j];
       }
     } else {
       const long rrow = d.r_mod > 0 ? row % d.r_mod : row;
@@ -582,9 +597,31 @@ __device__ __forceinline__ void epi_writeout_m2pf(const hv_gemm_desc& d, int r0,
           x += d.r_dtype == HV_BF16 ? bf2f(((const unsigned short*)d.residual)[rrow * d.ldr + col + j])
                                     : ((const float*)d.residual)[rrow * d.ldr + col + j];
         const long o = (long)row * d.ldc + col + j;
-        if (c_bf) ((unsigned short*)d.C)[o] = f2bf(x);
-        else ((float*)d.C)[o] = x;
+        if (c_bf) {
+          const unsigned short h = f2bf(x);
+          ((unsigned short*)d.C)[o] = h;
+          csum[j] += bf2f(h);
+        } else {
+          ((float*)d.C)[o] = x;
+          csum[j] += x;
+        }
       }
+    }
+  }
+  if (want_cs) {
+    // every thread's reads of the staged tile are done before its LDS is reused
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);                 // [RPP][BN]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(threadIdx.x / TPR) * BN + c8 + j] = csum[j];
+    __syncthreads();
+    if ((int)threadIdx.x < BN && n0 + (int)threadIdx.x < d.N) {
+      float t = 0.f;
+      for (int q = 0; q < RPP; ++q) t += red[q * BN + threadIdx.x];       // fixed order
+      const long b0 = r0 / 64, cidx = n0 + threadIdx.x;
+      d.colsum_part[b0 * d.N + cidx] = t;
+#pragma unroll
+      for (int e = 1; e < SLAB / 64; ++e) d.colsum_part[(b0 + e) * d.N + cidx] = 0.f;
     }
   }
 }

@@ -297,8 +297,10 @@ __global__ void __launch_bounds__(256) k_colred(const ColRed r, int nblk, float*
 // workgroups, each thread walking 64 partials in series: ~14 us per launch, 459 launches per
 // training step); four independent accumulators per thread, combined in a fixed order
 // (deterministic).
+// sums_hi: columns >= split go to sums_hi[col - split] instead (one image; the LN gamma / beta
+// gradients straight into their parameters' buffers)
 __global__ void __launch_bounds__(256) k_colred_final(const float* part, int nblk, int width, float* sums,
-                                                      int accumulate) {
+                                                      int accumulate, float* sums_hi, int split) {
   __shared__ float sm[32][9];
   const int img = blockIdx.y;
   const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
@@ -321,7 +323,7 @@ __global__ void __launch_bounds__(256) k_colred_final(const float* part, int nbl
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 32; ++q) s += sm[q][c];
-    float* o = sums + (long)img * width + col;
+    float* o = sums_hi && col >= split ? sums_hi + (col - split) : sums + (long)img * width + col;
     *o = accumulate ? *o + s : s;
   }
 }
@@ -343,7 +345,8 @@ inline size_t colred_work(long rows, int cols, int imgs, int nv) {
 
 // launch part + final; sums receives [imgs][NV*cols] (NV-major per image)
 template <typename TA, typename TB, int MODE>
-int colred_run(const ColRed& r, int imgs, float* work, float* sums, int accumulate, hipStream_t s) {
+int colred_run(const ColRed& r, int imgs, float* work, float* sums, int accumulate, hipStream_t s,
+               float* sums_hi = nullptr, int split = 0) {
   constexpr int NV = CrNV<MODE>::V;
   const int nblk = colred_blocks(r.rows, r.cols, imgs);
   const int cpr = r.cols / 4;
@@ -351,7 +354,8 @@ int colred_run(const ColRed& r, int imgs, float* work, float* sums, int accumula
   if (cpr <= 256) k_colred<TA, TB, MODE, 1><<<grid, 256, 0, s>>>(r, nblk, work);
   else if (cpr <= 512) k_colred<TA, TB, MODE, 2><<<grid, 256, 0, s>>>(r, nblk, work);
   else k_colred<TA, TB, MODE, 4><<<grid, 256, 0, s>>>(r, nblk, work);
-  k_colred_final<<<dim3(hv_cdiv(NV * r.cols, 8), imgs), 256, 0, s>>>(work, nblk, NV * r.cols, sums, accumulate);
+  k_colred_final<<<dim3(hv_cdiv(NV * r.cols, 8), imgs), 256, 0, s>>>(work, nblk, NV * r.cols, sums, accumulate,
+                                                                    sums_hi, split);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }
@@ -767,17 +771,13 @@ __global__ void k_scatter_rows(const T* dy, long stride, int n, int c, T* dx) {
 // ------------------------------------------------------------------ YOLO loss
 // object count: block partial counts added atomically (integer-valued floats < 2^24: exact in
 // any order, so deterministic)
-// Small fills / copies as kernels, not hipMemsetAsync / hipMemcpyAsync: inside a captured
-// training step these become kernel nodes ordered like every other launch (the memset-node
-// form of the object-count reset left the first replay's YOLO loss normalised by a wrong
-// count on some runs -- tools/train_bisect.py: identical predictions, total 2002.99 vs 1700.07).
+// Small fills as kernels, not hipMemsetAsync: inside a captured training step these become
+// kernel nodes ordered like every other launch (the memset-node form of the object-count reset
+// left the first replay's YOLO loss normalised by a wrong count on some runs --
+// tools/train_bisect.py: identical predictions, total 2002.99 vs 1700.07).
 __global__ void k_fill_f32(float* p, int n, float v) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) p[i] = v;
-}
-__global__ void k_copy_f32(const float* __restrict__ src, float* __restrict__ dst, int n) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) dst[i] = src[i];
 }
 
 __global__ void __launch_bounds__(256) k_yolo_count(const float* targets, long cells, int P, float* nobj) {
@@ -1037,6 +1037,14 @@ extern "C" int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, fl
   return HV_OK;
 }
 
+extern "C" int hv_colsum_final(const float* part, int nblk, int cols, float* out, int accumulate,
+                               hv_stream_t stream) {
+  if (!part || !out || nblk <= 0 || cols <= 0) return HV_EINVAL;
+  k_colred_final<<<dim3(hv_cdiv(cols, 8), 1), 256, 0, (hipStream_t)stream>>>(part, nblk, cols, out, accumulate, nullptr, 0);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
 extern "C" size_t hv_colsum_work_floats(int rows, int cols) {
   return colred_ok(cols) ? colred_work(rows, cols, 1, 1) : (size_t)red_chunks(rows) * cols;
 }
@@ -1155,19 +1163,19 @@ extern "C" int hv_rownorm_backward(int mode, int x_dtype, const void* x, int dy_
 #undef RB_LAUNCH
   if (rc) return rc;
   if (params) {
-    float* sums = work + colred_work(rows, cols, 1, 2);   // [sum g xhat | sum g]
+    // [sum g xhat | sum g] written straight into dgamma / dbeta (the scratch row for a missing one)
+    float* sums = work + colred_work(rows, cols, 1, 2);
+    float* lo = dgamma ? dgamma : sums;
+    float* hi = dbeta ? dbeta : sums + cols;
     ColRed r{};
     r.a = x; r.b = dy; r.rows = rows; r.cols = cols;
     r.mean = mode == 0 ? mean : nullptr; r.rstd = rstd; r.p = drop_p; r.seed = seed; r.soff = seed_offset;
     int rc;
-    if (x_dtype == HV_F32 && dy_dtype == HV_F32) rc = colred_run<float, float, CR_ROWN>(r, 1, work, sums, 0, s);
-    else if (x_dtype == HV_F32) rc = colred_run<float, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
-    else if (dy_dtype == HV_F32) rc = colred_run<unsigned short, float, CR_ROWN>(r, 1, work, sums, 0, s);
-    else rc = colred_run<unsigned short, unsigned short, CR_ROWN>(r, 1, work, sums, 0, s);
+    if (x_dtype == HV_F32 && dy_dtype == HV_F32) rc = colred_run<float, float, CR_ROWN>(r, 1, work, lo, 0, s, hi, cols);
+    else if (x_dtype == HV_F32) rc = colred_run<float, unsigned short, CR_ROWN>(r, 1, work, lo, 0, s, hi, cols);
+    else if (dy_dtype == HV_F32) rc = colred_run<unsigned short, float, CR_ROWN>(r, 1, work, lo, 0, s, hi, cols);
+    else rc = colred_run<unsigned short, unsigned short, CR_ROWN>(r, 1, work, lo, 0, s, hi, cols);
     if (rc) return rc;
-    if (dgamma) k_copy_f32<<<hv_cdiv(cols, 256), 256, 0, s>>>(sums, dgamma, cols);
-    if (dbeta) k_copy_f32<<<hv_cdiv(cols, 256), 256, 0, s>>>(sums + cols, dbeta, cols);
-    HV_CHECK_LAUNCH();
   }
   return HV_OK;
 }

@@ -28,7 +28,7 @@ MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
 MV_TOK, MV_TOK16 = 0x400, 0x800
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
-ABI_VERSION = 2          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
+ABI_VERSION = 3          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
 _LIB = None
 _LOCK = threading.Lock()
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -83,7 +83,7 @@ class GemmDesc(C.Structure):
                 ("aux", vp), ("ld_aux", i64), ("aux_dtype", i32), ("epi_mode", i32),
                 ("drop_p", f32), ("drop_seed", C.c_uint), ("conv_transposed", i32), ("variant", i32),
                 ("splitk_work", vp), ("splitk_count", vp), ("splitk", i32), ("pad2_", i32),
-                ("seed_offset", vp)]
+                ("seed_offset", vp), ("colsum_part", vp)]
 
 
 class CopySegment(C.Structure):
@@ -210,6 +210,7 @@ _SIGS = {
     "hv_conv_grad_reorder": ([vp, i32, i32, i32, vp, vp], i32),
     "hv_colsum_work_floats": ([i32, i32], C.c_size_t),
     "hv_colsum": ([i32, vp, i64, i32, i32, vp, i32, vp, vp], i32),
+    "hv_colsum_final": ([vp, i32, i32, vp, i32, vp], i32),
     "hv_bn_work_floats": ([i32, i32], C.c_size_t),
     "hv_bn_stats": ([i32, vp, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp], i32),
     "hv_bn_apply": ([i32, vp, i32, i32, vp, vp, vp, vp, i32, vp, vp], i32),

@@ -29,10 +29,14 @@ def gemm_train(a: Tensor, b: Tensor, *, mode: int, act: str = "none", aux: Optio
                bias: Optional[Tensor] = None, drop_p: float = 0.0, seed: int = 0,
                residual: Optional[Tensor] = None, a_mean: Optional[Tensor] = None,
                a_rstd: Optional[Tensor] = None, b_colsum: Optional[Tensor] = None, a2: Optional[Tensor] = None,
-               out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0) -> Tensor:
+               out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0,
+               colsum: Optional[Tensor] = None) -> Tensor:
     """C = A' B^T with a training epilogue (hv_gemm_desc.epi_mode):
     mode 1: aux <- pre-activation (written), C = dropout(act(pre));
-    mode 2: C = acc * keep * act'(aux) (+ residual)  -- gradient through act + dropout."""
+    mode 2: C = acc * keep * act'(aux) (+ residual)  -- gradient through act + dropout.
+    colsum (mode 2, fp32 [N]): receives the column sums of C as stored (the bias gradient of the
+    layer), summed in the GEMM's epilogue (hv_gemm_desc.colsum_part) -- or, where the call takes
+    another kernel, by a separate pass over C."""
     _cuda(a, b)
     M, K1 = a.shape
     K = K1 + (a2.shape[1] if a2 is not None else 0)
@@ -65,7 +69,22 @@ def gemm_train(a: Tensor, b: Tensor, *, mode: int, act: str = "none", aux: Optio
         _contig(residual, "residual")
         d.residual, d.ldr, d.r_dtype = residual.data_ptr(), N, dtype_code(residual.dtype)
     d.variant = options().gemm_variant
-    check(L.lib().hv_gemm(C.byref(d), stream_ptr()), f"hv_gemm(train mode {mode}) M={M} N={N} K={K}")
+    what = f"hv_gemm(train mode {mode}) M={M} N={N} K={K}"
+    if colsum is not None:
+        if mode != 2 or colsum.shape != (N,) or colsum.dtype != torch.float32 or not colsum.is_contiguous():
+            raise ValueError("gemm_train: colsum needs mode 2 and a contiguous fp32 [N] tensor")
+        part = torch.empty((-(-M // 128) * 2) * N, device=a.device, dtype=torch.float32)
+        d.colsum_part = part.data_ptr()
+        rc = L.lib().hv_gemm(C.byref(d), stream_ptr())
+        if rc != -2:                                  # HV_EUNSUPPORTED: nothing was launched
+            check(rc, what)
+            check(L.lib().hv_colsum_final(part.data_ptr(), -(-M // 64), N, colsum.data_ptr(), 0, stream_ptr()),
+                  "hv_colsum_final")
+            return out
+        d.colsum_part = None
+    check(L.lib().hv_gemm(C.byref(d), stream_ptr()), what)
+    if colsum is not None:
+        colsum.copy_(_colsum_pass(out))
     return out
 
 
@@ -198,6 +217,9 @@ def colsum(x: Tensor) -> Tensor:
     check(L.lib().hv_colsum(dtype_code(x.dtype), x.data_ptr(), cols, rows, cols, out.data_ptr(), 0,
                             work.data_ptr(), stream_ptr()), "hv_colsum")
     return out
+
+
+_colsum_pass = colsum      # gemm_train's fallback (its `colsum` argument shadows the function)
 
 
 # ---------------------------------------------------------------------------- BatchNorm

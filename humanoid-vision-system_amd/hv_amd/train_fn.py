@@ -172,6 +172,9 @@ def _mhc_coefficients(m, H_res: Tensor, W1: Tensor, b1: Tensor, dt):
     return gc, u, wct, A1, c1
 
 
+EPILOGUE_COLSUM = True    # mHC bias gradients from the dgrad GEMM epilogue (tools/train_ab.py TF.EPILOGUE_COLSUM)
+
+
 class MhcFn(torch.autograd.Function):
     """ManifoldHyperConnection.forward in training mode (manifold_layers.py:223-280):
     LN_pre -> (H_pre . Linear1 folded) -> GELU -> dropout -> Linear2 -> GELU -> dropout ->
@@ -228,13 +231,18 @@ class MhcFn(torch.autograd.Function):
         dwc_x = T.wgrad(x, dyc)                            # [D, D]
         dwc_h = T.wgrad(h2, dyc)                           # [Hd, D]
         dx_res = ops.gemm(dyc, wc[:D])                     # [T, D]
-        dpre2 = T.gemm_train(dyc, wc[D:], mode=2, act="gelu", aux=pre2, drop_p=p2, seed=s2)
+        # the bias gradients db2 / dc1 are summed in the dgrad GEMMs' epilogues (colsum=; the
+        # separate column-sum pass over dpre when EPILOGUE_COLSUM is off)
+        ecs = EPILOGUE_COLSUM
+        db2 = torch.empty(Hd, device=x.device, dtype=torch.float32) if ecs else None
+        dpre2 = T.gemm_train(dyc, wc[D:], mode=2, act="gelu", aux=pre2, drop_p=p2, seed=s2, colsum=db2)
+        db2 = db2 if ecs else T.colsum(dpre2)
         dW2 = T.wgrad(dpre2, h1, out=T.grad_out(W2))       # [Hd, 2Hd]
-        db2 = T.colsum(dpre2)
         w2t = co.w2t if co is not None else T.transpose_cast(W2, dt)    # [2Hd, Hd]
-        dpre1 = T.gemm_train(dpre2, w2t, mode=2, act="gelu", aux=pre1, drop_p=p1, seed=s1)
+        dc1 = torch.empty(2 * Hd, device=x.device, dtype=torch.float32) if ecs else None
+        dpre1 = T.gemm_train(dpre2, w2t, mode=2, act="gelu", aux=pre1, drop_p=p1, seed=s1, colsum=dc1)
+        dc1 = dc1 if ecs else T.colsum(dpre1)
         dA1t = T.wgrad(dpre1, z)                           # [2Hd, D]
-        dc1 = T.colsum(dpre1)
         dz = ops.gemm(dpre1, co.a1 if co is not None else ops.cast(A1, dt))   # [T, D]
         dx, _, _ = T.rownorm_backward(T.LN, x, dz, mean, rstd, None, dx_dtype=dt, dx_add=dx_res,
                                       param_grads=False)

@@ -35,8 +35,9 @@ enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
 /* ABI version: 2 since hv_adamw gained `steps` and `active`, hv_grad_norms `active`, the dropout
  * entry points and hv_gemm_desc a device `seed_offset`, hv_mhc_fused_supported gained `variant`,
  * hv_mhc_fused_args grew by 8 bytes and the hv_gemm_set_* / hv_mhc_fused_set_* setters were
- * removed.  Bindings compare it with the version they were written against. */
-#define HV_ABI_VERSION 2
+ * removed; 3 since hv_gemm_desc gained `colsum_part` (appended).  Bindings compare it with the
+ * version they were written against. */
+#define HV_ABI_VERSION 3
 int hv_abi_version(void);
 /* build provenance: a hash of the sources (the .hip / .h files of csrc, the include headers, the Makefile) the
  * library was compiled from; the Python loader recomputes it and refuses a stale build */
@@ -147,6 +148,15 @@ typedef struct hv_gemm_desc {
      *seed_offset, so a graph-captured training step draws new masks on every replay by
      advancing one device word (the seed arguments baked into the graph stay constant) */
   const unsigned int* seed_offset;
+  /* gradient epilogue (epi_mode 2) only, may be NULL: column sums of C as stored, per 64-row
+     block -- colsum_part[b * N + n] = sum of C[m, n] over m in [64 b, 64 b + 64) (fp32; a
+     workgroup owning a taller tile writes its sum into its first block and zeros into the
+     others).  ceil(M / 128) * 2 blocks must be allocated; hv_colsum_final reduces the first
+     ceil(M / 64).  The bias gradient of the layer whose activation backward this launch fuses,
+     without a second pass over C (replaces hv_colsum on it).  HV_EUNSUPPORTED when the call
+     does not take the LDS-DMA kernel's staged gradient epilogue (bf16, K % 64 == 0, aligned C,
+     no variant forcing another path); nothing is launched then. */
+  float* colsum_part;
 } hv_gemm_desc;
 
 #define HV_SPLITK_MAX_TILES 4096
@@ -530,6 +540,9 @@ int hv_conv_grad_reorder(const float* g, int cout, int cin, int k, float* y, hv_
 size_t hv_colsum_work_floats(int rows, int cols);
 int hv_colsum(int dtype, const void* x, long ldx, int rows, int cols, float* out, int accumulate,
               float* work, hv_stream_t stream);
+/* out[c] (+)= sum_b part[b * cols + c] over b < nblk, fixed order (the second pass of hv_colsum;
+   reduces hv_gemm_desc.colsum_part) */
+int hv_colsum_final(const float* part, int nblk, int cols, float* out, int accumulate, hv_stream_t stream);
 
 /* BatchNorm2d in training mode over NHWC rows (vision_backbone.py:113, feature_fusion.py:44,
    yolo_head.py:122): batch mean / biased var -> rstd; running stats updated with momentum

@@ -1049,6 +1049,31 @@ def test_gemm_train_staged_epilogue_bitwise(gpu_device, M, N, K, act, ln):
             assert torch.equal(x0, x1), key
 
 
+@pytest.mark.parametrize("M,N,K,tile", [(300, 136, 128, 0), (1000, 256, 256, 0), (777, 96, 64, 0), (4100, 1024, 512, 0),
+                                        (1000, 256, 256, 1), (1000, 256, 256, 3), (200, 64, 128, 4)])
+def test_gemm_train_epilogue_colsum(gpu_device, M, N, K, tile):
+    """gemm_train(mode 2, colsum=): the bias gradient summed in the gradient epilogue
+    (hv_gemm_desc.colsum_part, per 64-row block, reduced by hv_colsum_final) equals the column
+    sums of the stored output, for every training tile shape (forced 128x128 / 128x64 / 64x64,
+    automatic 64x128) and ragged M / N; C itself is bitwise the colsum-free launch's; a variant
+    whose kernel cannot sum (GV_TRAIN_NOPF) falls back to the separate pass."""
+    from hv_amd import _lib
+    T = OT()
+    g = torch.Generator().manual_seed(M + N + tile)
+    a = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu_device)
+    b = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(gpu_device)
+    pre = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu_device)
+    from conftest import gemm_variant
+    for v in (tile, _lib.GV_TRAIN_NOPF):
+        with gemm_variant(v):
+            db = torch.full((N,), float("nan"), device=gpu_device)
+            d0 = T.gemm_train(a, b, mode=2, act="gelu", aux=pre, drop_p=0.2, seed=5)
+            d1 = T.gemm_train(a, b, mode=2, act="gelu", aux=pre, drop_p=0.2, seed=5, colsum=db)
+        assert torch.equal(d0, d1)
+        ref = T.colsum(d1)
+        assert torch.allclose(db, ref, rtol=1e-5, atol=1e-4 * ref.abs().max().item()), (v, (db - ref).abs().max())
+
+
 def test_dropout_seed_offset_word(gpu_device):
     """hv_kernels.h seed_offset: every dropout kernel (GEMM training epilogue, row norm,
     elementwise dropout / activation backward, MFMA attention forward + backward) uses

@@ -1,7 +1,8 @@
 """Same-process A/B of training-step options on the bench's training workload (base 640, B=16,
 bf16, HVTrainer graph replay): model attributes toggled per arm, separate trainers and models,
 arms interleaved.  usage: python tools/train_ab.py <attr> [batch] [steps]
-  attr: a model attribute switched False (arm A) / True (arm B), e.g. hv_train_group_prep"""
+  attr: a model attribute switched False (arm A) / True (arm B), e.g. hv_train_group_prep, or
+        TF.<name>: a hv_amd.train_fn module switch (e.g. TF.EPILOGUE_COLSUM)"""
 import os
 import sys
 import time
@@ -23,7 +24,11 @@ arms = {}
 for val in (False, True):
     torch.manual_seed(0)
     m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False}).to(dev).train()
-    setattr(m, attr, val)
+    if attr.startswith("TF."):            # a hv_amd.train_fn module switch, set around each arm's steps
+        import hv_amd.train_fn as TF
+        setattr(TF, attr[3:], val)
+    else:
+        setattr(m, attr, val)
     arms[val] = HVTrainer(m, monitor_every=0, graph=True)
     for _ in range(3):
         arms[val].step(x, tg)
@@ -32,6 +37,8 @@ res = {False: [], True: []}
 for rnd in range(3):
     for val in (False, True):
         tr = arms[val]
+        if attr.startswith("TF."):
+            setattr(TF, attr[3:], val)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(N):
