@@ -408,6 +408,356 @@ __global__ void __launch_bounds__(512, 1) mhc_tok_kernel(TokArgs args) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Hidden-split form (HV_MV_TOKSPLIT2 / 4; (D, Hd) = (256, 512), 16-token tiles).  With few tiles
+// (T = 401 at B=1: 26 workgroups) every workgroup streaming all 2 MB of the site's weights leaves
+// most CUs idle; here NSPL workgroups share a tile, part s owning the h2 units
+// [s HD/NSPL, (s+1) HD/NSPL): each part runs GEMM1 in full (the h1 all of GEMM2 reads), GEMM2 for
+// its h2 units only (the 8 waves split the contraction four / two ways per 64-unit group and
+// sum in LDS in fixed order), and the share of GEMM3 those units (+ x columns [s D/NSPL, ..))
+// contribute.  The parts' fp32 partial y go to a workspace; the LAST part to finish (agent-scope
+// release + ticket counter, acquire) sums them in part order (deterministic) and runs LN_post.
+// Weight bytes per workgroup: A1 + (W2 + Wc) / NSPL (0.86 MB at NSPL = 4 instead of 2 MB).
+template <int D, int HD, int NSPL>
+struct CfgS {
+  static constexpr int NW = 8, NT = 512, TW = 16;
+  static constexpr int KS1 = D / 32, KP1 = D / 64;                 // GEMM1 contraction (D)
+  static constexpr int KS2 = 2 * HD / 32, KP2 = 2 * HD / 64;       // GEMM2 contraction (2HD)
+  static constexpr int HDS = HD / NSPL;                            // h2 units of one part
+  static constexpr int NG2 = HDS / 64, WPG = NW / NG2, KPW2 = KP2 / WPG;   // unit groups, waves per group, k-pairs per wave
+  static constexpr int XPP = D / NSPL / 64;                        // x k-pairs of this part's GEMM3 share
+  static constexpr int KP3 = XPP + NG2;                            // + its h2 k-pairs
+  static constexpr int N1W = 2 * HD / NW, G1 = N1W / 64;
+  static constexpr int N3W = D / NW, J3 = N3W / 16;
+  static constexpr int S1 = G1 * KP1, S2 = KPW2, S3 = KP3, S = S1 + S2 + S3;
+  // LDS: z (then this part's h2 images) | x images | h1 images | GEMM2 partials | constants | transposers | flag
+  static constexpr int ZB = KS1 * 1024, H2B = (HDS / 32) * 1024;
+  static constexpr int ZF = 0, H2F = 0, XF = ZB > H2B ? ZB : H2B, H1F = XF + KS1 * 1024;
+  static constexpr int R2F = H1F + KS2 * 1024;                     // [NW][4 tiles][64 lanes] f32x4
+  static constexpr int C1S = R2F + NW * 4 * 64 * 16, B2S = C1S + 2 * HD * 4, GPS = B2S + HD * 4, BPS = GPS + D * 4;
+  static constexpr int TRS = BPS + D * 4, FLAG = TRS + NW * 4096, LDS = FLAG + 16;
+  static constexpr int CPL = D / 64;                               // LN_post columns per lane
+  static_assert(NG2 >= 1 && NW % NG2 == 0 && KP2 % WPG == 0 && XPP >= 1 && (D / NSPL) % 64 == 0, "split shape");
+  static_assert(D % 128 == 0 && G1 >= 1 && J3 >= 1 && J3 <= 4 && CPL == 4, "shape");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+struct TokSplitArgs {
+  TokSite s[kTokMaxSites];
+  int T, tiles;
+  float* work;       // [sites][tiles][NSPL][16][D] fp32 partial y
+  int* count;        // [sites][tiles] arrival counters, zero before the launch (left zero)
+};
+
+template <int D, int HD, int NSPL, int PF>
+__global__ void __launch_bounds__(512, 1) mhc_toks_kernel(TokSplitArgs args) {
+  using C = CfgS<D, HD, NSPL>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int sy = blockIdx.y;
+  const TokSite st = sy == 0 ? args.s[0] : (sy == 1 ? args.s[1] : args.s[2]);
+  const int T = args.T;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int tile = blockIdx.x / NSPL, part = blockIdx.x % NSPL;
+  const long t0 = (long)tile * 16;
+  const unsigned short* __restrict__ x = st.x;
+  const unsigned short* __restrict__ a1t = st.a1t;
+  const unsigned short* __restrict__ w2 = st.w2;
+  const unsigned short* __restrict__ wct = st.wct;
+
+  float* const c1s = reinterpret_cast<float*>(smem + C::C1S);
+  float* const b2s = reinterpret_cast<float*>(smem + C::B2S);
+  float* const gps = reinterpret_cast<float*>(smem + C::GPS);
+  float* const bps = reinterpret_cast<float*>(smem + C::BPS);
+  for (int i = tid; i < 2 * HD / 4; i += C::NT)
+    reinterpret_cast<float4*>(c1s)[i] = reinterpret_cast<const float4*>(st.c1)[i];
+  for (int i = tid; i < HD / 4; i += C::NT)
+    reinterpret_cast<float4*>(b2s)[i] = reinterpret_cast<const float4*>(st.b2)[i];
+  for (int i = tid; i < D / 4; i += C::NT) {
+    reinterpret_cast<float4*>(gps)[i] = reinterpret_cast<const float4*>(st.g_post)[i];
+    reinterpret_cast<float4*>(bps)[i] = reinterpret_cast<const float4*>(st.b_post)[i];
+  }
+  uint4 xv[C::KP1][2];
+  if (w == 0) {
+    const long tok = min(t0 + fr, (long)T - 1);
+#pragma unroll
+    for (int p = 0; p < C::KP1; ++p) {
+      xv[p][0] = *reinterpret_cast<const uint4*>(x + tok * D + 64 * p + 16 * fg);
+      xv[p][1] = *reinterpret_cast<const uint4*>(x + tok * D + 64 * p + 16 * fg + 8);
+    }
+  }
+
+  // flat k-pair schedule: GEMM1 (all 2HD units), GEMM2 (this wave's contraction share of its unit
+  // group), GEMM3 (this part's x / h2 k-pairs)
+  const int lr = lane >> 3, lc = lane & 7;
+  const int g2 = w / C::WPG, kq = w % C::WPG;
+  auto load_step = [&](auto sc, v4u (&r)[8]) {
+    constexpr int s = decltype(sc)::value;
+    if constexpr (s < C::S1) {
+      constexpr int g = s / C::KP1, p = s % C::KP1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rr = 8 * (i & 1) + lr, q = i >> 1;
+        const int u = w * C::N1W + 64 * g + 16 * (rr >> 2) + 4 * q + (rr & 3);
+        r[i] = *reinterpret_cast<const v4u*>(a1t + (long)u * D + 64 * p + 8 * (lc ^ tsw(rr)));
+      }
+    } else if constexpr (s < C::S1 + C::S2) {
+      constexpr int s2 = s - C::S1;
+      const int kp = kq * C::KPW2 + s2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rr = 8 * (i & 1) + lr, q = i >> 1;
+        const int u = part * C::HDS + 64 * g2 + 16 * (rr >> 2) + 4 * q + (rr & 3);
+        r[i] = *reinterpret_cast<const v4u*>(w2 + (long)u * (2 * HD) + 64 * kp + 8 * (lc ^ tsw(rr)));
+      }
+    } else {
+      constexpr int p = s - C::S1 - C::S2;
+      const int col0 = p < C::XPP ? 64 * (part * C::XPP + p) : D + part * C::HDS + 64 * (p - C::XPP);
+#pragma unroll
+      for (int i = 0; i < 2 * C::J3; ++i) {
+        const int rr = 8 * (i & 1) + lr, q = i >> 1;
+        r[i] = *reinterpret_cast<const v4u*>(wct + (long)(w * C::N3W + 16 * q + rr) * (D + HD) + col0 +
+                                               8 * (lc ^ tsw(rr)));
+      }
+    }
+  };
+  unsigned char* const trs = smem + C::TRS + w * 4096;
+  auto transpose_half = [&](auto hc, auto nc, const v4u (&r)[8], v4u (&a)[4][2]) {
+    constexpr int h = decltype(hc)::value, ntiles = decltype(nc)::value;
+    static_for<4 * h, (4 * h + 4 < 2 * ntiles ? 4 * h + 4 : 2 * ntiles)>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      *reinterpret_cast<v4u*>(trs + ((i >> 1) & 1) * 2048 + (8 * (i & 1) + lr) * 128 + 16 * lc) = r[i];
+    });
+    static_for<2 * h, (2 * h + 2 < ntiles ? 2 * h + 2 : ntiles)>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        a[q][e] = *reinterpret_cast<const v4u*>(trs + (q & 1) * 2048 + fr * 128 + 16 * ((2 * fg + e) ^ tsw(fr)));
+    });
+  };
+  v4u ring[PF][8];
+  static_for<0, PF>([&](auto ic) __attribute__((always_inline)) { load_step(ic, ring[decltype(ic)::value]); });
+
+  // LN_pre (wave 0): x and z = (x - mean) * rstd as B-fragment images
+  if (w == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < C::KP1; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t v[4] = {xv[p][h].x, xv[p][h].y, xv[p][h].z, xv[p][h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s += __uint_as_float(v[e] << 16) + __uint_as_float(v[e] & 0xffff0000u);
+      }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mu = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int p = 0; p < C::KP1; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t v[4] = {xv[p][h].x, xv[p][h].y, xv[p][h].z, xv[p][h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = __uint_as_float(v[e] << 16) - mu, b = __uint_as_float(v[e] & 0xffff0000u) - mu;
+          q += a * a + b * b;
+        }
+      }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rs = rsqrtf(q * (1.0f / D) + 1e-5f);
+#pragma unroll
+    for (int p = 0; p < C::KP1; ++p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t v[4] = {xv[p][h].x, xv[p][h].y, xv[p][h].z, xv[p][h].w};
+        uint32_t z[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          z[e] = pack_bf16x2((__uint_as_float(v[e] << 16) - mu) * rs, (__uint_as_float(v[e] & 0xffff0000u) - mu) * rs);
+        const int blk = (2 * p + h) * 1024 + lane * 16;
+        *reinterpret_cast<uint4*>(smem + C::XF + blk) = xv[p][h];
+        *reinterpret_cast<uint4*>(smem + C::ZF + blk) = make_uint4(z[0], z[1], z[2], z[3]);
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[4];
+  auto act_store = [&](const float* bias, int unit0, int img, int ks_img) __attribute__((always_inline)) {
+    const float4* bp = reinterpret_cast<const float4*>(bias + unit0 + 16 * fg);
+    const float4 bq[4] = {bp[0], bp[1], bp[2], bp[3]};
+    uint32_t hv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 a = acc[q];
+      hv[2 * q] = pack_bf16x2(hv_gelu_fast(a[0] + bq[q].x), hv_gelu_fast(a[1] + bq[q].y));
+      hv[2 * q + 1] = pack_bf16x2(hv_gelu_fast(a[2] + bq[q].z), hv_gelu_fast(a[3] + bq[q].w));
+    }
+    (void)ks_img;
+    unsigned char* b0 = smem + img + (2 * (unit0 / 64)) * 1024 + lane * 16;
+    *reinterpret_cast<uint4*>(b0) = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+    *reinterpret_cast<uint4*>(b0 + 1024) = make_uint4(hv[4], hv[5], hv[6], hv[7]);
+  };
+
+  static_for<0, C::S>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int NTL = s < C::S1 + C::S2 ? 4 : C::J3;
+    v4u raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) raw[i] = ring[s % PF][i];
+    if constexpr (s + PF < C::S) load_step(std::integral_constant<int, s + PF>{}, ring[s % PF]);
+    __builtin_amdgcn_sched_barrier(0);
+    v4u cur[4][2];
+    transpose_half(std::integral_constant<int, 0>{}, std::integral_constant<int, NTL>{}, raw, cur);
+    if constexpr (NTL > 2) transpose_half(std::integral_constant<int, 1>{}, std::integral_constant<int, NTL>{}, raw, cur);
+    if constexpr (s < C::S1) {
+      // GEMM1: z [16 x D] -> h1 units of group g (all 2HD units: every part needs all of h1)
+      constexpr int g = s / C::KP1, p = s % C::KP1;
+      if constexpr (p == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const unsigned char* bz = smem + C::ZF + (2 * p) * 1024 + lane * 16;
+      const uint4 be = *reinterpret_cast<const uint4*>(bz), bo = *reinterpret_cast<const uint4*>(bz + 1024);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q] = mfma_t(cur[q][0], be, acc[q]);
+        acc[q] = mfma_t(cur[q][1], bo, acc[q]);
+      }
+      if constexpr (p == C::KP1 - 1) act_store(c1s, w * C::N1W + 64 * g, C::H1F, C::KS2);
+      if constexpr (s == C::S1 - 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // h1 images complete (z no longer read)
+      }
+    } else if constexpr (s < C::S1 + C::S2) {
+      // GEMM2: this wave's k-pairs [kq KPW2, (kq+1) KPW2) of unit group g2 of this part
+      constexpr int s2 = s - C::S1;
+      if constexpr (s2 == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kp = kq * C::KPW2 + s2;
+      const unsigned char* bh = smem + C::H1F + (2 * kp) * 1024 + lane * 16;
+      const uint4 be = *reinterpret_cast<const uint4*>(bh), bo = *reinterpret_cast<const uint4*>(bh + 1024);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q] = mfma_t(cur[q][0], be, acc[q]);
+        acc[q] = mfma_t(cur[q][1], bo, acc[q]);
+      }
+      if constexpr (s2 == C::KPW2 - 1) {
+        // contraction shares of a unit group -> LDS; its first wave sums them in share order,
+        // adds b2, GELU -> the h2 images of this part (over z)
+        if (kq != 0)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4*>(smem + C::R2F + ((w * 4 + q) * 64 + lane) * 16) = acc[q];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kq == 0) {
+#pragma unroll
+          for (int k = 1; k < C::WPG; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[q] += *reinterpret_cast<const f32x4*>(smem + C::R2F + (((w + k) * 4 + q) * 64 + lane) * 16);
+          act_store(b2s + part * C::HDS, 64 * g2, C::H2F, C::HDS / 32);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // this part's h2 images complete
+      }
+    } else {
+      // GEMM3 share: [x k-pairs of this part | this part's h2] -> partial y columns
+      constexpr int p = s - C::S1 - C::S2;
+      if constexpr (p == 0)
+#pragma unroll
+        for (int j = 0; j < C::J3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const unsigned char* bb = p < C::XPP ? smem + C::XF + (2 * (part * C::XPP + p)) * 1024
+                                           : smem + C::H2F + (2 * (p - C::XPP)) * 1024;
+      const uint4 be = *reinterpret_cast<const uint4*>(bb + lane * 16);
+      const uint4 bo = *reinterpret_cast<const uint4*>(bb + 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < C::J3; ++j) {
+        acc[j] = mfma_t(cur[j][0], be, acc[j]);
+        acc[j] = mfma_t(cur[j][1], bo, acc[j]);
+      }
+    }
+  });
+
+  // ---- partial y -> workspace; the last part of the tile to arrive reduces (fixed part order)
+  const long tbase = ((long)sy * args.tiles + tile) * NSPL;
+  float* const wsp = args.work + (tbase + part) * 16 * D;
+#pragma unroll
+  for (int j = 0; j < C::J3; ++j)
+    *reinterpret_cast<f32x4*>(wsp + fr * D + w * C::N3W + 16 * j + 4 * fg) = acc[j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* const flag = reinterpret_cast<int*>(smem + C::FLAG);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* const cnt = args.count + (long)sy * args.tiles + tile;
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == NSPL - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next launch
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+
+  constexpr int CPL = C::CPL;
+  float gv[CPL], bv[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) { gv[c] = gps[lane * CPL + c]; bv[c] = bps[lane * CPL + c]; }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int lt = w + 8 * i;
+    const long tok = t0 + lt;
+    const float* src = args.work + tbase * 16 * D + lt * D + lane * CPL;
+    f32x4 yv = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+    for (int q = 1; q < NSPL; ++q) yv += *reinterpret_cast<const f32x4*>(src + (long)q * 16 * D);
+    float v[CPL] = {yv[0], yv[1], yv[2], yv[3]};
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) s += v[c];
+    const float mu = wave_sum(s) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) { const float d0 = v[c] - mu; q += d0 * d0; }
+    const float inv = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+    if (tok < T) {
+      float o[CPL];
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) o[c] = (v[c] - mu) * inv * gv[c] + bv[c];
+      if (st.res) {
+        const unsigned short* rp = st.res + tok * D + lane * CPL;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) o[c] += bf2f(rp[c]);
+      }
+      *reinterpret_cast<uint2*>(st.out + tok * D + lane * CPL) =
+          make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+    }
+  }
+}
+
+template <int D, int HD, int NSPL, int PF>
+int launch_toks(const TokSplitArgs& ta, int nsites, hipStream_t s) {
+  using C = CfgS<D, HD, NSPL>;
+  auto k = mhc_toks_kernel<D, HD, NSPL, PF>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hv_diag_count(HV_KF_MHC_FUSED);
+  k<<<dim3(ta.tiles * NSPL, nsites), C::NT, C::LDS, s>>>(ta);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
 template <int D, int HD, int TW, int PF>
 int launch_tok(const TokArgs& ta, int nsites, hipStream_t s) {
   using C = CfgT<D, HD, TW>;
@@ -444,6 +794,18 @@ int hv_mhc_tok_launch(const hv_mhc_fused_args* a, int n, hipStream_t s) {
   }
   const bool t16 = (a[0].variant & HV_MV_TOK16) != 0;
   const int D = a[0].D, Hd = a[0].Hd;
+  const int spl = a[0].variant & HV_MV_TOKSPLIT4 ? 4 : (a[0].variant & HV_MV_TOKSPLIT2 ? 2 : 1);
+  if (spl > 1) {
+    // hidden-split form: workspace + zeroed arrival counters from the caller (hv_kernels.h)
+    if (D != 256 || Hd != 512 || !a[0].split_work || !a[0].split_count) return HV_EINVAL;
+    TokSplitArgs sa{};
+    for (int i = 0; i < n; ++i) sa.s[i] = ta.s[i];
+    sa.T = ta.T;
+    sa.tiles = hv_cdiv(ta.T, 16);
+    sa.work = a[0].split_work;
+    sa.count = a[0].split_count;
+    return spl == 4 ? launch_toks<256, 512, 4, 2>(sa, n, s) : launch_toks<256, 512, 2, 2>(sa, n, s);
+  }
   if (D == 128 && Hd == 512) return t16 ? launch_tok<128, 512, 16, 2>(ta, n, s) : launch_tok<128, 512, 32, 2>(ta, n, s);
   if (D == 256 && Hd == 512) return t16 ? launch_tok<256, 512, 16, 2>(ta, n, s) : launch_tok<256, 512, 32, 2>(ta, n, s);
   if (D == 256 && Hd == 1024) return launch_tok<256, 1024, 16, 2>(ta, n, s);

@@ -26,6 +26,7 @@ MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_
 MV_SPLIT256, MV_SPLITW = 0x200, 12
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
 MV_TOK, MV_TOK16 = 0x400, 0x800
+MV_TOKSPLIT2, MV_TOKSPLIT4 = 0x1000, 0x2000
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
 ABI_VERSION = 3          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
@@ -115,7 +116,8 @@ class ParamEntry(C.Structure):
 class MhcFusedArgs(C.Structure):
     _fields_ = [("dtype", i32), ("D", i32), ("Hd", i32), ("T", i32),
                 ("x", vp), ("a1t", vp), ("c1", vp), ("w2", vp), ("b2", vp), ("wct", vp),
-                ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp), ("variant", i32), ("pad_", i32)]
+                ("g_post", vp), ("b_post", vp), ("residual", vp), ("out", vp), ("variant", i32), ("pad_", i32),
+                ("split_work", vp), ("split_count", vp)]
 
 
 class SymeigEntry(C.Structure):

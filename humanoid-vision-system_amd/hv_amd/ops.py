@@ -317,9 +317,41 @@ def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
     if Hd is None or T > TOK_MAX_T.get((D, Hd), -1):
         return 0
     v = L.MV_TOK
-    if -(-T // 16) * nsites <= TOK_CUS:
+    tiles16 = -(-T // 16) * nsites
+    if tiles16 <= TOK_CUS:
         v |= L.MV_TOK16
+        # at most a quarter as many tiles as CUs: each tile's hidden units split over 4
+        # workgroups (per launch, profiles/r05/mhc_toksplit_ab.txt: T = 401 21.1 vs 23.2 us, T = 16
+        # 17.6 vs 22.7; in-model B=1 frozen p50 4.20-4.25 vs 4.43-4.46 ms).  The 2-way split is
+        # kept for tests only: 24.5 vs 25.1 us on the grouped q / k / v at T = 401, and slower
+        # than the unsplit kernel at T = 1,604 (26.9 vs 24.0)
+        if (D, Hd) == (256, 512) and options().mhc_tok_split and 4 * tiles16 <= TOK_CUS:
+            v |= L.MV_TOKSPLIT4
     return v
+
+
+_TOKSPLIT_COUNTERS: dict = {}
+TOKSPLIT_MAX_TILES = 4096
+
+
+def _tok_split_buffers(a, n: int, T: int, D: int, variant: int, device):
+    """Workspace + arrival counters of a hidden-split token-tile launch (hv_kernels.h
+    HV_MV_TOKSPLIT*), set on the first site's args.  Counters are per (device, stream), zero and
+    left zero by every launch; launches on one stream are ordered, so they can share them.
+    Returns the workspace (kept alive by the caller until the launch is enqueued)."""
+    nspl = 4 if variant & L.MV_TOKSPLIT4 else (2 if variant & L.MV_TOKSPLIT2 else 1)
+    if nspl == 1:
+        return None
+    tiles = -(-T // 16) * n
+    if tiles > TOKSPLIT_MAX_TILES:
+        raise ValueError(f"token-tile split: {tiles} tiles > {TOKSPLIT_MAX_TILES}")
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    c = _TOKSPLIT_COUNTERS.get(key)
+    if c is None:
+        c = _TOKSPLIT_COUNTERS[key] = torch.zeros(TOKSPLIT_MAX_TILES, device=device, dtype=torch.int32)
+    work = torch.empty(tiles * nspl * 16 * D, device=device, dtype=torch.float32)
+    a.split_work, a.split_count = work.data_ptr(), c.data_ptr()
+    return work
 
 
 def mhc_fused_supported(D: int, Hd: int, dtype: torch.dtype, variant: Optional[int] = None,
@@ -343,9 +375,11 @@ def mhc_fused(x: Tensor, a1t, c1, w2, b2, wct, g_post, b_post, residual: Optiona
     if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype or not residual.is_contiguous()):
         raise ValueError("mhc_fused: residual must match x")
     out = torch.empty_like(x)
+    v = _mhc_variant(D, T, variant, Hd)
     a = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), a1t.data_ptr(), c1.data_ptr(), w2.data_ptr(),
                        b2.data_ptr(), wct.data_ptr(), g_post.data_ptr(), b_post.data_ptr(), ptr(residual),
-                       out.data_ptr(), _mhc_variant(D, T, variant, Hd), 0)
+                       out.data_ptr(), v, 0)
+    work = _tok_split_buffers(a, 1, T, D, v, x.device)     # noqa: F841  (alive until enqueued)
     check(L.lib().hv_mhc_fused(C.byref(a), stream_ptr()), f"hv_mhc_fused D={D}")
     return out
 
@@ -377,6 +411,7 @@ def mhc_fused_group(x: Tensor, plans, variant: int) -> list:
         arr[i] = L.MhcFusedArgs(dtype_code(x.dtype), D, Hd, T, x.data_ptr(), p.b1.data_ptr(), p.c1.data_ptr(),
                                 p.w2.data_ptr(), p.bias2.data_ptr(), p.wct.data_ptr(), p.g_post.data_ptr(),
                                 p.b_post.data_ptr(), None, o.data_ptr(), variant, 0)
+    work = _tok_split_buffers(arr[0], n, T, D, variant, x.device)     # noqa: F841  (alive until enqueued)
     check(L.lib().hv_mhc_fused_group(arr, n, stream_ptr()), f"hv_mhc_fused_group D={D} n={n}")
     return outs
 

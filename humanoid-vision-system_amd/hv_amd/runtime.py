@@ -41,6 +41,7 @@ class HVOptions:
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
     mhc256_min_tokens: int = 25600    # D = 256 sites fused (split-hidden) from this many tokens (ops._mhc_variant)
     mhc_tok: bool = True              # token-tile fused kernel for small-T sites (HV_MV_TOK, ops._mhc_variant)
+    mhc_tok_split: bool = True        # ... with a tile's hidden units split over 2 / 4 workgroups when tiles < CUs
     branch_min_batch: int = 8         # independent branches on side streams from this batch (Branches)
 
     def replace(self, **kw) -> "HVOptions":

@@ -35,8 +35,8 @@ enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
 /* ABI version: 2 since hv_adamw gained `steps` and `active`, hv_grad_norms `active`, the dropout
  * entry points and hv_gemm_desc a device `seed_offset`, hv_mhc_fused_supported gained `variant`,
  * hv_mhc_fused_args grew by 8 bytes and the hv_gemm_set_* / hv_mhc_fused_set_* setters were
- * removed; 3 since hv_gemm_desc gained `colsum_part` (appended).  Bindings compare it with the
- * version they were written against. */
+ * removed; 3 since hv_gemm_desc gained `colsum_part` and hv_mhc_fused_args `split_work` /
+ * `split_count` (appended).  Bindings compare it with the version they were written against. */
 #define HV_ABI_VERSION 3
 int hv_abi_version(void);
 /* build provenance: a hash of the sources (the .hip / .h files of csrc, the include headers, the Makefile) the
@@ -241,6 +241,11 @@ typedef struct hv_mhc_fused_args {
   void* out;            /* [T, D] */
   int variant;          /* per-call kernel selection, 0 = automatic; HV_MV_* below */
   int pad_;
+  /* HV_MV_TOKSPLIT2 / 4 only (read from the first site of a group): fp32 workspace of
+     n_sites * ceil(T / 16) * NSPL * 16 * D floats, and n_sites * ceil(T / 16) int arrival
+     counters that are zero before the launch (every launch leaves them zero) */
+  float* split_work;
+  int* split_count;
 } hv_mhc_fused_args;
 #define HV_MV_SHAPE_MASK  0xff   /* workgroup shape: 1 three 4-wave groups per CU, 2 one 8-wave group,
                                     5 (D = 128) the per-wave 4-wave kernel instead of split-hidden,
@@ -256,6 +261,8 @@ typedef struct hv_mhc_fused_args {
                                     weights streamed L2 -> registers; (D, Hd) in {(128, 512), (256, 512),
                                     (256, 1024)} -- small token counts (ViT, B=1) */
 #define HV_MV_TOK16       0x800  /* with HV_MV_TOK: 16-token tiles (Hd = 1024 always uses 16) */
+#define HV_MV_TOKSPLIT2   0x1000 /* with HV_MV_TOK, (256, 512): 16-token tiles shared by 2 / 4 workgroups, each */
+#define HV_MV_TOKSPLIT4   0x2000 /* owning Hd / NSPL of the h2 units; the last to finish reduces (split_work) */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
 int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant);

@@ -31,7 +31,9 @@ T_ = _lib.MV_TOK
 CASES = {"unfused": HVOptions(use_fused_mhc=False, mhc_tok=False),
          "fused_old": HVOptions(mhc_tok=False, mhc256_min_tokens=0),
          "tok32": HVOptions(mhc_variant=T_),
-         "tok16": HVOptions(mhc_variant=T_ | _lib.MV_TOK16)}
+         "tok16": HVOptions(mhc_variant=T_ | _lib.MV_TOK16),
+         "toks2": HVOptions(mhc_variant=T_ | _lib.MV_TOK16 | _lib.MV_TOKSPLIT2),
+         "toks4": HVOptions(mhc_variant=T_ | _lib.MV_TOK16 | _lib.MV_TOKSPLIT4)}
 
 for D, T, ex in shapes:
     Hd = ex * D
@@ -58,7 +60,10 @@ for D, T, ex in shapes:
         if ops.mhc_fused_supported(D, Hd, torch.bfloat16, variant=T_):
             ms = [ManifoldHyperConnection(D, expansion_rate=ex).cuda().eval() for _ in range(3)]
             ps = [mm.plan() for mm in ms]
-            for tag, v in (("tok32", T_), ("tok16", T_ | _lib.MV_TOK16)):
+            for tag, v in (("tok32", T_), ("tok16", T_ | _lib.MV_TOK16), ("toks2", T_ | _lib.MV_TOK16 | _lib.MV_TOKSPLIT2),
+                           ("toks4", T_ | _lib.MV_TOK16 | _lib.MV_TOKSPLIT4)):
+                if not ops.mhc_fused_supported(D, Hd, torch.bfloat16, variant=v):
+                    continue
                 outs = ops.mhc_fused_group(x, ps, v)
                 with use_ctx(RunCtx(dtype=torch.bfloat16, opts=HVOptions(mhc_variant=v))):
                     singles = [MF.mhc_apply(x, pp) for pp in ps]
