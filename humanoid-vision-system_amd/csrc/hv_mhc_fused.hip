@@ -1044,7 +1044,8 @@ int hv_mhc_tok_launch(const hv_mhc_fused_args* a, int n, hipStream_t s);
 extern "C" int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant) {
   if (dtype != HV_BF16) return 0;
   if (variant & HV_MV_TOK)
-    return (variant & (HV_MV_TOKSPLIT2 | HV_MV_TOKSPLIT4)) ? (D == 256 && Hd == 512) : hv_mhc_tok_supported(D, Hd);
+    return (variant & (HV_MV_TOKSPLIT2 | HV_MV_TOKSPLIT4)) ? (D == 256 && (Hd == 512 || Hd == 1024))
+                                                           : hv_mhc_tok_supported(D, Hd);
   return (D == 32 && Hd == 128) || (D == 64 && Hd == 256) || (D == 128 && Hd == 512) ||
          (D == 256 && Hd == 512 && (variant & (HV_MV_WIDE | HV_MV_SPLIT256)));
 }

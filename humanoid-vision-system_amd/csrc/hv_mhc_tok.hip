@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(512, 1) mhc_tok_kernel(TokArgs args) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Hidden-split form (HV_MV_TOKSPLIT2 / 4; (D, Hd) = (256, 512), 16-token tiles).  With few tiles
+// Hidden-split form (HV_MV_TOKSPLIT2 / 4; D = 256, Hd = 512 or 1024, 16-token tiles).  With few tiles
 // (T = 401 at B=1: 26 workgroups) every workgroup streaming all 2 MB of the site's weights leaves
 // most CUs idle; here NSPL workgroups share a tile, part s owning the h2 units
 // [s HD/NSPL, (s+1) HD/NSPL): each part runs GEMM1 in full (the h1 all of GEMM2 reads), GEMM2 for
@@ -433,8 +433,9 @@ struct CfgS {
   // LDS: z (then this part's h2 images) | x images | h1 images | GEMM2 partials | constants | transposers | flag
   static constexpr int ZB = KS1 * 1024, H2B = (HDS / 32) * 1024;
   static constexpr int ZF = 0, H2F = 0, XF = ZB > H2B ? ZB : H2B, H1F = XF + KS1 * 1024;
-  static constexpr int R2F = H1F + KS2 * 1024;                     // [NW][4 tiles][64 lanes] f32x4
-  static constexpr int C1S = R2F + NW * 4 * 64 * 16, B2S = C1S + 2 * HD * 4, GPS = B2S + HD * 4, BPS = GPS + D * 4;
+  static constexpr int R2F = H1F + KS2 * 1024;                     // [NW][4 tiles][64 lanes] f32x4 (WPG > 1)
+  static constexpr int R2B = WPG > 1 ? NW * 4 * 64 * 16 : 0;
+  static constexpr int C1S = R2F + R2B, B2S = C1S + 2 * HD * 4, GPS = B2S + HD * 4, BPS = GPS + D * 4;
   static constexpr int TRS = BPS + D * 4, FLAG = TRS + NW * 4096, LDS = FLAG + 16;
   static constexpr int CPL = D / 64;                               // LN_post columns per lane
   static_assert(NG2 >= 1 && NW % NG2 == 0 && KP2 % WPG == 0 && XPP >= 1 && (D / NSPL) % 64 == 0, "split shape");
@@ -797,13 +798,14 @@ int hv_mhc_tok_launch(const hv_mhc_fused_args* a, int n, hipStream_t s) {
   const int spl = a[0].variant & HV_MV_TOKSPLIT4 ? 4 : (a[0].variant & HV_MV_TOKSPLIT2 ? 2 : 1);
   if (spl > 1) {
     // hidden-split form: workspace + zeroed arrival counters from the caller (hv_kernels.h)
-    if (D != 256 || Hd != 512 || !a[0].split_work || !a[0].split_count) return HV_EINVAL;
+    if (D != 256 || (Hd != 512 && Hd != 1024) || !a[0].split_work || !a[0].split_count) return HV_EINVAL;
     TokSplitArgs sa{};
     for (int i = 0; i < n; ++i) sa.s[i] = ta.s[i];
     sa.T = ta.T;
     sa.tiles = hv_cdiv(ta.T, 16);
     sa.work = a[0].split_work;
     sa.count = a[0].split_count;
+    if (Hd == 1024) return spl == 4 ? launch_toks<256, 1024, 4, 2>(sa, n, s) : launch_toks<256, 1024, 2, 2>(sa, n, s);
     return spl == 4 ? launch_toks<256, 512, 4, 2>(sa, n, s) : launch_toks<256, 512, 2, 2>(sa, n, s);
   }
   if (D == 128 && Hd == 512) return t16 ? launch_tok<128, 512, 16, 2>(ta, n, s) : launch_tok<128, 512, 32, 2>(ta, n, s);

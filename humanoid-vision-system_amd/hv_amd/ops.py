@@ -309,7 +309,7 @@ def _mhc_variant(D: int, T: Optional[int], variant: Optional[int], Hd: Optional[
 # (64 vs 94 us); (256, 1024) ties the chain at 1,600 and loses at 6,400: not taken.  Every
 # workgroup streams all of a site's weights, so 16-token tiles (twice the workgroups) win while
 # the grid fits the 256 CUs in one round, 32-token tiles (half the weight traffic per token) after.
-TOK_MAX_T = {(128, 512): 12800, (256, 512): 51200}
+TOK_MAX_T = {(128, 512): 12800, (256, 512): 51200, (256, 1024): 2048}   # (256, 1024): hidden split only
 TOK_CUS = 256
 
 
@@ -327,6 +327,12 @@ def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
         # than the unsplit kernel at T = 1,604 (26.9 vs 24.0)
         if (D, Hd) == (256, 512) and options().mhc_tok_split and 4 * tiles16 <= TOK_CUS:
             v |= L.MV_TOKSPLIT4
+    if (D, Hd) == (256, 1024):
+        # (256, 1024) only split (5.9 MB of weights per unsplit workgroup ties the chain): T = 400
+        # 32.6 (4-way) vs 57.7 us chain, T = 1,600 48.7 (2-way) vs 62.6 us
+        if not (options().mhc_tok_split and v & L.MV_TOK16 and 2 * tiles16 <= TOK_CUS):
+            return 0
+        v |= L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2
     return v
 
 

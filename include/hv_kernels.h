@@ -261,7 +261,7 @@ typedef struct hv_mhc_fused_args {
                                     weights streamed L2 -> registers; (D, Hd) in {(128, 512), (256, 512),
                                     (256, 1024)} -- small token counts (ViT, B=1) */
 #define HV_MV_TOK16       0x800  /* with HV_MV_TOK: 16-token tiles (Hd = 1024 always uses 16) */
-#define HV_MV_TOKSPLIT2   0x1000 /* with HV_MV_TOK, (256, 512): 16-token tiles shared by 2 / 4 workgroups, each */
+#define HV_MV_TOKSPLIT2   0x1000 /* with HV_MV_TOK, D = 256, Hd 512 / 1024: 16-token tiles shared by 2 / 4 workgroups, each */
 #define HV_MV_TOKSPLIT4   0x2000 /* owning Hd / NSPL of the h2 units; the last to finish reduces (split_work) */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
