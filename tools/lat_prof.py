@@ -12,6 +12,13 @@ from hv_amd import HybridVisionSystem  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 torch.manual_seed(0)
 m = HybridVisionSystem({"image_size": 640, "precision": "bf16", "verbose": False}).cuda().eval()
+if os.environ.get("HV_SET"):       # e.g. HV_SET="detect.LATERALS_BESIDE_VIT=False": hv_amd module switches
+    import ast
+    import importlib
+    for kv in os.environ["HV_SET"].split(","):
+        k, v = kv.split("=")
+        mod, name = k.rsplit(".", 1)
+        setattr(importlib.import_module("hv_amd." + mod), name, ast.literal_eval(v))
 if os.environ.get("HV_OPTS"):      # e.g. HV_OPTS="branch_min_batch=1,mhc_tok=False"
     import ast
     m.set_options(**{k: ast.literal_eval(v) for k, v in (kv.split("=") for kv in os.environ["HV_OPTS"].split(","))})
