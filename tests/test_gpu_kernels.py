@@ -484,11 +484,11 @@ def test_se_mlp_batched_vs_torch(gpu_device, n, c):
 
 @pytest.mark.parametrize("n,h,c,dt", [(1, 80, 64, torch.bfloat16), (3, 40, 128, torch.bfloat16),
                                       (16, 20, 256, torch.bfloat16), (5, 13, 32, torch.float32),
-                                      (2, 10, 1024, torch.float32)])
+                                      (2, 10, 1024, torch.float32), (1, 320, 32, torch.bfloat16)])
 def test_se_gate_matches_mean_then_mlp_bitwise(gpu_device, n, h, c, dt):
     """hv_se_gate (pool chunk sums + MLP finishing the mean) is bitwise hv_channel_mean followed by
-    hv_se_mlp2, on both MLP forms (n <= 4 batched, n > 4 per image), and agrees with CPU fp32 torch
-    of vision_backbone.py:77-83 on the same rounded input."""
+    hv_se_mlp2, on both MLP forms (n <= 4 batched, n > 4 per image), repeatably, and agrees with CPU
+    fp32 torch of vision_backbone.py:77-83 on the same rounded input."""
     ops = _ops()
     cr = max(c // 16, 4)
     g = torch.Generator().manual_seed(n * 131 + h + c)
@@ -498,8 +498,10 @@ def test_se_gate_matches_mean_then_mlp_bitwise(gpu_device, n, h, c, dt):
     xd, ws = x.to(gpu_device), [t.to(gpu_device) for t in (w1, b1, w2, b2)]
     fused = ops.se_gate(xd, *ws)
     pair = ops.se_mlp(ops.channel_mean(xd), *ws)
+    again = ops.se_gate(xd, *ws)
     torch.cuda.synchronize()
     assert torch.equal(fused, pair)
+    assert torch.equal(fused, again)
     ref = torch.sigmoid(F.linear(F.silu(F.linear(x.float().mean((1, 2)), w1, b1)), w2, b2))
     assert rel_err(fused, ref) < 1e-5
 
