@@ -26,7 +26,7 @@ MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_
 MV_SPLIT256, MV_SPLITW = 0x200, 12
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
 MV_TOK, MV_TOK16 = 0x400, 0x800
-MV_TOKSPLIT2, MV_TOKSPLIT4 = 0x1000, 0x2000
+MV_TOKSPLIT2, MV_TOKSPLIT4, MV_TOKSPLIT_SC1 = 0x1000, 0x2000, 0x4000
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
 ABI_VERSION = 3          # include/hv_kernels.h HV_ABI_VERSION this binding is written against

@@ -326,14 +326,17 @@ def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
         # kept for tests only: 24.5 vs 25.1 us on the grouped q / k / v at T = 401, and slower
         # than the unsplit kernel at T = 1,604 (26.9 vs 24.0)
         if (D, Hd) == (256, 512) and options().mhc_tok_split and 4 * tiles16 <= TOK_CUS:
-            v |= L.MV_TOKSPLIT4
+            v |= L.MV_TOKSPLIT4 | (L.MV_TOKSPLIT_SC1 if TOKSPLIT_SC1 else 0)
     if (D, Hd) == (256, 1024):
         # (256, 1024) only split (5.9 MB of weights per unsplit workgroup ties the chain): T = 400
         # 32.6 (4-way) vs 57.7 us chain, T = 1,600 48.7 (2-way) vs 62.6 us
         if not (options().mhc_tok_split and v & L.MV_TOK16 and 2 * tiles16 <= TOK_CUS):
             return 0
-        v |= L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2
+        v |= (L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2) | (L.MV_TOKSPLIT_SC1 if TOKSPLIT_SC1 else 0)
     return v
+
+
+TOKSPLIT_SC1 = False      # split token-tile hand-off by write-through stores instead of fences (A/B: equal)
 
 
 _TOKSPLIT_COUNTERS: dict = {}

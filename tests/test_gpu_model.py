@@ -172,7 +172,7 @@ def test_mhc_fused_kernel_matches_unfused_chain(gpu_device, D, e, T, with_res):
     assert np.abs(y1 - y0).max() < 0.1
 
 
-@pytest.mark.parametrize("tile", [16, 32, "split2", "split4"])
+@pytest.mark.parametrize("tile", [16, 32, "split2", "split4", "split4_sc1"])
 @pytest.mark.parametrize("D,e,T,with_res", [(256, 2, 401, False), (256, 2, 401, True), (256, 2, 6416, True),
                                              (256, 2, 130, False), (256, 2, 7, True), (128, 4, 1000, False),
                                              (128, 4, 6400, True), (256, 4, 1600, True), (256, 4, 77, False)])
@@ -191,7 +191,8 @@ def test_mhc_tok_kernel_matches_unfused_chain(gpu_device, tile, D, e, T, with_re
     x = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device)
     res = torch.randn(T, D, generator=g).to(torch.bfloat16).to(gpu_device) if with_res else None
     v = _lib.MV_TOK | (_lib.MV_TOK16 if tile != 32 else 0)
-    v |= {"split2": _lib.MV_TOKSPLIT2, "split4": _lib.MV_TOKSPLIT4}.get(tile, 0)
+    v |= {"split2": _lib.MV_TOKSPLIT2, "split4": _lib.MV_TOKSPLIT4,
+          "split4_sc1": _lib.MV_TOKSPLIT4 | _lib.MV_TOKSPLIT_SC1}.get(tile, 0)
     from hv_amd import ops
     with torch.no_grad():
         ops.launch_counts(reset=True)
