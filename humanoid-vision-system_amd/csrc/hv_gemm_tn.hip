@@ -13,6 +13,9 @@
 // 8 consecutive image rows, conflict-free with a 32-byte row pad.
 // Split-K over p: blockIdx.y owns a p range, partials go to `work` and hv_wgrad_reduce sums them
 // in a fixed order (deterministic).  B may be an implicit im2col of an NHWC image.
+// KM > 1 (hv_wgrad_desc.variant HV_WV_K64): each LDS stage holds KM k-steps (one barrier per
+// KM x 32 rows); the MFMAs run in the same k order, and the p partition is the KM = 1 plan's, so
+// the result is bitwise the KM = 1 result (a stage past a split's end multiplies zero rows).
 #include "hv_common.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -29,9 +32,10 @@ __device__ __forceinline__ v4i16 tr_read(const unsigned char* p) {
 }
 
 // BGATHER: 0 dense B, 1 conv im2col with 16-B channel chunks, 2 conv im2col scalar
-template <typename T, int BM, int BN, int BGATHER>
+template <typename T, int BM, int BN, int BGATHER, int KM = 1>
 __global__ void __launch_bounds__(256) gemm_tn_kernel(const hv_wgrad_desc d, int p_chunk) {
-  constexpr int KSTEP = TnTr<T>::KSTEP, EPC = TnTr<T>::EPC;
+  constexpr int KSTEP = TnTr<T>::KSTEP * KM, EPC = TnTr<T>::EPC;
+  constexpr int KS1 = TnTr<T>::KSTEP;               // MFMA k-step (rows per permuted block)
   constexpr int APITCH = BM * (int)sizeof(T) + 32;
   constexpr int BPITCH = BN * (int)sizeof(T) + 32;
   constexpr int ACH = KSTEP * BM / EPC / 256;       // 16-B chunks per thread per k-step
@@ -135,8 +139,10 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(const hv_wgrad_desc d, int
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const unsigned char* sa = As + buf * KSTEP * APITCH;
-    const unsigned char* sb = Bs + buf * KSTEP * BPITCH;
+#pragma unroll
+    for (int h = 0; h < KM; ++h) {
+    const unsigned char* sa = As + (buf * KSTEP + h * KS1) * APITCH;
+    const unsigned char* sb = Bs + (buf * KSTEP + h * KS1) * BPITCH;
     if constexpr (IS_BF16) {
       bf16x8 fa[RM], fb[RN];
 #pragma unroll
@@ -175,6 +181,7 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(const hv_wgrad_desc d, int
           for (int b = 0; b < RN; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[b], fa[a], acc[a][b], 0, 0, 0);
       }
+    }
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
@@ -223,11 +230,46 @@ __global__ void k_wgrad_reduce(const float* __restrict__ work, int splits, int N
   }
 }
 
+// Many-split form (splits > 64, small outputs over many pixels): a block owns 64 output columns
+// and its 4 thread groups take the splits g, g + 4, ... with 8 loads in flight each, combined in
+// a fixed order through LDS (deterministic).  The one-thread-per-output form above would wait
+// splits / 4 memory latencies per thread.
+__global__ void __launch_bounds__(256) k_wgrad_reduce_many(const float* __restrict__ work, int splits, int N1,
+                                                           int N2, float* C, long ldc, int accumulate) {
+  __shared__ float part[4][64];
+  const long total = (long)N1 * N2;
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long i = blockIdx.x * 64L + c;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    int k = g;
+    for (; k + 28 < splits; k += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += work[(long)(k + 4 * u) * total + i];
+    }
+    for (int u = 0; k < splits; k += 4, ++u) a[u] += work[(long)k * total + i];
+  }
+  part[g][c] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (g == 0 && i < total) {
+    const float s = (part[0][c] + part[1][c]) + (part[2][c] + part[3][c]);
+    const long n1 = i / N2, n2 = i - n1 * N2;
+    float* o = C + n1 * ldc + n2;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
 struct TnPlan {
   int bm, bn, splits, p_chunk;
 };
 
-TnPlan plan_tn(int P, int N1, int N2, int kstep) {
+// split cap: 256 (small outputs over many pixels -- e.g. 128 x 64 over 409,600 pixels is ONE
+// tile, which at the round-4 cap of 64 ran on 64 workgroups); HV_WV_CAP64 keeps the old cap
+// (a 1024-workgroup target with up to 1024 splits measured slower: 128.55 -> 132.48 ms/step,
+// profiles/r05/wgrad_plan_ab.txt)
+constexpr int kTnMaxSplits = 256;
+
+TnPlan plan_tn(int P, int N1, int N2, int kstep, int max_splits = kTnMaxSplits) {
   TnPlan t;
   t.bm = N1 >= 128 ? 128 : 64;
   t.bn = N2 >= 128 ? 128 : 64;
@@ -240,7 +282,7 @@ TnPlan plan_tn(int P, int N1, int N2, int kstep) {
   s = s < 1 ? 1 : s;
   const long max_s = ksteps / 4 > 0 ? ksteps / 4 : 1; // each split keeps >= 4 k-steps
   s = s > max_s ? max_s : s;
-  s = s > 64 ? 64 : s;
+  s = s > max_splits ? max_splits : s;
   const long per = (ksteps + s - 1) / s;
   t.p_chunk = (int)(per * kstep);
   t.splits = (int)((P + t.p_chunk - 1) / t.p_chunk);
@@ -248,18 +290,29 @@ TnPlan plan_tn(int P, int N1, int N2, int kstep) {
   return t;
 }
 
-template <typename T, int BM, int BN>
-int launch_tn(const hv_wgrad_desc& d, const TnPlan& pl, hipStream_t s) {
+template <typename T, int BM, int BN, int KM>
+void launch_tn_k(const hv_wgrad_desc& d, const TnPlan& pl, hipStream_t s) {
   dim3 grid(hv_cdiv(d.N1, BM) * hv_cdiv(d.N2, BN), pl.splits);
   constexpr int EPC = TnTr<T>::EPC;
   if (d.conv_k > 0) {
-    if (d.conv_c % EPC == 0) gemm_tn_kernel<T, BM, BN, 1><<<grid, 256, 0, s>>>(d, pl.p_chunk);
-    else gemm_tn_kernel<T, BM, BN, 2><<<grid, 256, 0, s>>>(d, pl.p_chunk);
+    if (d.conv_c % EPC == 0) gemm_tn_kernel<T, BM, BN, 1, KM><<<grid, 256, 0, s>>>(d, pl.p_chunk);
+    else gemm_tn_kernel<T, BM, BN, 2, KM><<<grid, 256, 0, s>>>(d, pl.p_chunk);
   } else {
-    gemm_tn_kernel<T, BM, BN, 0><<<grid, 256, 0, s>>>(d, pl.p_chunk);
+    gemm_tn_kernel<T, BM, BN, 0, KM><<<grid, 256, 0, s>>>(d, pl.p_chunk);
   }
+}
+
+template <typename T, int BM, int BN>
+int launch_tn(const hv_wgrad_desc& d, const TnPlan& pl, hipStream_t s) {
+  if (sizeof(T) == 2 && (d.variant & HV_WV_K64)) launch_tn_k<T, BM, BN, 2>(d, pl, s);
+  else launch_tn_k<T, BM, BN, 1>(d, pl, s);
   HV_CHECK_LAUNCH();
-  if (pl.splits > 1) {
+  if (pl.splits > 64) {
+    const long total = (long)d.N1 * d.N2;
+    k_wgrad_reduce_many<<<(unsigned)((total + 63) / 64), 256, 0, s>>>(d.work, pl.splits, d.N1, d.N2, d.C, d.ldc,
+                                                                      d.accumulate);
+    HV_CHECK_LAUNCH();
+  } else if (pl.splits > 1) {
     const long total = (long)d.N1 * d.N2;
     const long nb = (total + 255) / 256;
     const unsigned blocks = (unsigned)(nb < 4096 ? nb : 4096);
@@ -295,7 +348,8 @@ extern "C" int hv_wgrad(const hv_wgrad_desc* dp, hv_stream_t stream) {
   } else if (d.ldb % epc || d.N2 % epc) {
     return HV_EUNSUPPORTED;
   }
-  const TnPlan pl = plan_tn(d.P, d.N1, d.N2, d.dtype == HV_BF16 ? 32 : 16);
+  const TnPlan pl = plan_tn(d.P, d.N1, d.N2, d.dtype == HV_BF16 ? 32 : 16,
+                            (d.variant & HV_WV_CAP64) ? 64 : kTnMaxSplits);
   if (pl.splits > 1 && !d.work) return HV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (d.dtype == HV_BF16) return dispatch_tn<unsigned short>(d, pl, s);

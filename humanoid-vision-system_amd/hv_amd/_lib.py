@@ -94,7 +94,7 @@ class CopySegment(C.Structure):
 class WgradDesc(C.Structure):
     _fields_ = [("dtype", i32), ("P", i32), ("N1", i32), ("N2", i32),
                 ("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("C", vp), ("ldc", i64),
-                ("accumulate", i32), ("pad_", i32), ("work", vp),
+                ("accumulate", i32), ("variant", i32), ("work", vp),
                 ("conv_n", i32), ("conv_h", i32), ("conv_w", i32), ("conv_c", i32),
                 ("conv_k", i32), ("conv_stride", i32), ("conv_pad", i32),
                 ("conv_oh", i32), ("conv_ow", i32), ("pad2_", i32)]

@@ -144,6 +144,7 @@ def wgrad(a: Tensor, b: Tensor, *, out: Optional[Tensor] = None, accumulate: boo
     d.C, d.ldc = out.data_ptr(), out.stride(0)
     d.accumulate = int(accumulate)
     d.work = work.data_ptr()
+    d.variant = options().wgrad_variant
     check(lib.hv_wgrad(C.byref(d), stream_ptr()), f"hv_wgrad P={P} N1={N1} N2={N2}")
     return out
 
@@ -168,6 +169,7 @@ def conv_wgrad(dy: Tensor, x: Tensor, k: int, stride: int, pad: int) -> Tensor:
     d.work = work.data_ptr()
     d.conv_n, d.conv_h, d.conv_w, d.conv_c = n, h, w, cin
     d.conv_k, d.conv_stride, d.conv_pad, d.conv_oh, d.conv_ow = k, stride, pad, oh, ow
+    d.variant = options().wgrad_variant
     check(lib.hv_wgrad(C.byref(d), stream_ptr()), f"hv_wgrad(conv {cin}->{cout} k{k})")
     return out
 

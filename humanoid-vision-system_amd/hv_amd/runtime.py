@@ -39,6 +39,7 @@ class HVOptions:
     splitk: bool = False              # split-K for small output grids: measured no gain
     gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
+    wgrad_variant: int = 0            # hv_wgrad_desc.variant for the weight gradients (HV_WV_*), 0 = automatic
     mhc256_min_tokens: int = 25600    # D = 256 sites fused (split-hidden) from this many tokens (ops._mhc_variant)
     mhc_tok: bool = True              # token-tile fused kernel for small-T sites (HV_MV_TOK, ops._mhc_variant)
     mhc_tok_split: bool = True        # ... with a tile's hidden units split over 2 / 4 workgroups when tiles < CUs

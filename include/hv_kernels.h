@@ -518,11 +518,14 @@ typedef struct hv_wgrad_desc {
   const void* B; long ldb;
   float* C; long ldc;
   int accumulate;            /* 1: C += result */
-  int pad_;
+  int variant;               /* 0 = automatic; HV_WV_* below (A/B selections) */
   float* work;
   int conv_n, conv_h, conv_w, conv_c, conv_k, conv_stride, conv_pad, conv_oh, conv_ow;
   int pad2_;
 } hv_wgrad_desc;
+#define HV_WV_K64    0x1       /* bf16: 64 pixel rows per LDS stage (bitwise the default result) */
+#define HV_WV_CAP64  0x2       /* at most 64 pixel splits (the round-4 plan) */
+/* upper bound over every variant's plan */
 size_t hv_wgrad_work_floats(int dtype, int P, int N1, int N2);
 int hv_wgrad(const hv_wgrad_desc* d, hv_stream_t stream);
 

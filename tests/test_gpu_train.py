@@ -52,6 +52,42 @@ def test_wgrad_accumulate(gpu_device):
     assert rel(out, c0 + a.t() @ b) < 1e-5
 
 
+def _wgrad_variant(v, fn):
+    from hv_amd.runtime import HVOptions, set_train_state
+    set_train_state(HVOptions(wgrad_variant=v))
+    try:
+        return fn()
+    finally:
+        set_train_state()
+
+
+@pytest.mark.parametrize("kind", ["dense", "conv_stem"])
+def test_wgrad_many_splits_and_variants(gpu_device, kind):
+    """Small outputs over many pixels (one or two tiles): the plan splits the pixels up to 256 ways
+    and sums the partials with the many-split reduction; HV_WV_K64 (64-row LDS stages) is bitwise
+    the default; HV_WV_CAP64 (the round-4 plan, <= 64 splits) agrees within fp32 rounding."""
+    T = OT()
+    g = torch.Generator().manual_seed(11)
+    if kind == "dense":
+        a = torch.randn(200003, 128, generator=g).to(torch.bfloat16)
+        b = torch.randn(200003, 64, generator=g).to(torch.bfloat16)
+        ad, bd = a.to(gpu_device), b.to(gpu_device)
+        run = lambda: T.wgrad(ad, bd)                                  # noqa: E731
+        ref = a.float().t() @ b.float()
+    else:                                              # the stem conv: Cin = 3, scalar im2col
+        x = torch.randn(2, 3, 320, 320, generator=g).to(torch.bfloat16).float()
+        dy = torch.randn(2, 32, 160, 160, generator=g).to(torch.bfloat16).float()
+        ref = torch.nn.grad.conv2d_weight(x, (32, 3, 3, 3), dy, 2, 1)
+        xd = x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu_device)
+        dyd = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu_device)
+        run = lambda: T.conv_grad_reorder(T.conv_wgrad(dyd, xd, 3, 2, 1), 32, 3, 3)   # noqa: E731
+    out = {v: _wgrad_variant(v, run).clone() for v in (0, 1, 2)}
+    assert torch.equal(out[0], out[1])
+    for v in (0, 2):
+        assert rel(out[v], ref) < 1e-5
+    assert torch.equal(out[0], _wgrad_variant(0, run))                 # deterministic
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("cin,cout,k,s,hw", [(32, 64, 3, 1, 16), (64, 128, 3, 2, 16), (64, 32, 1, 1, 12),
                                              (3, 32, 3, 2, 32), (256, 256, 3, 1, 10), (128, 64, 3, 2, 15)])

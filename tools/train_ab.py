@@ -2,7 +2,9 @@
 bf16, HVTrainer graph replay): model attributes toggled per arm, separate trainers and models,
 arms interleaved.  usage: python tools/train_ab.py <attr> [batch] [steps]
   attr: a model attribute switched False (arm A) / True (arm B), e.g. hv_train_group_prep, or
-        TF.<name>: a hv_amd.train_fn module switch (e.g. TF.EPILOGUE_COLSUM)"""
+        TF.<name>: a hv_amd.train_fn module switch (e.g. TF.EPILOGUE_COLSUM), or
+        GV.<bits>: arm B runs with HVOptions.gemm_variant = bits (e.g. GV.0x80, 128x128 training tiles)
+        WV.<bits>: arm B runs with HVOptions.wgrad_variant = bits (HV_WV_*)"""
 import os
 import sys
 import time
@@ -27,6 +29,12 @@ for val in (False, True):
     if attr.startswith("TF."):            # a hv_amd.train_fn module switch, set around each arm's steps
         import hv_amd.train_fn as TF
         setattr(TF, attr[3:], val)
+    elif attr.startswith("GV."):
+        if val:
+            m.set_options(gemm_variant=int(attr[3:], 0))
+    elif attr.startswith("WV."):
+        if val:
+            m.set_options(wgrad_variant=int(attr[3:], 0))
     else:
         setattr(m, attr, val)
     arms[val] = HVTrainer(m, monitor_every=0, graph=True)
