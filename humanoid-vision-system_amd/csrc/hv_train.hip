@@ -328,11 +328,25 @@ __global__ void __launch_bounds__(256) k_colred_final(const float* part, int nbl
   }
 }
 
+// block cap of the partial pass: 1,024 (4 per CU: enough rows in flight for the BN / LN backward
+// reductions over 409,600 pixels; 512 -> 1024 measured 127.8-128.2 -> 126.7 ms per training step,
+// 2,048 no further gain, profiles/r05/colred_cap_ab.txt).  HV_COLRED_CAP (64..4096, read once per
+// process) overrides it for A/Bs.
+inline long colred_cap() {
+  static const long c = [] {
+    const char* e = getenv("HV_COLRED_CAP");
+    const long v = e ? atol(e) : 1024;
+    return v < 64 ? 64L : (v > 4096 ? 4096L : v);
+  }();
+  return c;
+}
+
 inline int colred_blocks(long rows, int cols, int imgs) {
   const int cpr = cols / 4;
   const int rpi = cpr <= 256 ? 256 / cpr : 1;
   long b = (rows + (long)rpi * 8 - 1) / ((long)rpi * 8);
-  const long cap = imgs > 1 ? (512 / imgs > 8 ? 512 / imgs : 8) : 512;
+  const long cm = colred_cap();
+  const long cap = imgs > 1 ? (cm / imgs > 8 ? cm / imgs : 8) : cm;
   b = b > cap ? cap : (b < 1 ? 1 : b);
   return (int)b;
 }
