@@ -22,6 +22,10 @@
 // read by out-of-image taps; one copy per translation unit (each TU is its own code object)
 static __device__ __attribute__((aligned(64))) uint4 hv_glds_zero_line[4];
 
+// A/B knob (hv_gemm_desc.variant): dense GEMMs with K % 64 != 0 back on the register-staged
+// kernel (the round-4 routing)
+#define HV_GV_NO_DENSE_KTAIL 0x200000
+
 namespace {
 
 constexpr int ROW = 128;                    // bytes per LDS row (64 bf16)
@@ -115,7 +119,7 @@ __global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm
   }
   const int tm = bid / tilesN, tn = bid % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
-  HV_DCHECK(tm < tilesM && (CONV || d.K % 64 == 0) && (d.A2 == nullptr || d.k1 % 64 == 0));
+  HV_DCHECK(tm < tilesM && (CONV || d.K % 64 == 0 || (d.A2 == nullptr && d.K % 8 == 0)) && (d.A2 == nullptr || d.k1 % 64 == 0));
 
   // ---- per-lane source rows: wave instruction i covers tile rows 8*(wid*AI+i) .. +7
   const int lrow = lane >> 3;               // row within the 8-row group
@@ -197,7 +201,8 @@ __global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm
           const int row = min(m0 + (wid * AI + i) * 8 + lrow, d.M - 1);
           src = (const unsigned short*)d.A2 + (long)row * d.lda2 + (k - d.k1);
         } else {
-          src = arow[i] + k;
+          // dense K % 64 != 0 (K % 8 == 0, no A2): the last K-tile's tail reads the zero line
+          src = k < d.K ? (const void*)(arow[i] + k) : (const void*)hv_glds_zero_line;
         }
       }
       glds16_asm(src, la + i * 1024);
@@ -205,7 +210,7 @@ __global__ void __launch_bounds__(256, (GldsOcc<BM, BN, NS, TRAIN>::value)) gemm
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const void* src = brow[i] + k;
-      if constexpr (CONV) src = k < d.K ? src : (const void*)hv_glds_zero_line;   // K tail of the padded conv
+      src = k < d.K ? src : (const void*)hv_glds_zero_line;   // K tail (padded conv, or dense K % 64 != 0)
       glds16_asm(src, lb + i * 1024);
     }
   };

@@ -28,14 +28,20 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   // K % 64 != 0 only for convolutions (channels a multiple of 8): the last K-tile's tail reads the
   // zero line for both operands (e.g. 3x3 convs with 32 input channels, K = 288)
   if (d.dtype != HV_BF16 || d.conv_transposed) return HV_EUNSUPPORTED;
-  if (d.K % 64 && !((d.variant & HV_GV_CONV_KTAIL) && d.conv_k > 0 && d.K % 8 == 0)) return HV_EUNSUPPORTED;
+  // dense K % 8 == 0 tails as well (e.g. the stem-stage mHC GEMMs, K = 32, M = 1.6 M rows: ~1 ms
+  // each on the register-staged kernel); not with an LN prologue (the zero tail would normalise to
+  // non-zero) or a second A operand
+  const bool dense_tail = d.conv_k == 0 && !d.A2 && !d.a_mean && d.K % 8 == 0 &&
+                          !(d.variant & HV_GV_NO_DENSE_KTAIL);
+  if (d.K % 64 && !((d.variant & HV_GV_CONV_KTAIL) && d.conv_k > 0 && d.K % 8 == 0) && !dense_tail)
+    return HV_EUNSUPPORTED;
   if (d.a_mean && (!d.b_colsum || d.A2 || d.conv_k > 0)) return HV_EUNSUPPORTED;
   if (d.conv_k > 0 ? (d.conv_c % 8) : (d.lda % 8)) return HV_EUNSUPPORTED;
   if (d.A2 && (d.k1 % 64 || d.lda2 % 8)) return HV_EUNSUPPORTED;
   if (d.ldb % 8) return HV_EUNSUPPORTED;
   if (d.splitk > 1) {
     // caller-requested split-K (small output grids, long K): inference epilogues only
-    if (d.conv_k > 0 && d.K % 64) return HV_EUNSUPPORTED;
+    if (d.K % 64) return HV_EUNSUPPORTED;
     if (d.epi_mode || !d.splitk_work || !d.splitk_count || d.splitk > 64 ||
         (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64) > HV_SPLITK_MAX_TILES)
       return HV_EINVAL;
