@@ -171,11 +171,12 @@ def pmc_child(a):
     torch.cuda.synchronize()
 
 
-def cpu_baseline(model_cpu_sd, size, threads, batch=4, iters=3):
+def cpu_baseline(model_cpu_sd, size, threads, batch=16, iters=3):
     """Oracle (CPU restatement of the reference path) on the host cores: a bounded sample of the
-    SAME workload as the GPU line (640x640 fp32 forward, same weights) -- `iters` timed batches of
-    `batch` images after a 1-image warmup (>= 3 timed iterations after a warmup),
-    the median batch giving the rate; about 15-20 s of CPU work on 16 cores."""
+    SAME workload as the GPU line (640x640 fp32 forward, same weights, the GPU line's batch) --
+    `iters` timed batches of `batch` images after a 1-image warmup (>= 3 timed
+    iterations after a warmup), the median batch giving the rate; about 60 s of CPU work on 16
+    cores at batch 16."""
     from oracle import hv_oracle as O
     torch.set_num_threads(threads)
     x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(1))
@@ -466,7 +467,8 @@ def main():
     value = imgs / elapsed
     ms_step = elapsed / a.steps * 1e3
     if rank == 0:
-        base = cpu_baseline(cpu_sd, a.size, a.cpu_threads or host_threads()) if cpu_sd is not None else None
+        base = cpu_baseline(cpu_sd, a.size, a.cpu_threads or host_threads(), batch=a.batch) \
+            if cpu_sd is not None else None
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),

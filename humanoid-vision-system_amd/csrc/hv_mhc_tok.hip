@@ -445,7 +445,7 @@ struct CfgS {
 
 struct TokSplitArgs {
   TokSite s[kTokMaxSites];
-  int T, tiles, fence;
+  int T, tiles;
   float* work;       // [sites][tiles][NSPL][16][D] fp32 partial y
   int* count;        // [sites][tiles] arrival counters, zero before the launch (left zero)
 };
@@ -684,38 +684,28 @@ __global__ void __launch_bounds__(512, 1) mhc_toks_kernel(TokSplitArgs args) {
   });
 
   // ---- partial y -> workspace; the last part of the tile to arrive reduces (fixed part order).
-  // Default hand-off (cdna_hip_programming.md Guideline 16): every wave drains its stores, lane 0
+  // Hand-off (cdna_hip_programming.md Guideline 16): every wave drains its stores, lane 0
   // releases at agent scope and adds to the tile's counter, the last adder acquires, then plain
-  // loads.  HV_MV_TOKSPLIT_SC1 (args.fence == 0): write-through (16-B `sc1`) partial stores, sc1
-  // loads, no fences -- MI355X_MICROARCH.md's visibility table row 1 (one workgroup per CU, one
-  // signalling lane, one unsharded counter, the last adder consumes; measured, not an
-  // architectural guarantee).  The two measured equal in-model (profiles/r05/mhc_toksplit_ab.txt).
+  // loads.  (Round 5's fence-free write-through variant measured equal and was removed: it relied
+  // on measured, not architectural, visibility.)
   const long tbase = ((long)sy * args.tiles + tile) * NSPL;
   float* const wsp = args.work + (tbase + part) * 16 * D;
-  const bool fence = args.fence != 0;
 #pragma unroll
-  for (int j = 0; j < C::J3; ++j) {
-    float* const p = wsp + fr * D + w * C::N3W + 16 * j + 4 * fg;
-    if (fence) *reinterpret_cast<f32x4*>(p) = acc[j];
-    else asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(acc[j]) : "memory");
-  }
+  for (int j = 0; j < C::J3; ++j)
+    *reinterpret_cast<f32x4*>(wsp + fr * D + w * C::N3W + 16 * j + 4 * fg) = acc[j];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* const flag = reinterpret_cast<int*>(smem + C::FLAG);
   if (tid == 0) {
-    if (fence) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int* const cnt = args.count + (long)sy * args.tiles + tile;
     const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == NSPL - 1;
     if (last) {
       __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next launch
-      if (fence) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     *flag = last;
   }
@@ -732,17 +722,8 @@ __global__ void __launch_bounds__(512, 1) mhc_toks_kernel(TokSplitArgs args) {
     const long tok = t0 + lt;
     const float* src = args.work + tbase * 16 * D + lt * D + lane * CPL;
     f32x4 yq[NSPL];
-    if (fence) {
 #pragma unroll
-      for (int q = 0; q < NSPL; ++q) yq[q] = *reinterpret_cast<const f32x4*>(src + (long)q * 16 * D);
-    } else {
-      // every load of the handed-off bytes is an sc1 load (no stale L1 line can be returned)
-#pragma unroll
-      for (int q = 0; q < NSPL; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          yq[q][e] = __hip_atomic_load(src + (long)q * 16 * D + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int q = 0; q < NSPL; ++q) yq[q] = *reinterpret_cast<const f32x4*>(src + (long)q * 16 * D);
     f32x4 yv = yq[0];
 #pragma unroll
     for (int q = 1; q < NSPL; ++q) yv += yq[q];
@@ -829,7 +810,6 @@ int hv_mhc_tok_launch(const hv_mhc_fused_args* a, int n, hipStream_t s) {
     for (int i = 0; i < n; ++i) sa.s[i] = ta.s[i];
     sa.T = ta.T;
     sa.tiles = hv_cdiv(ta.T, 16);
-    sa.fence = (a[0].variant & HV_MV_TOKSPLIT_SC1) == 0;
     sa.work = a[0].split_work;
     sa.count = a[0].split_count;
     if (Hd == 1024) return spl == 4 ? launch_toks<256, 1024, 4, 2>(sa, n, s) : launch_toks<256, 1024, 2, 2>(sa, n, s);

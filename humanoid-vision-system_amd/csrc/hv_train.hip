@@ -934,10 +934,14 @@ __global__ void __launch_bounds__(256) k_grad_norm_final(int nblk, const float* 
 
 __global__ void __launch_bounds__(256) k_adamw(const hv_param_entry* tab, int count, const float* coefs, float lr,
                                                float b1, float b2, float eps, float wd, float bc1, float bc2s,
-                                               const int* __restrict__ steps, const int* __restrict__ active) {
+                                               const int* __restrict__ steps, const int* __restrict__ active,
+                                               const float* __restrict__ hyper) {
   const int ei = find_param(tab, count, blockIdx.x);
   const hv_param_entry e = tab[ei];
   if (!e.grad || (active && !active[ei])) return;     // no gradient this step: no decay, no update
+  if (hyper) {                                  // device hyper-parameters (a scheduler's lr per step)
+    lr = hyper[0]; b1 = hyper[1]; b2 = hyper[2]; eps = hyper[3]; wd = hyper[4];
+  }
   if (steps) {                                  // per-parameter bias correction (torch state['step'])
     const float t = (float)max(steps[ei], 1);
     bc1 = 1.f - powf(b1, t);
@@ -1340,7 +1344,16 @@ extern "C" int hv_adamw(const hv_param_entry* tab, int count, int total_blocks, 
   const float bc1 = 1.f - powf(beta1, (float)max(step, 1));
   const float bc2s = sqrtf(1.f - powf(beta2, (float)max(step, 1)));
   k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, lr, beta1, beta2, eps, weight_decay, bc1,
-                                                         bc2s, steps, active);
+                                                         bc2s, steps, active, nullptr);
+  HV_CHECK_LAUNCH();
+  return HV_OK;
+}
+
+extern "C" int hv_adamw_dev(const hv_param_entry* tab, int count, int total_blocks, const float* coefs,
+                            const float* hyper, const int* steps, const int* active, hv_stream_t stream) {
+  if (!tab || count <= 0 || total_blocks <= 0 || !hyper || !steps) return HV_EINVAL;
+  k_adamw<<<total_blocks, 256, 0, (hipStream_t)stream>>>(tab, count, coefs, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f, 1.f, steps,
+                                                         active, hyper);
   HV_CHECK_LAUNCH();
   return HV_OK;
 }

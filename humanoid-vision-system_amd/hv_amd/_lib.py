@@ -26,10 +26,10 @@ MV_THREE_GROUPS, MV_ONE_GROUP8, MV_PERWAVE128, MV_PERWAVE64, MV_WIDE, MV_ABLATE_
 MV_SPLIT256, MV_SPLITW = 0x200, 12
 MV_NOMERGE, MV_PIPE, MV_PIPE_NOMERGE, MV_PERWAVE = 7, 8, 9, 10
 MV_TOK, MV_TOK16 = 0x400, 0x800
-MV_TOKSPLIT2, MV_TOKSPLIT4, MV_TOKSPLIT_SC1 = 0x1000, 0x2000, 0x4000
+MV_TOKSPLIT2, MV_TOKSPLIT4 = 0x1000, 0x2000
 ACT = {"none": 0, "relu": 1, "silu": 2, "gelu": 3, "leaky": 4, "sigmoid": 5}
 
-ABI_VERSION = 3          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
+ABI_VERSION = 4          # include/hv_kernels.h HV_ABI_VERSION this binding is written against
 _LIB = None
 _LOCK = threading.Lock()
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -198,12 +198,14 @@ _SIGS = {
     "hv_write_bytes": ([vp, vp, C.c_longlong, vp], i32),
     "hv_attention_general": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp], i32),
     "hv_yolo_decode": ([i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
-    "hv_nms_work_bytes": ([i32, i32, i32], C.c_size_t),
+    "hv_nms_work_bytes": ([i32, i32, i32, C.c_long], C.c_size_t),
     "hv_preprocess": ([vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp], i32),
     "hv_pil_table_ints": ([i32, i32, i32, i32], C.c_size_t),
     "hv_pil_resample_tables": ([i32, i32, i32, i32, vp], i32),
     "hv_preprocess_pil": ([vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, vp], i32),
-    "hv_nms": ([vp, i32, i32, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
+    "hv_nms": ([vp, i32, i32, f32, f32, i32, C.c_long, vp, vp, vp, vp, vp, vp], i32),
+    "hv_sort_desc_exact_work_bytes": ([i32], C.c_size_t),
+    "hv_sort_desc_exact": ([vp, i32, i32, vp, vp, vp], i32),
     # ---- training step
     "hv_wgrad_work_floats": ([i32, i32, i32, i32], C.c_size_t),
     "hv_wgrad": ([vp, vp], i32),
@@ -249,6 +251,7 @@ _SIGS = {
     "hv_param_blocks": ([i64], i32),
     "hv_grad_norms": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, vp], i32),
     "hv_adamw": ([vp, i32, i32, vp, f32, f32, f32, f32, f32, i32, vp, vp, vp], i32),
+    "hv_adamw_dev": ([vp, i32, i32, vp, vp, vp, vp, vp], i32),
 }
 
 EXPORTED = tuple(_SIGS)

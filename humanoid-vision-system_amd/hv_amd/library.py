@@ -116,7 +116,7 @@ def _mhc_train_graph(sk_iters):
 
     def fn(x, H_pre_raw, H_post_raw, H_res_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post):
         g = ops.SinkhornGroup([H_res_raw.detach().float().contiguous()], [sk_iters], x.device)
-        (h_res,) = SinkhornGroupFn.apply(g, H_res_raw)
+        (h_res,) = SinkhornGroupFn.apply(g, None, H_res_raw)
         m = _mhc_namespace(H_pre_raw, H_post_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post)
         return MhcFn.apply(x, h_res, H_pre_raw, H_post_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post, m, (0, 0, 0))
     return fn

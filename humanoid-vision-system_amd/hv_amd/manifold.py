@@ -68,7 +68,7 @@ class SinkhornKnoppProjection(nn.Module):
             from .train_fn import SinkhornGroupFn
             if matrix.dtype != torch.float32 or not matrix.is_contiguous():
                 raise TypeError("SinkhornKnoppProjection: differentiable input must be contiguous fp32")
-            (out,) = SinkhornGroupFn.apply(g, matrix)
+            (out,) = SinkhornGroupFn.apply(g, None, matrix)
         else:
             out = g.run()[0]
             out = out.squeeze(0) if matrix.dim() == 2 else out

@@ -13,6 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib as L
+from . import tables
 from ._lib import check, dtype_code, ptr, stream_ptr
 from .runtime import options
 
@@ -326,17 +327,16 @@ def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
         # kept for tests only: 24.5 vs 25.1 us on the grouped q / k / v at T = 401, and slower
         # than the unsplit kernel at T = 1,604 (26.9 vs 24.0)
         if (D, Hd) == (256, 512) and options().mhc_tok_split and 4 * tiles16 <= TOK_CUS:
-            v |= L.MV_TOKSPLIT4 | (L.MV_TOKSPLIT_SC1 if TOKSPLIT_SC1 else 0)
+            v |= L.MV_TOKSPLIT4
     if (D, Hd) == (256, 1024):
         # (256, 1024) only split (5.9 MB of weights per unsplit workgroup ties the chain): T = 400
         # 32.6 (4-way) vs 57.7 us chain, T = 1,600 48.7 (2-way) vs 62.6 us
         if not (options().mhc_tok_split and v & L.MV_TOK16 and 2 * tiles16 <= TOK_CUS):
             return 0
-        v |= (L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2) | (L.MV_TOKSPLIT_SC1 if TOKSPLIT_SC1 else 0)
+        v |= L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2
     return v
 
 
-TOKSPLIT_SC1 = False      # split token-tile hand-off by write-through stores instead of fences (A/B: equal)
 
 
 _TOKSPLIT_COUNTERS: dict = {}
@@ -539,9 +539,9 @@ class SinkhornGroup:
                 e.raw = p
             for k, i in enumerate(self._large_idx):
                 self.entries_large[k].raw = rp[i]
-            self.table = upload_table(self.entries, self.device)
+            self.table = tables.upload(self.entries, self.device, self, "entries")
             if self.has_large:
-                self.table_large = upload_table(self.entries_large, self.device)
+                self.table_large = tables.upload(self.entries_large, self.device, self, "entries_large")
             self._raw_ptrs = rp
         lib = L.lib()
         mx = max(self.iters)
@@ -926,20 +926,42 @@ class NmsPlan:
             ents[i].boxes, ents[i].class_scores, ents[i].class_indices, ents[i].cells = \
                 bx.data_ptr(), sc.data_ptr(), ci.data_ptr(), cells
             self._keep += [bx, sc, ci]
-        self.table = upload_table(ents, dev)
+        self.table = tables.upload(ents, dev, self, "scales")
         self.n_scales, self.B = len(keys), B
         self.conf, self.iou, self.max_det = float(conf_thr), float(iou_thr), int(max_det)
         self.boxes = torch.empty((B, max_det, 4), device=dev, dtype=torch.float32)
         self.scores = torch.empty((B, max_det), device=dev, dtype=torch.float32)
         self.labels = torch.empty((B, max_det), device=dev, dtype=torch.int64)
         self.count = torch.empty(B, device=dev, dtype=torch.int32)
-        self.work = torch.empty(L.lib().hv_nms_work_bytes(B, len(keys), max_det), device=dev, dtype=torch.uint8)
+        if int(max_det) < 1:
+            raise ValueError("nms: max_det must be >= 1")
+        self.max_cells = max(int(o["class_scores"].numel()) // B for o in decoded.values())
+        nbytes = L.lib().hv_nms_work_bytes(B, len(keys), self.max_det, self.max_cells)
+        if nbytes == 0:
+            raise ValueError(f"nms: unsupported sizes (batch {B}, max_det {max_det}, cells {self.max_cells})")
+        self.work = torch.empty(nbytes, device=dev, dtype=torch.uint8)
 
     def run(self):
         check(L.lib().hv_nms(self.table.data_ptr(), self.n_scales, self.B, self.conf, self.iou, self.max_det,
-                             self.boxes.data_ptr(), self.scores.data_ptr(), self.labels.data_ptr(),
+                             self.max_cells, self.boxes.data_ptr(), self.scores.data_ptr(), self.labels.data_ptr(),
                              self.count.data_ptr(), self.work.data_ptr(), stream_ptr()), "hv_nms")
         return self.boxes, self.scores, self.labels, self.count
+
+
+def sort_desc_exact(vals: torch.Tensor, depth_limit: int = -1) -> torch.Tensor:
+    """torch.sort(vals, descending=True).indices of the reference's CPU sort (libstdc++ introsort,
+    tie order included), on the GPU (hv_sort_desc_exact; the sort hv_nms falls back to on ties).
+    depth_limit >= 0 forces introsort's depth limit (reaches its heap-sort fallback)."""
+    v = vals.detach().float().contiguous().reshape(-1)
+    _cuda(v)
+    n = v.numel()
+    out = torch.empty(n, device=v.device, dtype=torch.int32)
+    if n == 0:
+        return out.long()
+    work = torch.empty(L.lib().hv_sort_desc_exact_work_bytes(n), device=v.device, dtype=torch.uint8)
+    check(L.lib().hv_sort_desc_exact(v.data_ptr(), n, int(depth_limit), out.data_ptr(), work.data_ptr(),
+                                     stream_ptr()), "hv_sort_desc_exact")
+    return out.long()
 
 
 def nms_batched(decoded, conf_thr: float, iou_thr: float, max_det: int):

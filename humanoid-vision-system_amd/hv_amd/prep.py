@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
+from . import tables
 from .ops import SinkhornGroup, check, dtype_code, stream_ptr
 
 
@@ -37,10 +38,6 @@ def _param(t: torch.Tensor, what: str) -> torch.Tensor:
 
 def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
-
-
-def _upload(entries, device) -> torch.Tensor:
-    return torch.frombuffer(bytearray(bytes(entries)), dtype=torch.uint8).to(device)
 
 
 class PrepProgram:
@@ -126,7 +123,7 @@ class PrepProgram:
                 tot[p] += blk[p]
             self.mout.append((fold, a1, c1, wct, w1c, w2c, cs))
         self.mtotals = (L.i32 * 4)(*tot)
-        self.mtable = _upload(self.mentries, device)
+        self.mtable = tables.upload(self.mentries, device, self, "mhc_prep")
         # ---- weight prep (casts of the mHC MLP weights + registered convs / linears)
         self.convs: Dict[int, Tuple] = {}
         self.linears: Dict[int, Tuple] = {}
@@ -205,7 +202,7 @@ class PrepProgram:
             tot += nb
         self.wentries = tab
         self.wtotal = tot
-        self.wtable = _upload(tab, self.device)
+        self.wtable = tables.upload(tab, self.device, self, "wprep")
         self._wdirty = False
 
     # ------------------------------------------------------------------ run

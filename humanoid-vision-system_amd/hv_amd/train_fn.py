@@ -143,9 +143,10 @@ class SinkhornGroupFn(torch.autograd.Function):
     (manifold_layers.py:32-93 and its autograd)."""
 
     @staticmethod
-    def forward(ctx, group, *raws):
+    def forward(ctx, group, token, *raws):
         outs = group.run(list(raws))
         ctx.group = group
+        ctx.token = token                  # train_model._InFlight: the group's buffers are in use
         ctx.set_materialize_grads(False)
         return tuple(o.squeeze(0) if r.dim() == 2 else o for o, r in zip(outs, raws))
 
@@ -153,9 +154,11 @@ class SinkhornGroupFn(torch.autograd.Function):
     def backward(ctx, *douts):
         g = ctx.group
         draws = g.backward(list(douts))
+        if ctx.token is not None:          # the Sinkhorn backward runs after every mHC backward
+            ctx.token.release()
         # a projection no loss depends on gets no gradient at all (None, as the reference's
         # per-module autograd leaves it): the optimizer then skips that H_res_raw
-        return (None,) + tuple(d if o is not None else None for d, o in zip(draws, douts))
+        return (None, None) + tuple(d if o is not None else None for d, o in zip(draws, douts))
 
 
 # =============================================================================== mHC

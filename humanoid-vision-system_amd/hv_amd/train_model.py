@@ -29,30 +29,55 @@ class HTable(dict):
     coefs: Dict[int, Any] = {}
 
 
+class _InFlight:
+    """Marks one cached (Sinkhorn group, coefficient prep) set as used by a forward whose backward
+    has not run yet: a second training forward before that backward (`model(x1) + model(x2)`,
+    checkpoint-style recomputation) must not overwrite the buffers the first one's backward
+    reads, so it takes another set.  Released by SinkhornGroupFn.backward, or when the forward's
+    autograd graph is dropped without a backward (the token lives in its ctx)."""
+
+    def __init__(self, entry: Dict):
+        self.entry = entry
+        entry["busy"] += 1
+
+    def release(self) -> None:
+        if self.entry is not None:
+            self.entry["busy"] -= 1
+            self.entry = None
+
+    def __del__(self):
+        self.release()
+
+
 def _hres_table(model) -> HTable:
     """Grouped differentiable Sinkhorn of all 76 sites + (model.hv_train_group_prep, default on)
     the grouped training coefficient prep of train_prep.TrainPrep over its outputs.  The Sinkhorn
     group and the prep program are cached on the model while the parameter storage is unchanged,
-    so their buffers (and a captured training graph's pointers) stay put."""
+    so their buffers (and a captured training graph's pointers) stay put.  The cache is a small
+    pool: a forward whose set is still waiting for its backward leaves it alone (_InFlight)."""
     from .train_prep import TrainPrep
     mods = model._mhc_modules
     raws = [m.H_res_raw for m in mods]
     dt = PRECISIONS[model.hv_precision]
     cache = model.__dict__.setdefault("_train_prep_cache", {})
     key = (tuple(r.data_ptr() for r in raws), tuple(m.sinkhorn.convergence_history.data_ptr() for m in mods))
-    group = cache.get("sk") if cache.get("sk_key") == key else None
-    if group is None:
+    pool = [e for e in cache.get("pool", []) if e["key"] == key]
+    cache["pool"] = pool
+    entry = next((e for e in pool if e["busy"] == 0), None)
+    if entry is None:
         group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
                                   raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
                                   hists=[m.sinkhorn.convergence_history for m in mods])
-        cache["sk"], cache["sk_key"], cache["prep"] = group, key, None
-    outs = TF.SinkhornGroupFn.apply(group, *raws)
+        entry = {"key": key, "sk": group, "prep": None, "busy": 0}
+        pool.append(entry)
+    token = _InFlight(entry) if torch.is_grad_enabled() else None
+    outs = TF.SinkhornGroupFn.apply(entry["sk"], token, *raws)
     H = HTable({id(m): h for m, h in zip(mods, outs)})
     H.coefs = {}
     if getattr(model, "hv_train_group_prep", True):
-        prep = cache.get("prep")
+        prep = entry["prep"]
         if prep is None or not prep.valid_for(mods, outs, dt):
-            prep = cache["prep"] = TrainPrep(mods, [o.detach() for o in outs], dt)
+            prep = entry["prep"] = TrainPrep(mods, [o.detach() for o in outs], dt)
         H.coefs = prep.run()
     return H
 
@@ -73,7 +98,7 @@ def module_H(module) -> Dict[int, torch.Tensor]:
     group = ops.SinkhornGroup([r.detach() for r in raws], [m.sinkhorn.num_iterations for m in mods],
                               raws[0].device, mods[0].sinkhorn.epsilon, mods[0].sinkhorn.tau,
                               hists=[m.sinkhorn.convergence_history for m in mods])
-    outs = TF.SinkhornGroupFn.apply(group, *raws)
+    outs = TF.SinkhornGroupFn.apply(group, None, *raws)
     return {id(m): h for m, h in zip(mods, outs)}
 
 

@@ -20,7 +20,8 @@ from typing import Dict, List
 import torch
 
 from . import _lib as L
-from .ops import check, dtype_code, stream_ptr, upload_table
+from . import tables
+from .ops import check, dtype_code, stream_ptr
 
 
 @dataclass
@@ -47,6 +48,7 @@ class TrainPrep:
         dev = h_res[0].device
         pdt = torch.bfloat16 if dtype == torch.bfloat16 else torch.float32
         self.h_ptrs = tuple(h.data_ptr() for h in h_res)
+        self.h_res = list(h_res)               # the Sinkhorn outputs the prep table reads
         self.param_ptrs = self._param_key()
         n = len(self.mods)
         offs, total = [], 0
@@ -90,7 +92,7 @@ class TrainPrep:
             if dtype != torch.float32:
                 trans.append((W2, co.w2, 0))
         self.mtotals = (L.i32 * 4)(*tot)
-        self.mtable = upload_table(self.mentries, dev)
+        self.mtable = tables.upload(self.mentries, dev, self, "mhc_prep")
         self.tentries = (L.TransposeEntry * len(trans))()
         tb = 0
         for j, (x, y, tr) in enumerate(trans):
@@ -100,7 +102,7 @@ class TrainPrep:
             t.x_dtype, t.y_dtype, t.transpose, t.blk = dtype_code(x.dtype), dtype_code(y.dtype), tr, tb
             tb += lib.hv_transpose_blocks(rows, cols)
         self.ttotal = tb
-        self.ttable = upload_table(self.tentries, dev)
+        self.ttable = tables.upload(self.tentries, dev, self, "transpose")
         self.gen = 0
 
     def _param_key(self):

@@ -309,6 +309,40 @@ class FusedAdamW:
         self._table = None
         self._key = None
         self.device = dev
+        # lr, beta1, beta2, eps, weight_decay as a DEVICE array read by hv_adamw_dev: a scheduler
+        # changing lr every step (mhc_trainer.py:275) updates it by a small async copy, so a
+        # captured training graph keeps replaying instead of re-capturing per value
+        self._hyper = torch.zeros(5, device=dev, dtype=torch.float32)
+        self._hyper_vals = None
+        self._hyper_ring = []               # (pinned host [5], event) staging slots
+        self._hyper_slot = 0
+
+    def hyper_values(self):
+        return (float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd))
+
+    def sync_hyper(self) -> None:
+        """Upload the hyper-parameters when they changed since the last upload, asynchronously on
+        the current stream (never inside a graph capture: the replay reads the device array)."""
+        vals = self.hyper_values()
+        if vals == self._hyper_vals:
+            return
+        if self._hyper.device.type != "cuda":
+            self._hyper.copy_(torch.tensor(vals, dtype=torch.float32))
+        else:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdamW.sync_hyper inside a graph capture")
+            if not self._hyper_ring:
+                self._hyper_ring = [(torch.empty(5, dtype=torch.float32).pin_memory(), None) for _ in range(4)]
+            pin, ev = self._hyper_ring[self._hyper_slot]
+            if ev is not None:
+                ev.synchronize()            # that slot's previous copy has left the staging buffer
+            pin.copy_(torch.tensor(vals, dtype=torch.float32))
+            self._hyper.copy_(pin, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._hyper_ring[self._hyper_slot] = (pin, ev)
+            self._hyper_slot = (self._hyper_slot + 1) % len(self._hyper_ring)
+        self._hyper_vals = vals
 
     @property
     def param_steps(self) -> List[int]:
@@ -334,8 +368,8 @@ class FusedAdamW:
             e.blk = blk
             blk += lib.hv_param_blocks(p.numel())
         self._blocks = blk
-        from .ops import upload_table
-        self._table = upload_table(ents, self.device)
+        from . import tables
+        self._table = tables.upload(ents, self.device, self, "params")
         self._work = torch.empty(2 * blk, device=self.device, dtype=torch.float32)
 
     def _active_tensor(self, active) -> Tensor:
@@ -370,10 +404,10 @@ class FusedAdamW:
                                     self.norms.data_ptr(), self.coefs.data_ptr(), self._work.data_ptr(),
                                     act.data_ptr(), stream_ptr()), "hv_grad_norms")
             coefs = self.coefs.data_ptr()
-        b1, b2 = self.betas
-        check(lib.hv_adamw(self._table.data_ptr(), len(self.named), self._blocks, coefs, self.lr, b1, b2, self.eps,
-                           self.wd, self.step_count, self._steps_dev.data_ptr(), act.data_ptr(), stream_ptr()),
-              "hv_adamw")
+        if not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self.sync_hyper()
+        check(lib.hv_adamw_dev(self._table.data_ptr(), len(self.named), self._blocks, coefs, self._hyper.data_ptr(),
+                               self._steps_dev.data_ptr(), act.data_ptr(), stream_ptr()), "hv_adamw_dev")
         # the kernel wrote the parameters behind autograd's back: bump their version counters as
         # an in-place torch update would, so frozen coefficients / captured graphs (VersionWatch)
         # see the new weights (every parameter: the skipped ones are unchanged but a version
@@ -585,15 +619,16 @@ class HVTrainer:
 
     def _graph_key(self, images: Tensor, targets: List[Tensor]):
         """Everything a captured step bakes in: shapes, parameter storage, precision, the kernel
-        variants (the model's HVOptions) and the optimizer hyper-parameters the captured clip +
-        AdamW launches carry by value -- changing opt.lr (a scheduler), loading an optimizer state
-        or model.set_options() re-captures instead of replaying stale values."""
+        variants (the model's HVOptions) and the clip norms the captured hv_grad_norms launch
+        carries by value -- model.set_options() or new clip norms re-capture instead of replaying
+        stale values.  lr / betas / eps / weight decay are NOT in it: AdamW reads them from the
+        optimizer's device array, refreshed before every replay (FusedAdamW.sync_hyper), so a
+        per-step scheduler keeps replaying the one captured graph."""
         from .runtime import module_options
         o = self.opt
         return (tuple(images.shape), images.dtype, tuple(tuple(t.shape) for t in targets),
                 tuple(p.data_ptr() for p in self.grads.params), self.model.hv_precision
                 if hasattr(self.model, "hv_precision") else None, module_options(self.model),
-                float(o.lr), float(o.wd), tuple(float(b) for b in o.betas), float(o.eps),
                 tuple(float(m) for m in o.max_norms))
 
     def _capture(self, images: Tensor, targets: List[Tensor], key) -> None:
@@ -648,6 +683,7 @@ class HVTrainer:
         if self._g is None or self._g["key"] != key:
             self._capture(images, targets, key)
         g = self._g
+        self.opt.sync_hyper()                      # this step's lr etc. into the array AdamW reads
         g["x"].copy_(images)
         for dst, src in zip(g["t"], targets):
             dst.copy_(src)

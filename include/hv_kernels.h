@@ -36,8 +36,9 @@ enum { HV_OK = 0, HV_EINVAL = -1, HV_EUNSUPPORTED = -2 };
  * entry points and hv_gemm_desc a device `seed_offset`, hv_mhc_fused_supported gained `variant`,
  * hv_mhc_fused_args grew by 8 bytes and the hv_gemm_set_* / hv_mhc_fused_set_* setters were
  * removed; 3 since hv_gemm_desc gained `colsum_part` and hv_mhc_fused_args `split_work` /
- * `split_count` (appended).  Bindings compare it with the version they were written against. */
-#define HV_ABI_VERSION 3
+ * `split_count` (appended); 4 since hv_nms / hv_nms_work_bytes take `max_cells` (any candidate count,
+ * any max_det).  Bindings compare it with the version they were written against. */
+#define HV_ABI_VERSION 4
 int hv_abi_version(void);
 /* build provenance: a hash of the sources (the .hip / .h files of csrc, the include headers, the Makefile) the
  * library was compiled from; the Python loader recomputes it and refuses a stale build */
@@ -154,8 +155,11 @@ typedef struct hv_gemm_desc {
      others).  ceil(M / 128) * 2 blocks must be allocated; hv_colsum_final reduces the first
      ceil(M / 64).  The bias gradient of the layer whose activation backward this launch fuses,
      without a second pass over C (replaces hv_colsum on it).  HV_EUNSUPPORTED when the call
-     does not take the LDS-DMA kernel's staged gradient epilogue (bf16, K % 64 == 0, aligned C,
-     no variant forcing another path); nothing is launched then. */
+     does not take the LDS-DMA kernel's staged gradient epilogue; nothing is launched then.  It
+     takes: epi_mode 2, bf16, no split-K, no transposed conv, not the Cin = 32 3x3 conv, C 16-B
+     aligned with ldc % 8 == 0 (the residual likewise), no variant forcing another path, and the
+     operands the LDS-DMA kernel accepts: dense K % 8 == 0 (K-tails of a 64-deep k-tile are
+     zero-filled) or an implicit conv with Cin % 8 == 0. */
   float* colsum_part;
 } hv_gemm_desc;
 
@@ -459,9 +463,13 @@ int hv_yolo_decode(int dtype, const void* logits, int n, int h, int w, int A, in
  * Detection post-processing: YOLODetectionHead.post_process +
  * non_max_suppression (yolo_head.py:571-731) for a whole batch in two launches.
  * Per (image, scale): class_score > conf_thr, greedy NMS (keep IoU < iou_thr, best first,
- * at most max_det, up to 8192 candidates per image and scale); then per image the same NMS
- * over the concatenated per-scale survivors.  Outputs [batch, max_det] (+ count[batch]);
- * rows at and past count[b] are written as zeros.
+ * at most max_det); then per image the same NMS over the concatenated per-scale survivors.
+ * No candidate cap: segments with more than 8192 candidates, and cross-scale passes with more
+ * than 8192 survivors, sort in the workspace (hv_nms_work_bytes sizes it from max_cells, which
+ * must be >= every scale's `cells`).  Outputs [batch, max_det] (+ count[batch]); rows at and past
+ * count[b] are written as zeros.  Bit-exact with the reference for any input; max_det >= 1
+ * (the reference keeps one box at max_detections = 0; that case is refused here).
+ * hv_nms_work_bytes returns 0 for arguments hv_nms refuses.
  * ------------------------------------------------------------------------------------ */
 typedef struct hv_nms_scale {
   const float* boxes;          /* [batch, cells, 4] xyxy (decoder output [B, A, H, W, 4]) */
@@ -469,10 +477,16 @@ typedef struct hv_nms_scale {
   const int64_t* class_indices;/* [batch, cells] */
   long cells;                  /* A * H * W */
 } hv_nms_scale;
-size_t hv_nms_work_bytes(int batch, int nscales, int max_det);
+size_t hv_nms_work_bytes(int batch, int nscales, int max_det, long max_cells);
 int hv_nms(const hv_nms_scale* dev_scales, int nscales, int batch, float conf_thr, float iou_thr,
-           int max_det, float* boxes, float* scores, int64_t* labels, int* count, void* work,
-           hv_stream_t stream);
+           int max_det, long max_cells, float* boxes, float* scores, int64_t* labels, int* count,
+           void* work, hv_stream_t stream);
+/* The sort inside it, on its own: out_idx = torch.sort(vals, descending=True).indices of the CPU
+ * reference (libstdc++ introsort over (value, index) pairs, NOT stable on ties), exactly, for
+ * vals[n] without NaNs.  depth_limit < 0: std::sort's own 2*floor(log2 n); >= 0 forces it (the
+ * heap-sort fallback).  One workgroup; work: hv_sort_desc_exact_work_bytes(n) bytes. */
+size_t hv_sort_desc_exact_work_bytes(int n);
+int hv_sort_desc_exact(const float* vals, int n, int depth_limit, int* out_idx, void* work, hv_stream_t stream);
 
 
 /* ------------------------------------------------------------------------------------
@@ -698,6 +712,11 @@ int hv_grad_norms(const hv_param_entry* dev_table, int count, int total_blocks, 
 int hv_adamw(const hv_param_entry* dev_table, int count, int total_blocks, const float* coefs,
              float lr, float beta1, float beta2, float eps, float weight_decay, int step,
              const int* steps, const int* active /* as hv_grad_norms */, hv_stream_t stream);
+/* the same step with the hyper-parameters read from DEVICE memory, hyper = {lr, beta1, beta2,
+   eps, weight_decay} (fp32): a captured graph replays with whatever the host last wrote there,
+   so a learning-rate scheduler does not force a re-capture.  Per-parameter `steps` required. */
+int hv_adamw_dev(const hv_param_entry* dev_table, int count, int total_blocks, const float* coefs,
+                 const float* hyper, const int* steps, const int* active, hv_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Stability monitor (ManifoldHyperConnection._monitor_stability, reference

@@ -80,23 +80,41 @@ def model_input(B: int, S: int) -> torch.Tensor:
     return torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(1))
 
 
-def nms_case(seed: int, B: int = 2, grids=((8, 8), (4, 4), (2, 2)), A: int = 3, frac_above: float = 0.3):
+def nms_case(seed: int, B: int = 2, grids=((8, 8), (4, 4), (2, 2)), A: int = 3, frac_above: float = 0.3,
+             spread: bool = False):
     """Random decoded outputs for the post-processing fixture: clustered xyxy boxes (so NMS
     suppresses), class scores u^(1/(1-frac_above)) for u ~ U(0,1) (larger frac_above -> fewer
-    scores above 0.5), random labels."""
+    scores above 0.5), random labels.  spread=True: small boxes at uniform centres instead, so
+    most candidates survive NMS (cases with thousands of kept boxes)."""
     g = gen_seed(seed, B, 77)
     out = {}
     for s, (h, w) in enumerate(grids):
         n = A * h * w
-        ctr = torch.rand(B, 4, 2, generator=g)                      # 4 clusters per image
-        pick = torch.randint(0, 4, (B, n), generator=g)
-        c = torch.gather(ctr, 1, pick.unsqueeze(-1).expand(B, n, 2)) + 0.03 * torch.randn(B, n, 2, generator=g)
-        wh = 0.05 + 0.2 * torch.rand(B, n, 2, generator=g)
-        boxes = torch.cat([c - wh / 2, c + wh / 2], -1).view(B, A, h, w, 4)
+        if spread:
+            c = torch.rand(B, n, 2, generator=g)
+            wh = 0.004 + 0.012 * torch.rand(B, n, 2, generator=g)
+        else:
+            ctr = torch.rand(B, 4, 2, generator=g)                  # 4 clusters per image
+            pick = torch.randint(0, 4, (B, n), generator=g)
+            c = torch.gather(ctr, 1, pick.unsqueeze(-1).expand(B, n, 2)) + 0.03 * torch.randn(B, n, 2, generator=g)
+            wh = 0.05 + 0.2 * torch.rand(B, n, 2, generator=g)
+        boxes = torch.cat([c - wh / 2, c + wh / 2], -1).reshape(B, A, h, w, 4)
         sc = torch.rand(B, A, h, w, generator=g) ** (1.0 / max(1e-3, 1 - frac_above))
         lab = torch.randint(0, 80, (B, A, h, w), generator=g)
         out[f"scale_{s}"] = {"boxes": boxes.float(), "class_scores": sc.float(), "class_indices": lab}
     return out
+
+
+# post_process past the LDS candidate capacity (8,192 per image and scale) and past max_det 1024:
+# (tag, seed, B, grids, conf, iou, max_det, spread).  640^2 / 1024^2 detection grids at an
+# evaluation-style threshold (verdict r5 item 1), and spread boxes with thousands kept per scale
+# (the cross-scale pass then also overflows the LDS).
+NMS_LARGE_CASES = [
+    ("640_c01", 21, 2, ((80, 80), (40, 40), (20, 20)), 0.01, 0.5, 100, False),
+    ("1024_c01", 22, 1, ((128, 128), (64, 64), (32, 32)), 0.01, 0.5, 100, False),
+    ("640_spread_md5000", 23, 1, ((80, 80), (40, 40), (20, 20)), 0.05, 0.6, 5000, True),
+    ("1024_spread_md1500", 24, 1, ((128, 128), (64, 64), (32, 32)), 0.2, 0.45, 1500, True),
+]
 
 
 PIL_CASES = [  # (tag, frames, in_h, in_w, out_h, out_w, seed)

@@ -548,6 +548,26 @@ def gen_nms(yh):
         save(f"nms_{seed}", **rec)
 
 
+def gen_nms_large(yh):
+    """post_process at detection-grid sizes past the GPU kernel's LDS capacity and max_det past
+    1024 (oracle/cases.NMS_LARGE_CASES).  Inputs are regenerated from oracle/cases.nms_case."""
+    print("G6b nms large")
+    from oracle.cases import NMS_LARGE_CASES, nms_case
+    torch.manual_seed(0)
+    head = yh.YOLODetectionHead([16, 16, 16], num_classes=80)
+    for tag, seed, B, grids, conf, iou, mx, spread in NMS_LARGE_CASES:
+        dec = nms_case(seed, B=B, grids=grids, spread=spread)
+        ncand = [int((v["class_scores"].reshape(B, -1) > conf).sum(1).max()) for _, v in sorted(dec.items())]
+        res = head.post_process(dec, confidence_threshold=conf, iou_threshold=iou, max_detections=mx)
+        rec = {"conf": conf, "iou": iou, "max_det": mx, "max_candidates": np.array(ncand)}
+        for b, r in enumerate(res):
+            rec[f"boxes{b}"] = r["boxes"].reshape(-1, 4)
+            rec[f"scores{b}"] = r["scores"].reshape(-1)
+            rec[f"labels{b}"] = r["labels"].reshape(-1)
+        print(f"  {tag}: candidates per scale {ncand}, kept {[len(r['scores']) for r in res]}")
+        save(f"nms_large_{tag}", **rec)
+
+
 def gen_preproc():
     """G7: the reference's default preprocessing resize -- torchvision Resize on a PIL image,
     i.e. Pillow Image.resize(BILINEAR) (preprocessing.py:104-131,268-274; Pillow pinned 10.0.0 in
@@ -595,6 +615,8 @@ def main():
         gen_train(hv, [m for m in a.trains.split(",") if m])
     if "nms" in parts:
         gen_nms(yh)
+    if "nms" in parts or "nmslarge" in parts:
+        gen_nms_large(yh)
     if "preproc" in parts:
         gen_preproc()
     if "seeded" in parts:

@@ -431,8 +431,10 @@ def _iou(b1: Tensor, b2: Tensor) -> Tensor:
 
 
 def nms(boxes: Tensor, scores: Tensor, iou_thr: float, max_det: int) -> List[int]:
-    """non_max_suppression (yolo_head.py:678-731): greedy, best first, keep IoU < thr."""
-    order = torch.sort(scores, descending=True, stable=True).indices
+    """non_max_suppression (yolo_head.py:678-731): greedy, best first, keep IoU < thr.  The sort
+    is the reference's own call (yolo_head.py:700): torch.sort's default, NOT stable -- on the CPU
+    libstdc++ introsort, whose tie order oracle/std_sort.py restates."""
+    order = torch.sort(scores, descending=True).indices
     keep: List[int] = []
     while order.numel() > 0:
         i = int(order[0])

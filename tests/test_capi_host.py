@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert set(declared) == set(_lib.EXPORTED), set(declared) ^ set(_lib.EXPORTED)
-    assert lib.hv_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.hv_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_library_built_from_this_tree():

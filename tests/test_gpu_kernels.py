@@ -635,6 +635,69 @@ def test_gpu_post_process_matches_reference_fixture(gpu_device, seed):
         np.testing.assert_array_equal(r["boxes"].reshape(-1, 4).cpu().numpy(), g[f"boxes{b}"])
 
 
+@pytest.mark.parametrize("case", cases.NMS_LARGE_CASES, ids=[c[0] for c in cases.NMS_LARGE_CASES])
+def test_gpu_post_process_large_matches_reference_fixture(gpu_device, case):
+    """§8f-1 past the LDS capacity: > 8,192 candidates per (image, scale) (640^2 / 1024^2 grids at
+    conf 0.01: up to 47,209), max_det 1,500 / 5,000 (cross-scale pass > 8,192 survivors) --
+    boxes, scores and labels bit-exact vs the reference post_process (tests/golden/nms_large_*),
+    and the same detections on a second run (no atomic-order dependence)."""
+    from hv_amd import ops
+    tag, seed, B, grids, conf, iou, mx, spread = case
+    g = golden(f"nms_large_{tag}")
+    assert int(np.max(g["max_candidates"])) > 8192
+    dec = {k: {n: t.to(gpu_device) for n, t in v.items()}
+           for k, v in cases.nms_case(seed, B=B, grids=grids, spread=spread).items()}
+    boxes, scores, labels, count = (t.clone() for t in ops.nms_batched(dec, conf, iou, mx))
+    again = ops.nms_batched(dec, conf, iou, mx)
+    for a, b2 in zip((boxes, scores, labels, count), again):
+        assert torch.equal(a, b2)
+    for b in range(B):
+        n = int(count[b])
+        assert n == len(g[f"scores{b}"])
+        np.testing.assert_array_equal(scores[b, :n].cpu().numpy(), g[f"scores{b}"])
+        np.testing.assert_array_equal(labels[b, :n].cpu().numpy(), g[f"labels{b}"])
+        np.testing.assert_array_equal(boxes[b, :n].cpu().numpy(), g[f"boxes{b}"])
+        assert not scores[b, n:].any() and not boxes[b, n:].any()
+
+
+@pytest.mark.parametrize("n,levels", [(1, 1), (16, 3), (17, 2), (300, 7), (5000, 40), (70000, 300)])
+def test_gpu_sort_desc_exact_matches_std_sort(gpu_device, n, levels):
+    """hv_sort_desc_exact == the reference's CPU torch.sort(descending=True).indices (libstdc++
+    introsort: tie order included) on heavily tied values; with the depth limit forced to 0 / 1 /
+    3 it matches oracle/std_sort.py's restatement through the heap-sort fallback too."""
+    from hv_amd import ops
+    from oracle.std_sort import std_sort_desc
+    g = torch.Generator().manual_seed(n)
+    v = (torch.randint(0, levels, (n,), generator=g).float() / levels) * torch.rand(1, generator=g)
+    got = ops.sort_desc_exact(v.to(gpu_device)).cpu()
+    assert torch.equal(got, torch.sort(v, descending=True).indices)
+    if n <= 5000:
+        for d in (0, 1, 3):
+            got = ops.sort_desc_exact(v.to(gpu_device), depth_limit=d).cpu().tolist()
+            assert got == std_sort_desc(v.tolist(), depth_limit=d), d
+
+
+def test_gpu_post_process_ties_match_oracle(gpu_device):
+    """Scores on a coarse grid (hundreds of ties per scale, > 8,192 candidates at scale 0) with
+    clustered boxes: which of two tied boxes survives, and the output order, follow the
+    reference's unstable CPU sort (oracle = the reference's own torch.sort call)."""
+    from oracle import hv_oracle as O
+    from hv_amd import ops
+    dec = cases.nms_case(31, B=2, grids=((80, 80), (40, 40), (20, 20)))
+    for v in dec.values():
+        v["class_scores"] = torch.round(v["class_scores"] * 200) / 200
+    for conf, iou, mx in ((0.01, 0.5, 100), (0.3, 0.7, 3000)):
+        ref = O.post_process(dec, conf, iou, mx)
+        dd = {k: {n: t.to(gpu_device) for n, t in v.items()} for k, v in dec.items()}
+        boxes, scores, labels, count = ops.nms_batched(dd, conf, iou, mx)
+        for b in range(2):
+            n = int(count[b])
+            assert n == len(ref[b]["scores"])
+            np.testing.assert_array_equal(scores[b, :n].cpu().numpy(), ref[b]["scores"].numpy())
+            np.testing.assert_array_equal(labels[b, :n].cpu().numpy(), ref[b]["labels"].numpy())
+            np.testing.assert_array_equal(boxes[b, :n].cpu().numpy(), ref[b]["boxes"].reshape(-1, 4).numpy())
+
+
 def test_gpu_nms_large_matches_oracle(gpu_device):
     """640x640-sized grids (19200 + 4800 + 1200 cells, many candidates) vs the oracle."""
     from oracle import hv_oracle as O
@@ -648,6 +711,7 @@ def test_gpu_nms_large_matches_oracle(gpu_device):
         assert n == len(ref[b]["scores"])
         np.testing.assert_array_equal(scores[b, :n].cpu().numpy(), ref[b]["scores"].numpy())
         np.testing.assert_array_equal(labels[b, :n].cpu().numpy(), ref[b]["labels"].numpy())
+        np.testing.assert_array_equal(boxes[b, :n].cpu().numpy(), ref[b]["boxes"].reshape(-1, 4).numpy())
 
 
 @pytest.mark.parametrize("h,w,oh,ow", [(480, 640, 640, 640), (720, 1280, 640, 640), (64, 64, 64, 64), (300, 200, 416, 416)])

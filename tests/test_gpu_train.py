@@ -229,7 +229,7 @@ def test_sinkhorn_backward_matches_reference_fixture(gpu_device, fam, D, it):
     gld = golden(f"sk_{fam}_D{D}_it{it}")
     raw = cases.sinkhorn_raw(D, it, fam).to(gpu_device).requires_grad_(True)
     grp = ops.SinkhornGroup([raw.detach()], [it], gpu_device)
-    (M,) = SinkhornGroupFn.apply(grp, raw)
+    (M,) = SinkhornGroupFn.apply(grp, None, raw)
     G = torch.randn(D, D, generator=cases.gen_seed(D, it, 3)).to(gpu_device)
     (M * G).sum().backward()
     gr = raw.grad.cpu()
@@ -247,13 +247,13 @@ def test_sinkhorn_backward_grouped_equals_single(gpu_device):
     raws = [cases.sinkhorn_raw(D, 20, "wc").to(gpu_device).requires_grad_(True) for D in Ds]
     Gs = [torch.randn(D, D, device=gpu_device) for D in Ds]
     grp = ops.SinkhornGroup([r.detach() for r in raws], list(its), gpu_device)
-    outs = SinkhornGroupFn.apply(grp, *raws)
+    outs = SinkhornGroupFn.apply(grp, None, *raws)
     sum((o * G).sum() for o, G in zip(outs, Gs)).backward()
     grouped = [r.grad.clone() for r in raws]
     for r, it, G, gg in zip(raws, its, Gs, grouped):
         r2 = r.detach().clone().requires_grad_(True)
         g1 = ops.SinkhornGroup([r2.detach()], [it], gpu_device)
-        (o,) = SinkhornGroupFn.apply(g1, r2)
+        (o,) = SinkhornGroupFn.apply(g1, None, r2)
         (o * G).sum().backward()
         assert torch.equal(r2.grad, gg)
 
@@ -521,8 +521,9 @@ def test_grouped_train_prep_matches_per_site(gpu_device, precision):
     """The grouped training coefficient prep (train_prep.TrainPrep: prep group + ONE transpose group
     launch for all sites) gives the loss and every parameter gradient of the per-site preparation
     (model.hv_train_group_prep = False), dropout off: bitwise-close in fp32 (the same fp32 products,
-    other launch boundaries), within bf16 rounding of the fold GEMM in bf16; a second forward before
-    the first backward is refused."""
+    other launch boundaries), within bf16 rounding of the fold GEMM in bf16.  Two forwards before one
+    backward (`model(x1) + model(x2)`, reference autograd semantics) give the per-site gradients too:
+    the second forward takes a second buffer set from the pool instead of overwriting the first's."""
     from hv_amd.targets import synthetic_targets
     res = {}
     for grouped in (True, False):
@@ -543,13 +544,27 @@ def test_grouped_train_prep_matches_per_site(gpu_device, precision):
     for n in g0:
         d = (g1[n] - g0[n]).norm().item()
         assert d <= tol * g0[n].norm().item() + 1e-6, (n, d, g0[n].norm().item())
-    m, _ = _tiny_model(gpu_device, precision)
-    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(3)).to(gpu_device)
-    tg = [t.to(gpu_device) for t in synthetic_targets(2, 64, seed=4)]
-    first = m(x, targets=tg, compute_loss=True)["loss"]["total_loss"]
-    m(x, targets=tg, compute_loss=True)
-    with pytest.raises(RuntimeError, match="one forward per backward"):
-        first.backward()
+    two = {}
+    for grouped in (True, False):
+        m, _ = _tiny_model(gpu_device, precision)
+        m.hv_train_group_prep = grouped
+        x1 = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(3)).to(gpu_device)
+        x2 = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(5)).to(gpu_device)
+        tg = [t.to(gpu_device) for t in synthetic_targets(2, 64, seed=4)]
+        loss = m(x1, targets=tg, compute_loss=True)["loss"]["total_loss"] + \
+            m(x2, targets=tg, compute_loss=True)["loss"]["total_loss"]
+        loss.backward()
+        torch.cuda.synchronize()
+        two[grouped] = {n: p.grad.detach().float().cpu() for n, p in m.named_parameters() if p.grad is not None}
+        pool = m.__dict__["_train_prep_cache"]["pool"]
+        assert len(pool) == 2 and all(e["busy"] == 0 for e in pool)
+        # a forward whose graph is dropped without a backward frees its set again
+        m(x1, targets=tg, compute_loss=True)
+        m(x2, targets=tg, compute_loss=True)
+        assert len(pool) == 2 and all(e["busy"] == 0 for e in pool)
+    for n in two[False]:
+        d = (two[True][n] - two[False][n]).norm().item()
+        assert d <= tol * two[False][n].norm().item() + 1e-6, (n, d)
 
 
 def test_tiny_train_step_grads_match_oracle(gpu_device):
@@ -961,31 +976,45 @@ def test_trainer_graph_dropout_masks_change_per_replay(gpu_device):
     assert res[False][1] == res[False][2] == res[False][3]
 
 
-def test_trainer_graph_recaptures_on_hyperparameter_change(gpu_device):
-    """A captured step carries lr / weight decay / betas / eps / clip norms and the model's kernel
-    variants by value: changing opt.lr between replays (a scheduler), or model.set_options(),
-    must re-capture -- with lr = wd = 0 after the change the parameters stay bit-identical, which
-    a stale replay at lr = 1e-3 would not give.  step_count counts steps, not captures."""
+def test_trainer_graph_hyperparameters_without_recapture(gpu_device):
+    """AdamW reads lr / betas / eps / weight decay from the optimizer's DEVICE array, refreshed
+    before every replay: a scheduler changing lr every step (mhc_trainer.py:275) keeps replaying
+    ONE captured graph, and the replayed steps equal the eager trainer's under the same schedule
+    bit for bit; lr = wd = 0 after a change leaves the parameters bit-identical (a stale replay
+    would not).  The clip norms and the model's kernel variants are baked in: changing them
+    re-captures.  step_count counts steps, not captures."""
     from hv_amd.targets import synthetic_targets
     from hv_amd.trainer import HVTrainer
-    m, _ = _tiny_model(gpu_device, "bf16")
-    tr = HVTrainer(m, lr=1e-3, monitor_every=0, graph=True)
+    ma, _ = _tiny_model(gpu_device, "bf16")
+    mb, _ = _tiny_model(gpu_device, "bf16")
+    ta = HVTrainer(ma, lr=1e-3, monitor_every=0)
+    tb = HVTrainer(mb, lr=1e-3, monitor_every=0, graph=True)
     B, S = 2, 96
     x = torch.randn(B, 3, S, S, generator=torch.Generator().manual_seed(9)).to(gpu_device)
     tg = [t.to(gpu_device) for t in synthetic_targets(B, S, seed=9)]
-    for _ in range(3):
-        tr.step(x, tg)
-    assert tr.captures == 1 and tr.replays == 2 and tr.opt.step_count == 3
-    tr.opt.lr, tr.opt.wd = 0.0, 0.0
-    before = [p.detach().clone() for p in m.parameters()]
-    tr.step(x, tg)
+    for step in range(6):
+        lr = 1e-3 * (0.5 + 0.5 * np.cos(np.pi * step / 6))     # cosine schedule, new value per step
+        for t in (ta, tb):
+            t.opt.lr = lr
+            t.opt.wd = 1e-4 * (1 + step)
+            t.step(x, tg)
+        torch.cuda.synchronize()
+        for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+            assert torch.equal(pa, pb), (step, n)
+    assert tb.captures == 1 and tb.replays == 5 and tb.opt.step_count == 6
+    tb.opt.lr, tb.opt.wd = 0.0, 0.0
+    before = [p.detach().clone() for p in mb.parameters()]
+    tb.step(x, tg)
     torch.cuda.synchronize()
-    assert tr.captures == 2 and tr.opt.step_count == 4
-    for a, p in zip(before, m.parameters()):
+    assert tb.captures == 1 and tb.opt.step_count == 7
+    for a, p in zip(before, mb.parameters()):
         assert torch.equal(a, p)
-    m.set_options(use_fused_mhc=False)
-    tr.step(x, tg)
-    assert tr.captures == 3 and tr.opt.step_count == 5
+    tb.opt.max_norms[0] = 0.25
+    tb.step(x, tg)
+    assert tb.captures == 2
+    mb.set_options(use_fused_mhc=False)
+    tb.step(x, tg)
+    assert tb.captures == 3 and tb.opt.step_count == 9
 
 
 def test_trainer_skips_parameters_without_gradient(gpu_device):

@@ -252,6 +252,35 @@ def test_post_process_oracle_matches_reference(seed):
         np.testing.assert_allclose(r["boxes"].reshape(-1, 4).numpy(), g[f"boxes{b}"], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_std_sort_restatement_matches_torch_sort(seed):
+    """oracle/std_sort.py (libstdc++ introsort over (value, index), descending) reproduces the
+    reference's torch.sort(descending=True).indices exactly -- tie order included -- on inputs
+    with heavy ties (the NMS sort, yolo_head.py:700)."""
+    from oracle.std_sort import std_sort_desc
+    g = torch.Generator().manual_seed(seed)
+    for _ in range(20):
+        n = int(torch.randint(1, 2500, (1,), generator=g))
+        k = int(torch.randint(1, 60, (1,), generator=g))
+        v = torch.randint(0, k, (n,), generator=g).float() / k
+        assert std_sort_desc(v.tolist()) == torch.sort(v, descending=True).indices.tolist()
+    v = torch.round(torch.rand(20000, generator=g) * 3000) / 3000
+    assert std_sort_desc(v.tolist()) == torch.sort(v, descending=True).indices.tolist()
+
+
+@pytest.mark.parametrize("case", cases.NMS_LARGE_CASES, ids=[c[0] for c in cases.NMS_LARGE_CASES])
+def test_post_process_oracle_matches_reference_large(case):
+    """§8f-1 at detection-grid sizes: > 8,192 candidates per scale (640^2 / 1024^2 grids at conf
+    0.01) and max_det up to 5,000 -- the oracle vs the reference (tests/golden/nms_large_*)."""
+    tag, seed, B, grids, conf, iou, mx, spread = case
+    g = golden(f"nms_large_{tag}")
+    res = O.post_process(cases.nms_case(seed, B=B, grids=grids, spread=spread), conf, iou, mx)
+    for b, r in enumerate(res):
+        np.testing.assert_array_equal(r["labels"].numpy(), g[f"labels{b}"])
+        np.testing.assert_array_equal(r["scores"].numpy(), g[f"scores{b}"])
+        np.testing.assert_array_equal(r["boxes"].reshape(-1, 4).numpy(), g[f"boxes{b}"])
+
+
 @pytest.mark.parametrize("case", [c[0] for c in cases.PIL_CASES])
 def test_preprocess_oracle_matches_pillow(case):
     """oracle/preproc.py (numpy restatement of Pillow's Resample.c) against Pillow's own output

@@ -9,6 +9,8 @@ mkdir -p $OUT
 for step in "$@"; do
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; } ; tail -3 $OUT/tests.log ;;
+    ktests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$KEXPR" > $OUT/ktests.log 2>&1 || { tail -40 $OUT/ktests.log; exit 1; } ; tail -3 $OUT/ktests.log ;;
+    vitprobe) timeout -k 10 300 python -u tools/vit_grad_probe.py > $OUT/vit_grad_probe.txt 2>&1 || { tail -30 $OUT/vit_grad_probe.txt; exit 1; } ; head -60 $OUT/vit_grad_probe.txt ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; } ; tail -2 $OUT/smoke.log ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
     benchq) timeout -k 10 300 python -u bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
