@@ -163,7 +163,7 @@ def pmc_child(a):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = HybridVisionSystem({"image_size": a.size, "precision": a.precision, "verbose": False}).to(dev).eval()
-    model.set_options(branch_min_batch=1 << 30)     # one stream: per-dispatch busy cycles are the kernel's own
+    model.set_options(branch_min_batch=1 << 30, prep_overlap_min_batch=1 << 30)     # one stream: per-dispatch busy cycles are the kernel's own
     x = torch.randn(a.batch, 3, a.size, a.size, device=dev)
     with torch.no_grad():
         for _ in range(2):
@@ -380,7 +380,7 @@ def main():
     # interval measures the shared GPU, not the kernel)
     from hv_amd.runtime import module_options
     opts0 = module_options(model)
-    model.set_options(branch_min_batch=1 << 30)
+    model.set_options(branch_min_batch=1 << 30, prep_overlap_min_batch=1 << 30)
     with torch.no_grad(), GemmTimer(ops) as gt:
         model(x)
     model.set_options(opts0)

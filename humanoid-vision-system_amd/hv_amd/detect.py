@@ -16,8 +16,10 @@ from .manifold import ManifoldHyperConnection, prepare_plans
 from .runtime import Branches, HVOptions, RunCtx, VersionWatch, current, module_options, require_cuda, use_ctx, PRECISIONS
 from .vit import HybridVisionEncoder
 
-# side-stream Sinkhorn + mHC prep (PrepProgram.run overlap): opt-in (HVOptions.prep_overlap); on
-# one box, interleaved runs measured it 0.1 ms/step SLOWER in graph and eager mode
+# side-stream Sinkhorn + mHC prep (PrepProgram.run overlap) from batch HVOptions.prep_overlap_min_batch
+# (8): round 6, base 640 bf16 B=16 graph step 17.30 -> 17.01 / 17.26 -> 17.10 ms (same box, alternating);
+# at B=1 (recompute) 5.81 vs 5.85 ms, so off there (profiles/r06/prep_overlap_ab.txt).  Round 1 measured
+# it 0.1 ms slower, before the weight prep and the GEMM kernels beside it were rewritten.
 
 # outputs['detections'] keys: the per-scale names DetectionPostprocessor (postprocessing.py:
 # 234-244, 270-281) and MHCYOLOLoss (loss_functions.py:86) look up
@@ -447,11 +449,12 @@ class HybridVisionSystem(nn.Module):
         self._frozen = (None, None) if enabled else None
         return self
 
-    def _make_ctx(self) -> RunCtx:
+    def _make_ctx(self, batch: int = 1) -> RunCtx:
         opts = module_options(self)
         ctx = RunCtx(dtype=PRECISIONS[self.hv_precision], opts=opts)
         key = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
-        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=opts.prep_overlap, groups=self._qkv_groups)
+        overlap = opts.prep_overlap or batch >= opts.prep_overlap_min_batch
+        prepare_plans(self._mhc_modules, ctx, self._sk_cache, key, overlap=overlap, groups=self._qkv_groups)
         return ctx
 
     def capture(self, example: torch.Tensor, task: str = "detection") -> "GraphRunner":
@@ -459,12 +462,12 @@ class HybridVisionSystem(nn.Module):
         graph; the returned runner copies its input into the captured buffer and replays."""
         return GraphRunner(self, example, task)
 
-    def _ctx(self) -> RunCtx:
+    def _ctx(self, batch: int = 1) -> RunCtx:
         if self._frozen is None:
-            return self._make_ctx()
+            return self._make_ctx(batch)
         ver = self._watch.snapshot()
         if self._frozen[0] != ver:
-            self._frozen = (ver, self._make_ctx())
+            self._frozen = (ver, self._make_ctx(batch))
         return self._frozen[1]
 
     # ---- forward (hybrid_vision.py:222-367)
@@ -484,7 +487,7 @@ class HybridVisionSystem(nn.Module):
         nothing per call is stored on the module, so concurrent forwards from several threads
         (the engine's worker pool) do not interfere."""
         require_cuda(x, "HybridVisionSystem")
-        ctx = self._ctx()
+        ctx = self._ctx(x.shape[0])
         with torch.no_grad(), use_ctx(ctx):
             # independent parts on side streams (runtime.Branches): base 640 bf16 B=16 graph step
             # 17.37 vs 17.85 ms; at B=1 the cross-stream edges cost more than the overlap wins

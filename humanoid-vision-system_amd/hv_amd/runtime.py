@@ -34,7 +34,8 @@ class HVOptions:
     cls_only_last_block: bool = True  # last ViT block on the CLS query only (exact)
     group_qkv: bool = True            # q / k / v GEMM1 as one N = 3*2Hd GEMM (exact)
     parallel_qkv: bool = False        # q / k / v on three streams: measured slower (tools/ab_vit.py)
-    prep_overlap: bool = False        # Sinkhorn + mHC prep on a side stream: measured no gain
+    prep_overlap: bool = False        # Sinkhorn + mHC prep on a side stream at every batch
+    prep_overlap_min_batch: int = 8   # ... and from this batch on (B=16: -0.9..-1.8 %; B=1 recompute: +0.7 %)
     direct_stem: bool = True          # MFMA stem conv straight from the NCHW image (hv_conv_stem)
     splitk: bool = False              # split-K for small output grids: measured no gain
     gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic

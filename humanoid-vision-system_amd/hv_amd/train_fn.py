@@ -186,7 +186,7 @@ class MhcFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, H_res, H_pre_raw, H_post_raw, g_pre, b_pre, W1, b1, W2, b2, g_post, b_post, m, seeds,
-                coef=None):
+                coef=None, out_f32=False):
         dt = x.dtype
         D, Hd = m.input_dim, m.hidden_dim
         p1, p2, p3 = m.mlp[2].p, m.mlp[5].p, m.dropout.p
@@ -208,7 +208,10 @@ class MhcFn(torch.autograd.Function):
             pre2 = torch.empty((x.shape[0], Hd), device=x.device, dtype=dt)
             h2 = T.gemm_train(h1, w2, mode=1, act="gelu", aux=pre2, bias=f32(b2), drop_p=p2, seed=s2)
             yc = ops.gemm(x, wct_dt, a2=h2, out_dtype=torch.float32)
-            y, mean2, rstd2 = T.rownorm_train(T.LN, yc, 1e-5, g_post, b_post, p3, s3, out_dtype=dt)
+            # out_f32: the output in fp32 (autocast's LayerNorm output dtype, manifold_layers.py:248-270)
+            # for sites that feed an fp32 residual stream (the ViT blocks' residual_mhc1/2)
+            y, mean2, rstd2 = T.rownorm_train(T.LN, yc, 1e-5, g_post, b_post, p3, s3,
+                                              out_dtype=torch.float32 if out_f32 else dt)
         ctx.m = m
         ctx.meta = (p1, p2, p3, s1, s2, s3)
         ctx.save_for_backward(x, z, mean, rstd, pre1, h1, pre2, h2, yc, mean2, rstd2, gc, u, wct, A1,
@@ -264,16 +267,17 @@ class MhcFn(torch.autograd.Function):
         dH_pre_raw, dg_pre, db_pre, dH_res, dH_post_raw = T.mhc_param_backward(
             dGc, du, H_pre_raw, g_pre, b_pre, dwc_x, dwc_h, H_post_raw)
         return (dx, dH_res, dH_pre_raw, dH_post_raw, dg_pre, db_pre, dW1, db1, dW2, db2, dg_post, db_post,
-                None, None, None)
+                None, None, None, None)
 
 
-def mhc(m, x: Tensor, H_res: Tensor, coef=None) -> Tensor:
+def mhc(m, x: Tensor, H_res: Tensor, coef=None, out_f32: bool = False) -> Tensor:
     """coef: the site's train_prep.TrainCoef when the model's coefficients were prepared in one
-    grouped pass (train_model.system_forward), else None (per-site preparation)."""
+    grouped pass (train_model.system_forward), else None (per-site preparation).  out_f32: fp32
+    output whatever the compute dtype (autocast's LayerNorm output dtype)."""
     seeds = tuple(next_seed() if pp > 0 else 0 for pp in (m.mlp[2].p, m.mlp[5].p, m.dropout.p))
     y = MhcFn.apply(x, H_res, m.H_pre_raw, m.H_post_raw, m.norm_pre.weight, m.norm_pre.bias,
                     m.mlp[0].weight, m.mlp[0].bias, m.mlp[3].weight, m.mlp[3].bias,
-                    m.norm_post.weight, m.norm_post.bias, m, seeds, coef)
+                    m.norm_post.weight, m.norm_post.bias, m, seeds, coef, bool(out_f32))
     if m.training:                                   # a4: manifold_layers.py:275-276 (throttled)
         cnt = getattr(m, "_mon_count", 0)
         m._mon_count = cnt + 1
@@ -398,8 +402,10 @@ class RMSNormFn(torch.autograd.Function):
     """RMSNorm (manifold_layers.py:449-456)."""
 
     @staticmethod
-    def forward(ctx, x, scale, eps: float):
-        y, _, rstd = T.rownorm_train(T.RMS, x.contiguous(), eps, scale)
+    def forward(ctx, x, scale, eps: float, out_dtype=None):
+        """out_dtype: the output dtype when it differs from x's (an fp32 residual stream normalised
+        into a bf16 GEMM operand, or a bf16 tensor starting an fp32 stream)."""
+        y, _, rstd = T.rownorm_train(T.RMS, x.contiguous(), eps, scale, out_dtype=out_dtype)
         ctx.save_for_backward(x, rstd, scale)
         return y
 
@@ -408,7 +414,7 @@ class RMSNormFn(torch.autograd.Function):
         x, rstd, scale = ctx.saved_tensors
         dx, dscale, _ = T.rownorm_backward(T.RMS, x.contiguous(), g.contiguous(), None, rstd, scale,
                                            dx_dtype=x.dtype)
-        return dx, dscale, None
+        return dx, dscale, None, None
 
 
 class GatherRowsFn(torch.autograd.Function):

@@ -82,9 +82,9 @@ def _hres_table(model) -> HTable:
     return H
 
 
-def _mhc(m, x: torch.Tensor, H) -> torch.Tensor:
+def _mhc(m, x: torch.Tensor, H, out_f32: bool = False) -> torch.Tensor:
     """TF.mhc with the site's grouped coefficients when the table carries them."""
-    return TF.mhc(m, x, H[id(m)], getattr(H, "coefs", {}).get(id(m)))
+    return TF.mhc(m, x, H[id(m)], getattr(H, "coefs", {}).get(id(m)), out_f32)
 
 
 def module_H(module) -> Dict[int, torch.Tensor]:
@@ -204,17 +204,25 @@ def attention(a, x, n, H):
     return _mhc(a.out_proj, o.reshape(n * L, -1), H)
 
 
-def encoder_block(blk, x, n, H):
-    """TransformerEncoderBlock.forward (vit_encoder_decoder.py:174-210)."""
-    h = TF.RMSNormFn.apply(x, blk.norm1.scale, blk.norm1.eps)
+VIT_F32_STREAM = True     # tools/vit_grad_probe.py A/B switch: the ViT residual stream in fp32
+
+
+def encoder_block(blk, x, n, H, dt):
+    """TransformerEncoderBlock.forward (vit_encoder_decoder.py:174-210).  The residual stream x is
+    fp32 in every precision, as under the reference's autocast: the residual mHC outputs are
+    LayerNorm outputs (fp32 under autocast) and the adds of fp32 tensors stay fp32, so the stream
+    -- and, in the backward, the gradient that flows down it through all blocks -- is never
+    rounded to bf16; only the operands of the GEMMs (the RMSNorm outputs) are `dt`."""
+    f32 = x.dtype == torch.float32
+    h = TF.RMSNormFn.apply(x, blk.norm1.scale, blk.norm1.eps, dt)
     a = attention(blk.attention, h, n, H)
-    a = _mhc(blk.residual_mhc1, a, H)
+    a = _mhc(blk.residual_mhc1, a, H, out_f32=f32)
     p = blk.dropout.p
     x = TF.DropAddFn.apply(x, a, p, TF.next_seed() if p > 0 else 0)
-    h = TF.RMSNormFn.apply(x, blk.norm2.scale, blk.norm2.eps)
+    h = TF.RMSNormFn.apply(x, blk.norm2.scale, blk.norm2.eps, dt)
     h = TF.linear(h, blk.mlp[0], act="gelu", p=blk.mlp[2].p)
     h = TF.linear(h, blk.mlp[3], act="none", p=blk.mlp[4].p)
-    h = _mhc(blk.residual_mhc2, h, H)
+    h = _mhc(blk.residual_mhc2, h, H, out_f32=f32)
     return TF.DropAddFn.apply(x, h, p, TF.next_seed() if p > 0 else 0)
 
 
@@ -228,15 +236,17 @@ def vit_encoder(enc, x, H, features=None, head: bool = True):
     pos = _positions(pe.position_embeddings, h * w)
     z = TF.VitAssembleFn.apply(t, pe.cls_token, pos)
     L = h * w + 1
-    t = TF.RMSNormFn.apply(z.view(n * L, d), pe.norm.scale, pe.norm.eps)
+    dt = z.dtype
+    t = TF.RMSNormFn.apply(z.view(n * L, d), pe.norm.scale, pe.norm.eps,
+                           torch.float32 if VIT_F32_STREAM else dt)          # the fp32 residual stream
     if features is not None:
         features.append(t.view(n, L, d))
     for blk in enc.blocks:
-        t = encoder_block(blk, t, n, H)
+        t = encoder_block(blk, t, n, H, dt)
         if features is not None:
             features.append(t.view(n, L, d))
     cls = TF.GatherRowsFn.apply(t, L)
-    cls = TF.RMSNormFn.apply(cls, enc.norm.scale, enc.norm.eps)
+    cls = TF.RMSNormFn.apply(cls, enc.norm.scale, enc.norm.eps, dt)
     if head and isinstance(enc.head, nn.Linear):
         cls = TF.linear(cls, enc.head)
     return cls

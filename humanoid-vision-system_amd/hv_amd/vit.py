@@ -122,8 +122,9 @@ class TransformerEncoderBlock(nn.Module):
             from . import train_model as TM
             from .runtime import resolve_dtype
             n, L, D = x.shape
-            t = x.reshape(n * L, D).to(resolve_dtype(self.residual_mhc1)).contiguous()
-            return TM.encoder_block(self, t, n, TM.module_H(self)).view(n, L, D).to(x.dtype)
+            t = x.reshape(n * L, D).float().contiguous()        # the block's residual stream is fp32
+            return TM.encoder_block(self, t, n, TM.module_H(self),
+                                    resolve_dtype(self.residual_mhc1)).view(n, L, D).to(x.dtype)
         with ctx_scope(self) as ctx:
             n, L, D = x.shape
             t = x.reshape(n * L, D).to(ctx.dtype).contiguous()

@@ -117,6 +117,13 @@ NMS_LARGE_CASES = [
 ]
 
 
+# extra input batches of the base training step's bf16 anchors (x seeds; the fixtures' own batches
+# are seed 1 at 224 and seed 7 at 640): oracle/gen_golden.py --only bf16ref --bf16ref
+# train,train224seeds,train640seeds writes train_base_{224,640}_b2_seeds.npz
+TRAIN224_SEEDS = (2, 3, 4, 5, 6, 7, 8, 9)
+TRAIN640_SEEDS = (8, 9, 10, 11)
+
+
 PIL_CASES = [  # (tag, frames, in_h, in_w, out_h, out_w, seed)
     ("720x1280_640", 1, 720, 1280, 640, 640, 11),    # the reference webcam (scripts/inference.py:236-238)
     ("480x640_640", 2, 480, 640, 640, 640, 12),      # vertical upscale, horizontal identity-ish

@@ -973,3 +973,28 @@ def test_device_tables_hold_every_pointer(gpu_device):
     for what, o in owners.items():
         assert tables._TABLES in o.__dict__, what
         assert tables.unheld_pointers(o) == [], what
+
+
+def test_prep_overlap_equals_serial_prep(gpu_device):
+    """HVOptions.prep_overlap (the Sinkhorn group + mHC coefficient prep on a side stream beside the
+    weight prep and the first layers; default from batch 8): the eager forward and a captured
+    graph's replay give bit-identical outputs with and without it."""
+    from hv_amd import HybridVisionSystem
+    m = HybridVisionSystem(dict(num_blocks=[1, 1, 1, 1], vit_depth=2, sk_iters=5, verbose=False))
+    W.load_formula_weights(m, "wc")
+    m = m.to(gpu_device).eval()
+    x = torch.randn(8, 3, 96, 96, generator=torch.Generator().manual_seed(4)).to(gpu_device)
+    outs = {}
+    for on in (False, True):
+        m.set_options(prep_overlap=on, prep_overlap_min_batch=1 << 30)
+        with torch.no_grad():
+            eager = {k: v.clone() for k, v in m(x)["predictions"].items()}
+            runner = m.capture(x)
+            g = {k: v.clone() for k, v in runner.replay()["predictions"].items()}
+        torch.cuda.synchronize()
+        outs[on] = (eager, g)
+        del runner
+    for s in outs[False][0]:
+        assert torch.equal(outs[False][0][s], outs[True][0][s]), s
+        assert torch.equal(outs[False][1][s], outs[True][1][s]), s
+        assert torch.equal(outs[True][0][s], outs[True][1][s]), s

@@ -21,7 +21,7 @@ def test_mhc_prep_group_matches_per_site(gpu_device, dtype):
     from hv_amd.prep import PrepProgram
     from hv_amd.runtime import RunCtx
     mods = [ManifoldHyperConnection(D, expansion_rate=e) for D, e in
-            [(32, 4), (64, 4), (256, 2), (256, 4), (96, 2), (1792, 2)]]
+            [(32, 4), (64, 4), (256, 2), (256, 4), (96, 2), (320, 2), (512, 4), (1792, 2)]]
     for m in mods:
         W.load_formula_weights(m, "wc")
         m.to(gpu_device).eval()

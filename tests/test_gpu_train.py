@@ -725,16 +725,18 @@ def _base_train_step(gpu_device, precision, B, S, seed_x, target_seed):
     return loss, preds, dict(norms), finite
 
 
-def _anchor_check(mine: dict, ref: dict, what: str):
-    """Per-group errors held to the reference's own bf16 errors (S8): each group within 3x its
-    reference error (floor 1e-2: near-exact groups would otherwise test rounding), and the mean
-    over groups within 2x the reference mean."""
-    bad = {k: (mine[k], ref[k]) for k in ref if mine.get(k, 1.0) > 3.0 * max(ref[k], 1e-2)}
+def _anchor_check(mine: dict, ref: dict, what: str, per_group: float = 1.5, mean: float = 1.5):
+    """Per-group errors held to the reference's own bf16 errors (S8): each group within
+    `per_group` x its reference error (floor 1e-2: near-exact groups would otherwise test
+    rounding), and the mean over groups within `mean` x the reference mean.  Both sides are
+    medians over input batches where the caller has several (the groups are chaotic at init)."""
+    bad = {k: (mine[k], ref[k]) for k in ref if mine.get(k, 1.0) > per_group * max(ref[k], 1e-2)}
     assert not bad, (what, bad)
     m_mean = float(np.mean([mine[k] for k in ref]))
     r_mean = float(np.mean(list(ref.values())))
-    assert m_mean <= 2.0 * r_mean, (what, m_mean, r_mean)
-    return {"hip_mean": m_mean, "ref_bf16_mean": r_mean}
+    assert m_mean <= mean * r_mean, (what, m_mean, r_mean)
+    return {"hip_mean": m_mean, "ref_bf16_mean": r_mean,
+            "max_ratio": max(mine[k] / max(ref[k], 1e-2) for k in ref)}
 
 
 def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
@@ -746,11 +748,15 @@ def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
       (1) 224x224 B=2 vs the reference's fp64 run (fixture train_base_224_b2): total loss within
           3x the reference-bf16 loss error; per (top-level module, clip group) gradient norm --
           the quantities the trainer's per-group clipping (mhc_trainer.py:342-383) acts on --
-          within 3x the reference-bf16 group error, mean over groups within 2x; head logits within
-          1.25x the reference-bf16 logits error;
+          within 1.5x the reference-bf16 group error, mean over groups within 1.5x, both sides the
+          MEDIAN over three input batches (x seeds 1, 2, 3; fixtures train_base_224_b2 and
+          train_base_224_b2_seeds: the reference in fp64 and under the bf16 policy per batch);
+          head logits within 1.25x the reference-bf16 logits error;
       (2) 640x640 B=2 (config C's resolution), HIP bf16 vs HIP fp32 on the same batch, against the
-          reference's bf16-vs-fp32 on that same batch (x seed 7, targets seed 11): the same loss /
-          group / logits bounds, plus finiteness of every gradient.
+          reference's bf16-vs-fp32 on the same batches (x seeds 7-11, targets seed 11; fixtures
+          train_base_640_b2_ref and train_base_640_b2_seeds): gradient groups as medians over the
+          five batches on both sides, loss / logits on the fixture batch, plus finiteness of every
+          gradient.
     Train-mode logits at init are NOT a usable bf16 observable: BatchNorm batch statistics over
     B=2 amplify rounding, and the reference's own bf16 logits are 0.89-0.96 rel-L2 from its
     fp64 / fp32 runs (measured on the fixtures) -- the loss and gradient groups are."""
@@ -767,25 +773,41 @@ def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
     refb = _group_norms([(n, v) for n, v in zip(names, gb["grad_norm"]) if v >= 0])
     mine = _group_norms(n16.items())
     l64 = float(g["total_loss_f64"])
-    e_groups = {k: abs(mine.get(k, 0.0) / v - 1) for k, v in ref64.items() if v > 0}
-    r_groups = {k: abs(refb[k] / v - 1) for k, v in ref64.items() if v > 0}
+    med = lambda ds: {k: float(np.median([d[k] for d in ds])) for k in ds[0]}   # noqa: E731
+    # group errors per input batch: x seed 1 (the fixture), 2 and 3 (train_base_224_b2_seeds)
+    gs = golden("train_base_224_b2_seeds")
+    e_seed = [{k: abs(mine.get(k, 0.0) / v - 1) for k, v in ref64.items() if v > 0}]
+    r_seed = [{k: abs(refb[k] / v - 1) for k, v in ref64.items() if v > 0}]
+    for xs in cases.TRAIN224_SEEDS:
+        _, _, n16s, fin = _base_train_step(gpu_device, "bf16", B, S, xs, int(g["target_seed"]))
+        assert fin
+        r64s = _group_norms([(n, v) for n, v in zip(names, gs[f"grad_norm_f64_s{xs}"]) if v >= 0])
+        rbs = _group_norms([(n, v) for n, v in zip(names, gs[f"grad_norm_bf16_s{xs}"]) if v >= 0])
+        mines = _group_norms(n16s.items())
+        e_seed.append({k: abs(mines.get(k, 0.0) / v - 1) for k, v in r64s.items() if v > 0})
+        r_seed.append({k: abs(rbs[k] / v - 1) for k, v in r64s.items() if v > 0})
+    e_groups, r_groups = med(e_seed), med(r_seed)
     e_log = {s: float(np.linalg.norm(p16[f"scale_{s}"] - g[f"pred{s}_f64"]) / np.linalg.norm(g[f"pred{s}_f64"]))
              for s in range(3)}
     r_log = {s: float(gb[f"pred{s}_err_vs_f64"]) for s in range(3)}
     rec = {"224_b2_vs_ref_f64": {"loss_rel": abs(loss16["total_loss"] / l64 - 1),
                                  "ref_bf16_loss_rel": abs(float(gb["total_loss"]) / l64 - 1),
+                                 "x_seeds": [1] + list(cases.TRAIN224_SEEDS),
+                                 "statistic": f"median over the {1 + len(cases.TRAIN224_SEEDS)} batches",
                                  "group_norm_rel": e_groups, "ref_bf16_group_norm_rel": r_groups,
+                                 "group_norm_rel_per_seed": e_seed, "ref_bf16_group_norm_rel_per_seed": r_seed,
                                  "logits_rel_l2": e_log, "ref_bf16_logits_rel_l2": r_log}}
     r1 = rec["224_b2_vs_ref_f64"]
-    r1["groups"] = _anchor_check(e_groups, r_groups, "224 groups")
     # (2) config C's resolution: bf16 vs fp32 HIP on the same batch, against the reference's own
-    # (fixture batch: x seed 7, targets seed 11).  Our errors are the MEDIAN over three input
-    # batches (x seeds 7, 8, 9): a gradient group's bf16 error at init swings with the summation
-    # order of its fp32 reductions (round 4: one ViT group 1.06 vs 1.04 allowed on one build,
-    # inside it on another), the median over batches does not
+    # on the same batches.  A gradient group's bf16 error at init is a heavy-tailed function of
+    # where the roundings fall (one batch's ViT group measured 0.04, another 0.79 on the same
+    # build; the reference's own per-batch values spread as widely), so both sides are medians
+    # over several batches
     gr = golden("train_base_640_b2_ref")
-    runs = []
-    for xs in (7, 8, 9):
+    gr2 = golden("train_base_640_b2_seeds")
+    seeds640 = (7,) + tuple(cases.TRAIN640_SEEDS)
+    runs, ref_runs = [], []
+    for xs in seeds640:
         loss32, p32, n32, fin32 = _base_train_step(gpu_device, "fp32", 2, 640, xs, 11)
         loss16b, p16b, n16b, fin16b = _base_train_step(gpu_device, "bf16", 2, 640, xs, 11)
         assert fin32 and fin16b
@@ -794,20 +816,25 @@ def test_base_train_step_bf16_matches_reference_and_fp32(gpu_device):
         runs.append(({k: abs(g16.get(k, 0.0) / v - 1) for k, v in g32.items() if v > 0},
                      {k: abs(loss16b[k] / loss32[k] - 1) for k in loss32 if abs(loss32[k]) > 1e-6},
                      {k: float(np.linalg.norm(p16b[k] - p32[k]) / np.linalg.norm(p32[k])) for k in p32}))
-    med = lambda ds: {k: float(np.median([d[k] for d in ds])) for k in ds[0]}   # noqa: E731
+        sfx = "" if xs == 7 else f"_s{xs}"
+        src = gr if xs == 7 else gr2
+        rf32 = _group_norms([(n, v) for n, v in zip(names, src["grad_norm_f32" + sfx]) if v >= 0])
+        rf16 = _group_norms([(n, v) for n, v in zip(names, src["grad_norm_bf16" + sfx]) if v >= 0])
+        ref_runs.append({k: abs(rf16[k] / v - 1) for k, v in rf32.items() if v > 0})
     e2 = med([r[0] for r in runs])
-    rf32 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_f32"]) if v >= 0])
-    rf16 = _group_norms([(n, v) for n, v in zip(names, gr["grad_norm_bf16"]) if v >= 0])
-    r2g = {k: abs(rf16[k] / v - 1) for k, v in rf32.items() if v > 0}
+    r2g = med(ref_runs)
     rec["640_b2_bf16_vs_fp32"] = {
-        "x_seeds": [7, 8, 9], "statistic": "median over the three batches",
+        "x_seeds": list(seeds640), "statistic": f"median over the {len(seeds640)} batches, both sides",
         "loss_rel": med([r[1] for r in runs]),
         "ref_bf16_loss_rel": abs(float(gr["total_loss_bf16"]) / float(gr["total_loss_f32"]) - 1),
         "group_norm_rel": e2, "ref_bf16_group_norm_rel": r2g,
+        "ref_bf16_group_norm_rel_per_seed": ref_runs,
         "group_norm_rel_per_seed": [r[0] for r in runs],
         "logits_rel_l2": med([r[2] for r in runs]),
         "ref_bf16_logits_rel_l2": [float(v) for v in gr["logits_rel_l2_bf16_vs_f32"]]}
     r2 = rec["640_b2_bf16_vs_fp32"]
+    record_parity("train_bf16_base", rec)          # on file before any bound is checked
+    r1["groups"] = _anchor_check(e_groups, r_groups, "224 groups")
     r2["groups"] = _anchor_check(e2, r2g, "640 groups")
     record_parity("train_bf16_base", rec)
     assert r1["loss_rel"] <= 3.0 * r1["ref_bf16_loss_rel"], r1
@@ -844,7 +871,7 @@ def test_large_1024_train_step_bf16_vs_fp32(gpu_device):
            "loss_rel": abs(loss16["total_loss"] / loss32["total_loss"] - 1),
            "ref640_bf16_loss_rel": abs(float(gr["total_loss_bf16"]) / float(gr["total_loss_f32"]) - 1),
            "group_norm_rel": e, "ref640_bf16_group_norm_rel": r}
-    rec["groups"] = _anchor_check(e, r, "1024 groups")
+    rec["groups"] = _anchor_check(e, r, "1024 groups", per_group=3.0, mean=2.0)   # across resolutions
     record_parity("train_bf16_large_1024", rec)
     for k in ("coord_loss", "obj_loss", "noobj_loss", "cls_loss", "total_loss"):
         assert loss16[k] > 0 and np.isfinite(loss16[k]), (k, loss16)

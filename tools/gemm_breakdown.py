@@ -18,7 +18,7 @@ P = sys.argv[3] if len(sys.argv) > 3 else "bf16"
 
 m = HybridVisionSystem({"precision": P, "verbose": False}).cuda().eval()
 # one stream: HIP events around a launch time that launch only when nothing runs beside it
-m.set_options(branch_min_batch=1 << 30, gemm_variant=int(os.environ.get("HV_GEMM_VARIANT", "0"), 0))
+m.set_options(branch_min_batch=1 << 30, prep_overlap_min_batch=1 << 30, gemm_variant=int(os.environ.get("HV_GEMM_VARIANT", "0"), 0))
 x = torch.randn(B, 3, S, S, device="cuda")
 with torch.no_grad():
     m(x)

@@ -11,6 +11,11 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; } ; tail -3 $OUT/tests.log ;;
     ktests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$KEXPR" > $OUT/ktests.log 2>&1 || { tail -40 $OUT/ktests.log; exit 1; } ; tail -3 $OUT/ktests.log ;;
     vitprobe) timeout -k 10 300 python -u tools/vit_grad_probe.py > $OUT/vit_grad_probe.txt 2>&1 || { tail -30 $OUT/vit_grad_probe.txt; exit 1; } ; head -60 $OUT/vit_grad_probe.txt ;;
+    streamab) timeout -k 10 600 python -u tools/vit_grad_probe.py stream_ab > $OUT/vit_stream_ab.txt 2>&1 || { tail -30 $OUT/vit_stream_ab.txt; exit 1; } ; grep seed $OUT/vit_stream_ab.txt ;;
+    determinism) timeout -k 10 600 python -u tools/vit_grad_probe.py determinism > $OUT/determinism.txt 2>&1 || { tail -30 $OUT/determinism.txt; exit 1; } ; grep differ $OUT/determinism.txt ;;
+    preptime) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/preptime -o run --output-format csv -- python tools/prep_time.py > $OUT/preptime.log 2>&1 || { tail -30 $OUT/preptime.log; exit 1; } ; f=$(find $OUT/preptime -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 32 20 > $OUT/preptime_summary.txt; head -14 $OUT/preptime_summary.txt ;;
+    sweep) timeout -k 10 400 python -u tools/tile_sweep.py > $OUT/tile_sweep.txt 2>&1 || { tail -30 $OUT/tile_sweep.txt; exit 1; } ; cat $OUT/tile_sweep.txt ;;
+    vitbisect) for m in attn32 lin32 qkv32; do timeout -k 10 300 python -u tools/vit_grad_probe.py vit_encoder $m > $OUT/vit_grad_probe_$m.txt 2>&1 || { tail -30 $OUT/vit_grad_probe_$m.txt; exit 1; } ; grep "==" $OUT/vit_grad_probe_$m.txt ; done ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; } ; tail -2 $OUT/smoke.log ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
     benchq) timeout -k 10 300 python -u bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;

@@ -77,11 +77,11 @@ CASES = [
 ]
 if os.environ.get("HV_SWEEP_ONLY"):
     CASES = [c for c in CASES if os.environ["HV_SWEEP_ONLY"] in c[0]]
-print(f"{'case':28s} " + " ".join(f"{n:>9s}" for n in ("auto", "128x128", "64x128", "128x64", "64x64", "256pp")))
+print(f"{'case':28s} " + " ".join(f"{n:>9s}" for n in ("auto", "128x128", "64x128", "128x64", "64x64", "256pp", "sk")))
 for name, mk in CASES:
     fn, flop = mk()
     row = []
-    for code in range(6):
+    for code in range(7):
         with use_ctx(RunCtx(dtype=torch.bfloat16, opts=HVOptions(gemm_variant=code))):   # per-call tile
             try:
                 row.append(timeit(fn))

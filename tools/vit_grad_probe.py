@@ -22,8 +22,82 @@ from test_gpu_train import _base_train_step  # noqa: E402
 from hv_amd.trainer import mhc_group  # noqa: E402
 
 
+def _patch(mode):
+    """Precision bisection: run one part of the ViT in fp32 inside the bf16 step."""
+    from hv_amd import train_fn as TF
+    from hv_amd import train_model as TM
+    f32, b16 = torch.float32, torch.bfloat16
+    if mode == "attn32":                          # attention core (QK^T, softmax, PV and backward) in fp32
+        orig = TF.AttentionFn.apply
+
+        def attn(q, k, v, heads, p, seed):
+            if q.dtype != b16:
+                return orig(q, k, v, heads, p, seed)
+            o = orig(TF.CastFn.apply(q, f32), TF.CastFn.apply(k, f32), TF.CastFn.apply(v, f32), heads, p, seed)
+            return TF.CastFn.apply(o, b16)
+        TF.AttentionFn.apply = attn
+    elif mode == "lin32":                         # the blocks' MLP Linears in fp32
+        orig_lin = TF.linear
+
+        def lin(x, l, act="none", p=0.0, out_dtype=None):
+            if x.dtype == b16 and out_dtype is None:
+                return orig_lin(TF.CastFn.apply(x, f32), l, act, p, out_dtype=b16)
+            return orig_lin(x, l, act, p, out_dtype)
+        TF.linear = lin
+    elif mode == "qkv32":                         # q / k / v / out_proj mHC outputs kept fp32
+        orig_att = TM.attention
+
+        def att(a, x, n, H):
+            if x.dtype != b16:
+                return orig_att(a, x, n, H)
+            L = x.shape[0] // n
+            q = TM._mhc(a.q_proj, x, H, out_f32=True).view(n, L, -1)
+            k = TM._mhc(a.k_proj, x, H, out_f32=True).view(n, L, -1)
+            v = TM._mhc(a.v_proj, x, H, out_f32=True).view(n, L, -1)
+            p = a.dropout.p
+            o = TF.AttentionFn.apply(q, k, v, a.num_heads, p, TF.next_seed() if p > 0 else 0)
+            return TM._mhc(a.out_proj, TF.CastFn.apply(o.reshape(n * L, -1), b16), H)
+        TM.attention = att
+
+
+def stream_ab():
+    """640 B=2 bf16-vs-fp32 gradient-group errors (x seeds 7, 8, 9; targets 11), with and without
+    the fp32 ViT residual stream (train_model.VIT_F32_STREAM)."""
+    from hv_amd import train_model as TM
+    from test_gpu_train import _group_norms
+    dev = torch.device("cuda:0")
+    for xs in (7, 8, 9):
+        _, _, n32, _ = _base_train_step(dev, "fp32", 2, 640, xs, 11)
+        g32 = _group_norms(n32.items())
+        for on in (True, False):
+            TM.VIT_F32_STREAM = on
+            _, _, n16, _ = _base_train_step(dev, "bf16", 2, 640, xs, 11)
+            g16 = _group_norms(n16.items())
+            e = {k: round(abs(g16[k] / v - 1), 4) for k, v in g32.items() if k.startswith("vit")}
+            print(f"seed {xs} f32_stream={on}: {e}", flush=True)
+    TM.VIT_F32_STREAM = True
+
+
+def determinism():
+    """The same 640 B=2 steps twice in one process: are the gradient norms bitwise repeatable?"""
+    dev = torch.device("cuda:0")
+    for prec in ("fp32", "bf16"):
+        a = _base_train_step(dev, prec, 2, 640, 7, 11)[2]
+        b = _base_train_step(dev, prec, 2, 640, 7, 11)[2]
+        diff = [n for n in a if a[n] != b[n]]
+        print(f"{prec}: {len(diff)} of {len(a)} parameter gradient norms differ between two runs; e.g. "
+              f"{[(n, a[n], b[n]) for n in diff[:3]]}", flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "stream_ab":
+        return stream_ab()
+    if len(sys.argv) > 1 and sys.argv[1] == "determinism":
+        return determinism()
     prefix = sys.argv[1] if len(sys.argv) > 1 else "vit_encoder"
+    for mode in sys.argv[2:]:
+        _patch(mode)
+        print(f"patched: {mode}")
     dev = torch.device("cuda:0")
     g = golden("train_base_224_b2")
     gb = golden("train_base_224_b2_bf16ref")
