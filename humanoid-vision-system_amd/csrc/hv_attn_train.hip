@@ -252,26 +252,59 @@ __global__ void __launch_bounds__(256) k_attn_fwd_mfma(const unsigned short* __r
   }
 }
 
-// Delta[b, h, i] = sum_d dO[i, d] O[i, d] (fp32), one wave per 64 rows
-__global__ void k_attn_delta(const unsigned short* __restrict__ o, const unsigned short* __restrict__ dout, int n,
-                             int L, int heads, float* __restrict__ delta) {
-  const long row = (long)blockIdx.x * 256 + threadIdx.x;      // (b, h, i)
-  if (row >= (long)n * heads * L) return;
-  const int i = (int)(row % L);
-  const int h = (int)((row / L) % heads);
-  const int b = (int)(row / ((long)L * heads));
-  const long off = ((long)b * L + i) * heads * 32 + h * 32;
-  float s = 0.f;
+// Delta[b, h, i] = sum_j P_ij keep_ij dP_ij with exactly the P (fp32, rebuilt from lse) and dP
+// (dO V^T on the MFMA) the dS passes use, so every row of dS = P (keep dP - Delta) sums to zero up
+// to fp32 rounding -- as in the reference's autograd, where softmax's backward forms
+// sum_j P_ij dP_ij from its own P and dP (manifold_layers.py:417, fp32 under autocast).  The
+// FlashAttention shortcut Delta = dO . O (this file's kernel until round 6) takes O as STORED, in bf16, and
+// formed with bf16-rounded P: near-uniform attention (dP_ij ~ Delta_i for every key, the state at
+// init) turns that 2^-9 mismatch into a large relative error of dS, which the backward carries
+// through every earlier block (round 6: the ViT gradient groups at 2.8-3.6x the reference's own
+// bf16 error, tools/vit_grad_probe.py).  Wave = 16 queries, loop over 32-key tiles (the dQ
+// kernel's layout).
+__global__ void __launch_bounds__(256) k_attn_delta_pdp(const unsigned short* __restrict__ q,
+                                                        const unsigned short* __restrict__ k,
+                                                        const unsigned short* __restrict__ v,
+                                                        const unsigned short* __restrict__ dout,
+                                                        const float* __restrict__ lse, int L, int heads, float scale,
+                                                        float p, uint32_t seed, const unsigned int* soff,
+                                                        float* __restrict__ delta) {
+  seed = hv_seed(seed, soff);
+  const int b = blockIdx.z, h = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int D = heads * 32;
+  const int q0 = blockIdx.x * 64 + w * 16;
+  if (q0 >= L) return;
+  const long bh = (long)b * heads + h;
+  const unsigned short* kb = k + (long)b * L * D + h * 32;
+  const unsigned short* vb = v + (long)b * L * D + h * 32;
+  const int qi = q0 + fr;
+  const bool qval = qi < L;
+  const uint4 qf = rowfrag(q + (long)b * L * D + h * 32, min(qi, L - 1), D, fg);
+  const uint4 gf = rowfrag(dout + (long)b * L * D + h * 32, min(qi, L - 1), D, fg);
+  const float l2e = 1.4426950408889634f, sl2 = scale * l2e;
+  const float lq = qval ? lse[bh * L + qi] * l2e : 0.f;
+  const unsigned long long rbase = ((unsigned long long)(bh * L + qi)) * L;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < L; k0 += 32) {
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 s0 = mfma32(rowfrag(kb, min(k0 + fr, L - 1), D, fg), qf, z);
+    const f32x4 s1 = mfma32(rowfrag(kb, min(k0 + 16 + fr, L - 1), D, fg), qf, z);
+    const f32x4 g0 = mfma32(rowfrag(vb, min(k0 + fr, L - 1), D, fg), gf, z);
+    const f32x4 g1 = mfma32(rowfrag(vb, min(k0 + 16 + fr, L - 1), D, fg), gf, z);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint4 a = *reinterpret_cast<const uint4*>(o + off + c * 8);
-    const uint4 g = *reinterpret_cast<const uint4*>(dout + off + c * 8);
-    const unsigned short* av = reinterpret_cast<const unsigned short*>(&a);
-    const unsigned short* gv = reinterpret_cast<const unsigned short*>(&g);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s = fmaf(bf2f(av[e]), bf2f(gv[e]), s);
+    for (int j = 0; j < 8; ++j) {
+      const int key = k0 + (j < 4 ? 0 : 16) + fg * 4 + (j & 3);
+      if (qval && key < L) {
+        const float sv = j < 4 ? s0[j] : s1[j - 4];
+        const float gv = j < 4 ? g0[j] : g1[j - 4];
+        acc = fmaf(__builtin_amdgcn_exp2f(sv * sl2 - lq) * hv_drop_scale(seed, rbase + key, p), gv, acc);
+      }
+    }
   }
-  delta[row] = s;
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  if (qval && fg == 0) delta[bh * L + qi] = acc;
 }
 
 // dK, dV: wave = 16 keys (S = Q K^T layout: key in the lane column, 4 queries per lane row group),
@@ -452,9 +485,10 @@ extern "C" int hv_attention_backward_mfma(const void* q, const void* k, const vo
   k_tpad<<<tg, 256, 0, s>>>((const unsigned short*)q, L, Lp, heads, qt);
   k_tpad<<<tg, 256, 0, s>>>((const unsigned short*)k, L, Lp, heads, kt);
   k_tpad<<<tg, 256, 0, s>>>((const unsigned short*)dout, L, Lp, heads, dot);
-  k_attn_delta<<<hv_cdiv((long)n * heads * L, 256), 256, 0, s>>>((const unsigned short*)o,
-                                                                 (const unsigned short*)dout, n, L, heads, delta);
   const dim3 g(hv_cdiv(L, 64), heads, n);
+  k_attn_delta_pdp<<<g, 256, 0, s>>>((const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v,
+                                     (const unsigned short*)dout, lse, L, heads, sm_scale, drop_p, seed, seed_offset,
+                                     delta);
   k_attn_bwd_kv_mfma<<<g, 256, 0, s>>>((const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, qt,
                                        dot, (const unsigned short*)dout, lse, delta, L, Lp, heads, sm_scale, drop_p,
                                        seed, seed_offset, (unsigned short*)dk, (unsigned short*)dv);

@@ -23,10 +23,14 @@ from hv_amd.trainer import mhc_group  # noqa: E402
 
 
 def _patch(mode):
-    """Precision bisection: run one part of the ViT in fp32 inside the bf16 step."""
+    """Precision bisection: run one part of the ViT in fp32 inside the bf16 step.  Returns the undo."""
     from hv_amd import train_fn as TF
     from hv_amd import train_model as TM
     f32, b16 = torch.float32, torch.bfloat16
+    saved = (TF.AttentionFn.apply, TF.linear, TM.attention)
+
+    def undo():
+        TF.AttentionFn.apply, TF.linear, TM.attention = saved
     if mode == "attn32":                          # attention core (QK^T, softmax, PV and backward) in fp32
         orig = TF.AttentionFn.apply
 
@@ -58,6 +62,28 @@ def _patch(mode):
             o = TF.AttentionFn.apply(q, k, v, a.num_heads, p, TF.next_seed() if p > 0 else 0)
             return TM._mhc(a.out_proj, TF.CastFn.apply(o.reshape(n * L, -1), b16), H)
         TM.attention = att
+    return undo
+
+
+def bisect640(modes):
+    """Median over the 640 anchor batches (x seeds 7-11) of the ViT groups' bf16-vs-fp32 error, per
+    precision variant (bf16 step with one ViT part in fp32)."""
+    import numpy as np
+    from test_gpu_train import _group_norms
+    from oracle import cases
+    dev = torch.device("cuda:0")
+    res = {m: [] for m in ["base"] + modes}
+    for xs in (7,) + tuple(cases.TRAIN640_SEEDS):
+        g32 = _group_norms(_base_train_step(dev, "fp32", 2, 640, xs, 11)[2].items())
+        for m in res:
+            undos = [_patch(part) for part in m.split("+")] if m != "base" else []
+            g16 = _group_norms(_base_train_step(dev, "bf16", 2, 640, xs, 11)[2].items())
+            for u in reversed(undos):
+                u()
+            res[m].append({k: abs(g16[k] / v - 1) for k, v in g32.items() if k.startswith("vit")})
+            print(f"seed {xs} {m}: {({k: round(v, 4) for k, v in res[m][-1].items()})}", flush=True)
+    for m, rs in res.items():
+        print(f"MEDIAN {m}: {({k: round(float(np.median([r[k] for r in rs])), 4) for k in rs[0]})}", flush=True)
 
 
 def stream_ab():
@@ -94,6 +120,8 @@ def main():
         return stream_ab()
     if len(sys.argv) > 1 and sys.argv[1] == "determinism":
         return determinism()
+    if len(sys.argv) > 1 and sys.argv[1] == "bisect640":
+        return bisect640(sys.argv[2:])
     prefix = sys.argv[1] if len(sys.argv) > 1 else "vit_encoder"
     for mode in sys.argv[2:]:
         _patch(mode)
