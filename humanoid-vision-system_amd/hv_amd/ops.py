@@ -110,7 +110,8 @@ def _splitk(d, M: int, N: int, K: int, dtype: torch.dtype, device) -> Optional[T
     split over `splitk` workgroups (>= 4 K-tiles each); the last workgroup of a tile to finish
     sums the fp32 partials in slice order and runs the epilogue (deterministic).  Returns the workspace
     (kept alive by the caller until the launch is enqueued) or None."""
-    if not options().splitk or dtype != torch.bfloat16 or K % 64:
+    o = options()
+    if not (o.splitk or M <= o.splitk_small_m) or dtype != torch.bfloat16 or K % 64:
         return None
     tiles = -(-M // 64) * -(-N // 64)
     if tiles >= 192:

@@ -38,6 +38,7 @@ class HVOptions:
     prep_overlap_min_batch: int = 8   # ... and from this batch on (B=16: -0.9..-1.8 %; B=1 recompute: +0.7 %)
     direct_stem: bool = True          # MFMA stem conv straight from the NCHW image (hv_conv_stem)
     splitk: bool = False              # split-K for small output grids: measured no gain
+    splitk_small_m: int = 0           # ... but for GEMMs of at most this many rows (the 16-row final fusion)
     gemm_variant: int = 0             # hv_gemm_desc.variant for every GEMM (HV_GV_*), 0 = automatic
     mhc_variant: int = 0              # hv_mhc_fused_args.variant (HV_MV_*), 0 = automatic
     wgrad_variant: int = 0            # hv_wgrad_desc.variant for the weight gradients (HV_WV_*), 0 = automatic
