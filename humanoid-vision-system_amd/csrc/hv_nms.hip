@@ -2,22 +2,23 @@
 // non_max_suppression (reference yolo_head.py:571-731), the whole batch in two launches with no
 // host round trip per box (the reference does one .item() per kept box).
 //
-// Stage 1, one workgroup per (image, scale): candidates with class_score > conf_thr are
-// compacted (any order), sorted by score (descending, ties by flattened [A, H, W] index: the
-// keys are unique, so the order -- and every output -- is a function of the inputs alone), then
-// greedy NMS: the best remaining box is kept and every remaining box with IoU >= iou_thr (the
-// reference keeps IoU < thr) is suppressed, until max_det are kept or none remain.  Stage 2, one
-// workgroup per image: the same greedy NMS over the concatenation of the per-scale survivors
-// (scale 0 first, each in kept order), as the reference's final cross-scale pass.  IoU is
-// computed exactly as compute_iou (yolo_head.py:733-750): inter / (area1 + area2 - inter + 1e-6).
+// Stage 1, one workgroup per (image, scale): candidates with class_score > conf_thr, sorted by
+// score exactly as the reference's torch.sort leaves them (below), then greedy NMS: the best
+// remaining box is kept and every remaining box with IoU >= iou_thr (the reference keeps
+// IoU < thr) is suppressed, until max_det are kept or none remain.  Stage 2, one workgroup per
+// image: the same over the concatenation of the per-scale survivors (scale 0 first, each in kept
+// order), the reference's final cross-scale pass.  IoU exactly as compute_iou
+// (yolo_head.py:733-750): inter / (area1 + area2 - inter + 1e-6).
 //
-// Any candidate count and any max_det (the reference has no cap): up to NMS_CAP candidates a
-// segment is sorted in LDS; past that its candidates go to a workspace region and are sorted by
-// a bitonic network whose stages with partner distance < NMS_CAP run chunk-wise in LDS and only
-// the wider ones stream through global memory (coherent within the workgroup across its
-// barriers).  Suppressed candidates are marked in place (the index's sign bit), and the sweep
-// that suppresses also finds the next survivor (one barrier per kept box).  Kept boxes are
-// written as they are found, so max_det bounds nothing but the output rows.
+// The order.  Up to NMS_CAP candidates are compacted into LDS (any order) and bitonic-sorted by
+// (score, index); with no two scores equal that is the only sorted order, so it is the
+// reference's.  With ties, or more than NMS_CAP candidates, the reference's UNSTABLE order is
+// rebuilt: the candidates in cell order go through a restatement of libstdc++'s introsort
+// (exact_sort below) -- only over the prefix the greedy reads, widened 4x whenever the greedy
+// runs off it before max_det.  The greedy reads the prefix from LDS when it fits.  Suppressed
+// candidates are marked in place (the index's sign bit) and the sweep that suppresses also finds
+// the next survivor (one barrier per kept box).  Kept boxes are written as they are found, so
+// neither the candidate count nor max_det has a cap.
 #include "hv_common.h"
 #include <climits>
 
@@ -26,6 +27,7 @@ namespace {
 constexpr int NMS_CAP = 8192;       // candidates sorted in LDS per segment (64 KiB)
 constexpr int NMS_THREADS = 1024;
 constexpr int NMS_DEAD = INT_MIN;   // sign bit of Cand::idx: suppressed
+constexpr int NMS_PREFIX0 = 2048;   // first prefix of the exact sort the greedy reads (widened 4x)
 
 struct Cand {
   float score;
@@ -67,55 +69,6 @@ __device__ void lds_sort(Cand* c, int n) {
         const int l = i ^ j;
         if (l > i) cmpx(c, i, l, (i & k) == 0);
       }
-      __syncthreads();
-    }
-  }
-}
-
-// bitonic sort of g[0..n) (global workspace, n > NMS_CAP, room for pow2ceil(n)), best first.
-// `s` is an NMS_CAP LDS scratch.  The network is the usual one over m = pow2ceil(n) elements;
-// every stage with partner distance j < NMS_CAP stays inside one aligned NMS_CAP chunk and runs
-// in LDS (direction bit k of the GLOBAL index), only j >= NMS_CAP passes touch global memory.
-__device__ void global_sort(Cand* g, int n, Cand* s) {
-  const int m = pow2ceil(n);
-  for (int i = n + threadIdx.x; i < m; i += blockDim.x) g[i] = Cand{-INFINITY, INT_MAX};
-  __syncthreads();
-  // every chunk through all stages k <= NMS_CAP
-  for (int base = 0; base < m; base += NMS_CAP) {
-    for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) s[i] = g[base + i];
-    __syncthreads();
-    for (int k = 2; k <= NMS_CAP; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) {
-          const int l = i ^ j;
-          if (l > i) cmpx(s, i, l, ((base + i) & k) == 0);
-        }
-        __syncthreads();
-      }
-    }
-    for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) g[base + i] = s[i];
-    __syncthreads();
-  }
-  for (int k = 2 * NMS_CAP; k <= m; k <<= 1) {
-    for (int j = k >> 1; j >= NMS_CAP; j >>= 1) {
-      for (int p = threadIdx.x; p < (m >> 1); p += blockDim.x) {
-        const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));    // p with a zero inserted at bit j
-        cmpx(g, i, i | j, (i & k) == 0);
-      }
-      __syncthreads();
-    }
-    for (int base = 0; base < m; base += NMS_CAP) {
-      const bool desc = (base & k) == 0;                           // constant over the chunk
-      for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) s[i] = g[base + i];
-      __syncthreads();
-      for (int j = NMS_CAP >> 1; j > 0; j >>= 1) {
-        for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) {
-          const int l = i ^ j;
-          if (l > i) cmpx(s, i, l, desc);
-        }
-        __syncthreads();
-      }
-      for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) g[base + i] = s[i];
       __syncthreads();
     }
   }
@@ -244,38 +197,46 @@ __device__ int block_excl_scan(int v, int* total) {
   return r;
 }
 
-// A[0..n) (global) in its ORIGINAL order -> std::sort's permutation.  depth < 0: std::sort's own
+// A[0..n) (global) in its ORIGINAL order -> std::sort's permutation of positions [0, limit): a
+// segment lying wholly at or past `limit` is never partitioned further (what std::sort does there
+// cannot move anything into the prefix: every element left of a cut is >= every element right of
+// it), so the greedy NMS -- which reads the sorted order front to back and usually stops at
+// max_det long before the end -- only pays for the top levels over all n plus the prefix.  Each
+// level sweeps [0, end) with end = the last active segment's bound.  depth < 0: std::sort's own
 // limit 2 * floor(log2 n); otherwise forced (tests reach the heap-sort fallback with it).
-__device__ void exact_sort(Cand* A, int n, const XWork w, int depth) {
-  __shared__ int s_any;
+__device__ void exact_sort(Cand* A, int n, const XWork w, int depth, int limit) {
+  __shared__ int s_any, s_end;
   const int T = blockDim.x, t = threadIdx.x;
   if (depth < 0) depth = n > 0 ? 2 * (31 - __clz(n)) : 0;
   for (int i = t; i < n; i += T) { w.lo[i] = 0; w.hi[i] = n; }
-  if (t == 0) { w.SR[n] = 0; s_any = n > 16; }
+  if (t == 0) { s_any = n > 16 && limit > 0; s_end = n; }
   __syncthreads();
-  const int C = (n + T - 1) / T;
-  const int c0 = min(n, t * C), c1 = min(n, c0 + C);
   while (s_any) {
-    __syncthreads();                     // every thread has read s_any
+    const int E = s_end;                 // positions past E belong to no active segment
+    __syncthreads();                     // every thread has read s_any / s_end
+    auto active = [&](int l, int h) { return h - l > 16 && l < limit; };
     if (depth == 0) {
-      for (int i = t; i < n; i += T) {
+      for (int i = t; i < E; i += T) {
         const int l = w.lo[i], h = w.hi[i];
-        if (l == i && h - l > 16) heap_sort(A + l, h - l);
+        if (l == i && active(l, h)) heap_sort(A + l, h - l);
       }
       __syncthreads();
       break;
     }
     --depth;
-    for (int i = t; i < n; i += T) {     // pivots: __unguarded_partition_pivot
+    for (int i = t; i < E; i += T) {     // pivots: __unguarded_partition_pivot
       const int l = w.lo[i], h = w.hi[i];
-      if (l == i && h - l > 16) median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
+      if (l == i && active(l, h)) median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
     }
+    if (t == 0) w.SR[E] = 0;
     __syncthreads();
+    const int C = (E + T - 1) / T;
+    const int c0 = min(E, t * C), c1 = min(E, c0 + C);
     int cL = 0, cR = 0;                  // stopper flags over this thread's chunk
     for (int i = c0; i < c1; ++i) {
       const int l = w.lo[i], h = w.hi[i];
       int f = 0;
-      if (h - l > 16 && i > l) {
+      if (active(l, h) && i > l) {
         const float p = A[l].score, v = A[i].score;
         f = (!(v > p) ? 1 : 0) | (!(p > v) ? 2 : 0);
       }
@@ -288,10 +249,10 @@ __device__ void exact_sort(Cand* A, int n, const XWork w, int depth) {
     const int exR = block_excl_scan(cR, &totR);
     int run = exL;                       // PL[i] = left stoppers in [0, i]
     for (int i = c0; i < c1; ++i) { run += w.fl[i] & 1; w.PL[i] = run; }
-    run = totR - exR - cR;               // SR[i] = right stoppers in [i, n)
+    run = totR - exR - cR;               // SR[i] = right stoppers in [i, E)
     for (int i = c1 - 1; i >= c0; --i) { run += w.fl[i] >> 1; w.SR[i] = run; }
     __syncthreads();
-    for (int i = t; i < n; i += T) {     // l_k, r_k by rank within the segment
+    for (int i = t; i < E; i += T) {     // l_k, r_k by rank within the segment
       const int f = w.fl[i];
       if (!f) continue;
       const int l = w.lo[i], h = w.hi[i];
@@ -299,7 +260,7 @@ __device__ void exact_sort(Cand* A, int n, const XWork w, int depth) {
       if (f & 2) w.Rp[l + w.SR[i] - w.SR[h]] = i;
     }
     __syncthreads();
-    for (int i = t; i < n; i += T) {     // the swaps (disjoint pairs) and each segment's cut
+    for (int i = t; i < E; i += T) {     // the swaps (disjoint pairs) and each segment's cut
       if (!(w.fl[i] & 1)) continue;
       const int l = w.lo[i], h = w.hi[i];
       const int k = w.PL[i] - w.PL[l];
@@ -313,20 +274,24 @@ __device__ void exact_sort(Cand* A, int n, const XWork w, int depth) {
         w.cut[l] = i;                    // no swap at all: cut = l_1
       }
     }
-    if (t == 0) s_any = 0;
+    if (t == 0) { s_any = 0; s_end = 0; }
     __syncthreads();
-    for (int i = t; i < n; i += T) {     // [first, cut) and [cut, last), one level deeper
+    for (int i = t; i < E; i += T) {     // [first, cut) and [cut, last), one level deeper
       const int l = w.lo[i], h = w.hi[i];
-      if (h - l <= 16) continue;
+      if (!active(l, h)) continue;
       const int c = w.cut[l];
       const int nl = i < c ? l : c, nh = i < c ? c : h;
       w.lo[i] = nl;
       w.hi[i] = nh;
-      if (nh - nl > 16) s_any = 1;
+      if (i == nl && active(nl, nh)) {   // one thread per new active segment
+        s_any = 1;
+        atomicMax(&s_end, nh);
+      }
     }
     __syncthreads();
   }
-  for (int i = t; i < n; i += T) {       // __final_insertion_sort = stable sort of every leaf
+  const int P = min(n, limit);
+  for (int i = t; i < P; i += T) {       // __final_insertion_sort = stable sort of every leaf
     const int l = w.lo[i], h = w.hi[i];
     if (l == i && h - l <= 16) insertion_sort(A + l, h - l);
   }
@@ -406,42 +371,53 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_scale(const hv_nms_scale* _
   }
   __syncthreads();
   const int n = min(s_n, cap);
-  bool in_lds = n <= NMS_CAP;
-  if (in_lds) {
-    lds_sort(c, n);
-  } else {
-    for (int i = threadIdx.x; i < NMS_CAP; i += blockDim.x) g[i] = c[i];
-    __syncthreads();
-    global_sort(g, n, c);
-  }
-  if (has_ties(in_lds ? c : g, n)) {
-    // the reference's tie order: rebuild the masked candidates in cell order, then std::sort
-    const long C = (cells + blockDim.x - 1) / blockDim.x;
-    const long c0 = min(cells, (long)threadIdx.x * C), c1 = min(cells, c0 + C);
-    int cnt = 0;
-    for (long i = c0; i < c1; ++i) cnt += score[i] > conf_thr;
-    int tot;
-    int o = block_excl_scan(cnt, &tot);
-    for (long i = c0; i < c1; ++i) {
-      const float v = score[i];
-      if (v > conf_thr && o < cap) g[o] = Cand{v, (int)i};
-      o += v > conf_thr;
-    }
-    __syncthreads();
-    exact_sort(g, n, xwork_at(gx + seg * XWORK_ARRAYS * (seg_stride + 1), seg_stride + 1), -1);
-    in_lds = false;
-  }
   const float4* boxes = reinterpret_cast<const float4*>(S.boxes) + (long)b * cells;
   const int64_t* lab = S.class_indices + (long)b * cells;
   auto box = [&](int id) { return boxes[id]; };
-  Cand* src = in_lds ? c : g;
-  auto emit = [&](int k, int pos) {
-    const Cand e = src[pos];
-    reinterpret_cast<float4*>(sboxes)[seg * max_det + k] = boxes[e.idx];
-    sscores[seg * max_det + k] = e.score;
-    slabels[seg * max_det + k] = lab[e.idx];
+  auto emit_from = [&](const Cand* src) {
+    return [=](int k, int pos) {
+      const Cand e = src[pos];
+      reinterpret_cast<float4*>(sboxes)[seg * max_det + k] = boxes[e.idx];
+      sscores[seg * max_det + k] = e.score;
+      slabels[seg * max_det + k] = lab[e.idx];
+    };
   };
-  const int kept = in_lds ? greedy(c, n, iou_thr, max_det, box, emit) : greedy(g, n, iou_thr, max_det, box, emit);
+  int kept = 0;
+  bool exact = n > NMS_CAP;                // past the LDS: std::sort's order straight away
+  if (!exact) {
+    lds_sort(c, n);
+    exact = has_ties(c, n);                // distinct scores: the one sorted order is the reference's
+    if (!exact) kept = greedy(c, n, iou_thr, max_det, box, emit_from(c));
+  }
+  if (exact) {
+    // the reference's order (ties included): the masked candidates in cell order, std::sort
+    // restated over the prefix the greedy reads; a greedy that runs off the prefix before
+    // max_det widens it 4x and starts over (deterministic)
+    const XWork xw = xwork_at(gx + seg * XWORK_ARRAYS * (seg_stride + 1), seg_stride + 1);
+    for (int limit = min(n, NMS_PREFIX0);; limit = min(n, 4 * limit)) {
+      const long C = (cells + blockDim.x - 1) / blockDim.x;
+      const long c0 = min(cells, (long)threadIdx.x * C), c1 = min(cells, c0 + C);
+      int cnt = 0;
+      for (long i = c0; i < c1; ++i) cnt += score[i] > conf_thr;
+      int tot;
+      int o = block_excl_scan(cnt, &tot);
+      for (long i = c0; i < c1; ++i) {
+        const float v = score[i];
+        if (v > conf_thr && o < cap) g[o] = Cand{v, (int)i};
+        o += v > conf_thr;
+      }
+      __syncthreads();
+      exact_sort(g, n, xw, -1, limit);
+      if (limit <= NMS_CAP) {              // the greedy reads the prefix from LDS
+        for (int i = threadIdx.x; i < limit; i += blockDim.x) c[i] = g[i];
+        __syncthreads();
+        kept = greedy(c, limit, iou_thr, max_det, box, emit_from(c));
+      } else {
+        kept = greedy(g, limit, iou_thr, max_det, box, emit_from(g));
+      }
+      if (kept >= max_det || limit == n) break;
+    }
+  }
   if (threadIdx.x == 0) scount[seg] = kept;
 }
 
@@ -469,30 +445,40 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_final(int nscales, float io
     }
     __syncthreads();
   };
-  bool in_lds = n <= NMS_CAP;
-  if (in_lds) {
-    gather(c);
-    lds_sort(c, n);       // idx grows with the concatenation order: ties keep it (stable sort)
-  } else {
-    gather(g);
-    global_sort(g, n, c);
-  }
-  if (has_ties(in_lds ? c : g, n)) {
-    gather(g);
-    exact_sort(g, n, xwork_at(gx + (long)b * XWORK_ARRAYS * (img_stride + 1), img_stride + 1), -1);
-    in_lds = false;
-  }
   const float4* sb = reinterpret_cast<const float4*>(sboxes);
   auto box = [&](int id) { return sb[id]; };
   float4* ob = reinterpret_cast<float4*>(boxes) + (long)b * max_det;
-  Cand* src = in_lds ? c : g;
-  auto emit = [&](int k, int pos) {
-    const int from = src[pos].idx;
-    ob[k] = sb[from];
-    scores[(long)b * max_det + k] = sscores[from];
-    labels[(long)b * max_det + k] = slabels[from];
+  auto emit_from = [&](const Cand* src) {
+    return [=](int k, int pos) {
+      const int from = src[pos].idx;
+      ob[k] = sb[from];
+      scores[(long)b * max_det + k] = sscores[from];
+      labels[(long)b * max_det + k] = slabels[from];
+    };
   };
-  const int kept = in_lds ? greedy(c, n, iou_thr, max_det, box, emit) : greedy(g, n, iou_thr, max_det, box, emit);
+  int kept = 0;
+  bool exact = n > NMS_CAP;
+  if (!exact) {
+    gather(c);
+    lds_sort(c, n);       // idx grows with the concatenation order
+    exact = has_ties(c, n);
+    if (!exact) kept = greedy(c, n, iou_thr, max_det, box, emit_from(c));
+  }
+  if (exact) {            // as stage 1: std::sort's order over the prefix the greedy reads
+    const XWork xw = xwork_at(gx + (long)b * XWORK_ARRAYS * (img_stride + 1), img_stride + 1);
+    for (int limit = min(n, NMS_PREFIX0);; limit = min(n, 4 * limit)) {
+      gather(g);
+      exact_sort(g, n, xw, -1, limit);
+      if (limit <= NMS_CAP) {
+        for (int i = threadIdx.x; i < limit; i += blockDim.x) c[i] = g[i];
+        __syncthreads();
+        kept = greedy(c, limit, iou_thr, max_det, box, emit_from(c));
+      } else {
+        kept = greedy(g, limit, iou_thr, max_det, box, emit_from(g));
+      }
+      if (kept >= max_det || limit == n) break;
+    }
+  }
   // rows past `count` are zero, so the fixed-size outputs are a function of the inputs alone
   for (int k = kept + threadIdx.x; k < max_det; k += blockDim.x) {
     ob[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -507,7 +493,7 @@ __global__ void __launch_bounds__(NMS_THREADS) k_sort_desc_exact(const float* va
                                                                  Cand* A, int* gx) {
   for (int i = threadIdx.x; i < n; i += blockDim.x) A[i] = Cand{vals[i], i};
   __syncthreads();
-  exact_sort(A, n, xwork_at(gx, (long)n + 1), depth);
+  exact_sort(A, n, xwork_at(gx, (long)n + 1), depth, n);
   for (int i = threadIdx.x; i < n; i += blockDim.x) out_idx[i] = A[i].idx;
 }
 

@@ -16,6 +16,7 @@ for step in "$@"; do
     preptime) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/preptime -o run --output-format csv -- python tools/prep_time.py > $OUT/preptime.log 2>&1 || { tail -30 $OUT/preptime.log; exit 1; } ; f=$(find $OUT/preptime -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 32 20 > $OUT/preptime_summary.txt; head -14 $OUT/preptime_summary.txt ;;
     sweep) timeout -k 10 400 python -u tools/tile_sweep.py > $OUT/tile_sweep.txt 2>&1 || { tail -30 $OUT/tile_sweep.txt; exit 1; } ; cat $OUT/tile_sweep.txt ;;
     bisect640) timeout -k 10 900 python -u tools/vit_grad_probe.py bisect640 attn32+lin32+qkv32 > $OUT/bisect640.txt 2>&1 || { tail -30 $OUT/bisect640.txt; exit 1; } ; grep MEDIAN $OUT/bisect640.txt ;;
+    nmstime) timeout -k 10 300 python -u tools/nms_time.py 1 > $OUT/nms_time.txt 2>&1 && timeout -k 10 300 python -u tools/nms_time.py 16 >> $OUT/nms_time.txt 2>&1 || { tail -30 $OUT/nms_time.txt; exit 1; } ; grep -v amdgpu.ids $OUT/nms_time.txt ;;
     vitbisect) for m in attn32 lin32 qkv32; do timeout -k 10 300 python -u tools/vit_grad_probe.py vit_encoder $m > $OUT/vit_grad_probe_$m.txt 2>&1 || { tail -30 $OUT/vit_grad_probe_$m.txt; exit 1; } ; grep "==" $OUT/vit_grad_probe_$m.txt ; done ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -30 $OUT/smoke.log; exit 1; } ; tail -2 $OUT/smoke.log ;;
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
