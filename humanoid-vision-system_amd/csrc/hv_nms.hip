@@ -10,24 +10,27 @@
 // order), the reference's final cross-scale pass.  IoU exactly as compute_iou
 // (yolo_head.py:733-750): inter / (area1 + area2 - inter + 1e-6).
 //
-// The order.  Up to NMS_CAP candidates are compacted into LDS (any order) and bitonic-sorted by
-// (score, index); with no two scores equal that is the only sorted order, so it is the
-// reference's.  With ties, or more than NMS_CAP candidates, the reference's UNSTABLE order is
-// rebuilt: the candidates in cell order go through a restatement of libstdc++'s introsort
-// (exact_sort below) -- only over the prefix the greedy reads, widened 4x whenever the greedy
-// runs off it before max_det.  The greedy reads the prefix from LDS when it fits.  Suppressed
-// candidates are marked in place (the index's sign bit) and the sweep that suppresses also finds
-// the next survivor (one barrier per kept box).  Kept boxes are written as they are found, so
-// neither the candidate count nor max_det has a cap.
+// The order.  Up to NMS_BITONIC candidates are compacted into LDS (any order) and bitonic-sorted
+// by (score, index); with no two scores equal that is the only sorted order, so it is the
+// reference's.  With ties, or more candidates, the reference's UNSTABLE order is rebuilt: the
+// candidates in cell order go through a restatement of libstdc++'s introsort (exact_sort below)
+// -- only over the prefix the greedy reads (NMS_PREFIX0, widened 4x whenever the greedy runs off
+// it before max_det), and in LDS once the segments meeting that prefix fit there.  The greedy
+// decides 64 candidates per step from an IoU bit matrix (greedy below), reading boxes from an
+// LDS cache; suppressed candidates are marked in place (the index's sign bit) and the kept ones
+// are written out at the end in parallel.  Neither the candidate count nor max_det has a cap.
 #include "hv_common.h"
 #include <climits>
 
 namespace {
 
-constexpr int NMS_CAP = 8192;       // candidates sorted in LDS per segment (64 KiB)
+constexpr int NMS_CAP = 6144;       // candidates held in LDS per segment (48 KiB): the exact sort's
+                                    // window and the greedy's prefix when it fits
 constexpr int NMS_THREADS = 1024;
 constexpr int NMS_DEAD = INT_MIN;   // sign bit of Cand::idx: suppressed
-constexpr int NMS_PREFIX0 = 2048;   // first prefix of the exact sort the greedy reads (widened 4x)
+constexpr int NMS_PREFIX0 = 1024;   // first prefix of the exact sort the greedy reads (widened 4x)
+constexpr int NMS_XL = 6144;        // exact-sort window (and greedy box cache) held in LDS
+constexpr int NMS_BITONIC = 2048;   // above: straight to the exact sort (as fast, and bf16 scores tie)
 
 struct Cand {
   float score;
@@ -58,7 +61,7 @@ __device__ __forceinline__ void cmpx(Cand* c, int i, int l, bool desc) {
   if (desc ? better(b, a) : better(a, b)) { c[i] = b; c[l] = a; }
 }
 
-// bitonic sort of c[0..n) in LDS (n <= NMS_CAP), best first; pads to a power of two
+// bitonic sort of c[0..n) in LDS (n <= NMS_BITONIC), best first; pads to a power of two
 __device__ void lds_sort(Cand* c, int n) {
   const int m = pow2ceil(n);
   for (int i = n + threadIdx.x; i < m; i += blockDim.x) c[i] = Cand{-INFINITY, INT_MAX};
@@ -93,15 +96,21 @@ __device__ void lds_sort(Cand* c, int n) {
 //  * __final_insertion_sort over the whole array only reorders within the <= 16-element leaves
 //    (nothing on the right of a cut is strictly better than anything on its left), so it is a
 //    stable insertion sort per leaf, one thread per leaf.
-// All arrays live in the workspace (global memory, coherent within the workgroup across its
-// barriers).
-struct XWork {
-  int *lo, *hi, *PL, *SR, *Lp, *Rp, *cut, *fl;   // each >= n + 1 ints
+// The arrays live in the workspace (global memory, coherent within the workgroup across its
+// barriers) while the segments that meet the prefix span more than NMS_XL positions; from then on
+// that window moves to LDS (A into the candidate array, the index arrays as 16-bit) and the
+// remaining levels -- most of them -- run there.
+template <typename I>
+struct XW {
+  I *lo, *hi, *PL, *SR, *Lp, *Rp, *cut, *fl;   // each >= window + 1 entries
 };
+using u16 = unsigned short;
+using XWork = XW<int>;
 constexpr int XWORK_ARRAYS = 8;
 
-__device__ __forceinline__ XWork xwork_at(int* base, long stride) {
-  XWork w;
+template <typename I>
+__device__ __forceinline__ XW<I> xw_at(I* base, long stride) {
+  XW<I> w;
   w.lo = base; w.hi = base + stride; w.PL = base + 2 * stride; w.SR = base + 3 * stride;
   w.Lp = base + 4 * stride; w.Rp = base + 5 * stride; w.cut = base + 6 * stride; w.fl = base + 7 * stride;
   return w;
@@ -174,128 +183,289 @@ __device__ void insertion_sort(Cand* F, int len) {
   }
 }
 
-// exclusive scan of one int per thread in thread order; *total = the sum
-__device__ int block_excl_scan(int v, int* total) {
-  __shared__ int s_w[NMS_THREADS / 64 + 1];
+// exclusive scan of one value per thread in thread order; *total = the sum.  Two counts travel
+// packed in one 64-bit value (low and high 32 bits), one scan for both.  One barrier: the wave
+// totals alternate between two buffers by the caller's call counter `ph` (uniform over the
+// workgroup), so a call never overwrites what a slow wave may still read from the previous one.
+__device__ long long block_excl_scan(long long v, long long* total, int& ph) {
+  __shared__ long long s_w[2][NMS_THREADS / 64];
+  long long* sw = s_w[ph & 1];
+  ++ph;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  int x = v;
+  long long x = v;
   for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
+    const long long y = __shfl_up(x, o);
     if (lane >= o) x += y;
   }
-  if (lane == 63) s_w[wv] = x;
+  if (lane == 63) sw[wv] = x;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < nw; ++i) { const int t = s_w[i]; s_w[i] = acc; acc += t; }
-    s_w[nw] = acc;
+  long long before = 0, all = 0;
+  for (int i = 0; i < nw; ++i) {
+    const long long t = sw[i];
+    before += i < wv ? t : 0;
+    all += t;
+  }
+  *total = all;
+  return before + x - v;
+}
+
+// Each segment carries its own std::sort depth budget, kept at Lp[head] (Lp[l + k] is written
+// for k >= 1 only); X_DONE marks a segment the heap-sort fallback has finished.
+template <typename I>
+__device__ __forceinline__ I x_done() { return (I)~(I)0; }
+
+template <typename I>
+__device__ __forceinline__ bool x_active(int l, int h, int limit, I d) {
+  return h - l > 16 && l < limit && d != x_done<I>();
+}
+
+// one recursion level: every active segment of A[0, E) partitioned at once (see above); a segment
+// whose budget is spent is heap-sorted instead (std::__partial_sort).  The split leaves s_any =
+// "an active segment remains" and s_end = the last one's end (the caller alternates two pairs of
+// them between levels, so the level never waits for their readers).
+template <typename I>
+__device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, int& s_any, int& s_end, int& ph) {
+  const int T = blockDim.x, t = threadIdx.x;
+  // distinct arrays: lets the compiler batch the loads of consecutive elements
+  I* __restrict__ lo = w.lo; I* __restrict__ hi = w.hi; I* __restrict__ PL = w.PL; I* __restrict__ SR = w.SR;
+  I* __restrict__ Lp = w.Lp; I* __restrict__ Rp = w.Rp; I* __restrict__ cut = w.cut; I* __restrict__ fl = w.fl;
+  for (int i = t; i < E; i += T) {       // pivots: __unguarded_partition_pivot (or the heap sort)
+    const int l = lo[i], h = hi[i];
+    if (l != i) continue;
+    const I d = Lp[l];
+    if (!x_active(l, h, limit, d)) continue;
+    if (d == 0) {
+      heap_sort(A + l, h - l);
+      Lp[l] = x_done<I>();
+    } else {
+      median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
+    }
+  }
+  if (t == 0) SR[E] = 0;
+  __syncthreads();
+  const int C = (E + T - 1) / T;
+  const int c0 = min(E, t * C), c1 = min(E, c0 + C);
+  int cL = 0, cR = 0;                    // stopper flags over this thread's chunk
+#pragma unroll 4
+  for (int i = c0; i < c1; ++i) {
+    const int l = lo[i], h = hi[i];
+    int f = 0;
+    if (i > l && x_active(l, h, limit, Lp[l])) {
+      const float p = A[l].score, v = A[i].score;
+      f = (!(v > p) ? 1 : 0) | (!(p > v) ? 2 : 0);
+    }
+    fl[i] = f;
+    cL += f & 1;
+    cR += f >> 1;
+  }
+  long long tot2;
+  const long long ex2 = block_excl_scan((long long)cL | ((long long)cR << 32), &tot2, ph);
+  const int exL = (int)(ex2 & 0xffffffffLL), exR = (int)(ex2 >> 32), totR = (int)(tot2 >> 32);
+  int run = exL;                         // PL[i] = left stoppers in [0, i]
+#pragma unroll 4
+  for (int i = c0; i < c1; ++i) { run += fl[i] & 1; PL[i] = run; }
+  run = totR - exR - cR;                 // SR[i] = right stoppers in [i, E)
+#pragma unroll 4
+  for (int i = c1 - 1; i >= c0; --i) { run += fl[i] >> 1; SR[i] = run; }
+  __syncthreads();
+  for (int i = t; i < E; i += T) {       // l_k, r_k by rank within the segment
+    const int f = fl[i];
+    if (!f) continue;
+    const int l = lo[i], h = hi[i];
+    if (f & 1) Lp[l + PL[i] - PL[l]] = i;
+    if (f & 2) Rp[l + SR[i] - SR[h]] = i;
   }
   __syncthreads();
-  const int r = s_w[wv] + x - v;
-  *total = s_w[nw];
-  __syncthreads();                       // s_w is reused by the next call
-  return r;
+  for (int i = t; i < E; i += T) {       // the swaps (disjoint pairs) and each segment's cut
+    if (!(fl[i] & 1)) continue;
+    const int l = lo[i], h = hi[i];
+    const int k = PL[i] - PL[l];
+    const int cntL = PL[h - 1] - PL[l], cntR = SR[l + 1] - SR[h];
+    const int r = k <= cntR ? (int)Rp[l + k] : -1;
+    int ct = -1;
+    if (r > i) {
+      xswap(A, i, r);
+      const bool next = k + 1 <= cntL && k + 1 <= cntR && Lp[l + k + 1] < Rp[l + k + 1];
+      if (!next) ct = k + 1 <= cntL ? min((int)Lp[l + k + 1], r) : r;
+    } else if (k == 1) {
+      ct = i;                            // no swap at all: cut = l_1
+    }
+    if (ct >= 0) {
+      cut[l] = ct;
+      Rp[l] = Lp[l] - 1;                 // the children's budget (Rp[l + k]: k >= 1 only)
+    }
+  }
+  if (t == 0) { s_any = 0; s_end = 0; }
+  __syncthreads();
+  for (int i = t; i < E; i += T) {       // [first, cut) and [cut, last), one level deeper
+    const int l = lo[i], h = hi[i];
+    if (!x_active(l, h, limit, Lp[l])) continue;   // Lp[l] may already be the child's: same test
+    const int c = cut[l];
+    const int nl = i < c ? l : c, nh = i < c ? c : h;
+    lo[i] = nl;
+    hi[i] = nh;
+    if (i == nl) {                       // one thread per new segment
+      const I d = Rp[l];
+      Lp[nl] = d;
+      if (x_active(nl, nh, limit, d)) {
+        s_any = 1;
+        atomicMax(&s_end, nh);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// __final_insertion_sort = a stable sort of every leaf meeting the prefix [0, P)
+template <typename I>
+__device__ void x_leaves(Cand* A, const XW<I> w, int P) {
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const int l = w.lo[i], h = w.hi[i];
+    if (l == i && h - l <= 16) insertion_sort(A + l, h - l);
+  }
+  __syncthreads();
+}
+
+// Hoare partition of the ONE segment A[l, h) (global) with all threads: the straddler phase of
+// exact_sort.  Waves own contiguous runs of 64-position rounds (coalesced), stopper ranks come
+// from ballots plus one scan of the wave totals, and the k-th pair is read by rank (coalesced).
+// Returns the cut (std::__unguarded_partition_pivot).
+__device__ int x_partition1(Cand* __restrict__ A, int l, int h, const XWork w, int& ph) {
+  __shared__ int s_cut;
+  const int T = blockDim.x, t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = T >> 6;
+  int* __restrict__ Lp = w.Lp;
+  int* __restrict__ Rp = w.Rp;
+  if (t == 0) median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
+  __syncthreads();
+  const float p = A[l].score;
+  const int rounds = (h - l - 1 + 63) >> 6, rpw = (rounds + nw - 1) / nw;
+  const int r0 = min(rounds, wv * rpw), r1 = min(rounds, r0 + rpw);
+  const unsigned long long below = (1ull << lane) - 1;
+  int cL = 0, cR = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int i = l + 1 + (r << 6) + lane;
+    bool fL = false, fR = false;
+    if (i < h) { const float v = A[i].score; fL = !(v > p); fR = !(p > v); }
+    cL += __popcll(__ballot(fL));
+    cR += __popcll(__ballot(fR));
+  }
+  long long tot;                         // lane 63 carries its wave's counts: every lane gets the
+  const long long ex = block_excl_scan(lane == 63 ? (long long)cL | ((long long)cR << 32) : 0, &tot, ph);
+  int bL = (int)(ex & 0xffffffffLL), bR = (int)(ex >> 32);   // ... counts of the waves before it
+  const int totL = (int)(tot & 0xffffffffLL), totR = (int)(tot >> 32);
+  for (int r = r0; r < r1; ++r) {
+    const int i = l + 1 + (r << 6) + lane;
+    bool fL = false, fR = false;
+    if (i < h) { const float v = A[i].score; fL = !(v > p); fR = !(p > v); }
+    const unsigned long long mL = __ballot(fL), mR = __ballot(fR);
+    if (fL) Lp[1 + bL + __popcll(mL & below)] = i;          // k-th left stopper from the left
+    if (fR) Rp[totR - bR - __popcll(mR & below)] = i;       // k-th right stopper from the right
+    bL += __popcll(mL);
+    bR += __popcll(mR);
+  }
+  __syncthreads();
+  for (int k = 1 + t; k <= totL; k += T) {
+    const int i = Lp[k];
+    const int r = k <= totR ? Rp[k] : -1;
+    if (r > i) {
+      xswap(A, i, r);
+      const bool next = k + 1 <= totL && k + 1 <= totR && Lp[k + 1] < Rp[k + 1];
+      if (!next) s_cut = k + 1 <= totL ? min(Lp[k + 1], r) : r;
+    } else if (k == 1) {
+      s_cut = i;
+    }
+  }
+  __syncthreads();
+  return s_cut;
 }
 
 // A[0..n) (global) in its ORIGINAL order -> std::sort's permutation of positions [0, limit): a
 // segment lying wholly at or past `limit` is never partitioned further (what std::sort does there
 // cannot move anything into the prefix: every element left of a cut is >= every element right of
 // it), so the greedy NMS -- which reads the sorted order front to back and usually stops at
-// max_det long before the end -- only pays for the top levels over all n plus the prefix.  Each
-// level sweeps [0, end) with end = the last active segment's bound.  depth < 0: std::sort's own
-// limit 2 * floor(log2 n); otherwise forced (tests reach the heap-sort fallback with it).
-__device__ void exact_sort(Cand* A, int n, const XWork w, int depth, int limit) {
-  __shared__ int s_any, s_end;
+// max_det long before the end -- only pays for the top levels over all n plus the prefix.
+// Segments are independent, each with its own depth budget, so the order they are partitioned
+// in does not matter:
+//  * straddler phase (n > NMS_XL >= limit): only the segment holding position limit-1 is
+//    partitioned while it reaches past NMS_XL; the pieces left of it wait in a list;
+//  * then every segment meeting the prefix is partitioned level-synchronously, in LDS (c and wl)
+//    once they all lie in [0, NMS_XL), in the workspace before that.
+// Returns true when the sorted prefix is in c, false when it is in A.  depth < 0: std::sort's
+// own limit 2 * floor(log2 n); otherwise forced (tests reach the heap-sort fallback with it).
+__device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16> wl, int depth, int limit,
+                           int& ph) {
+  constexpr int XSEG_MAX = 64;           // > 2 log2(2^30): one piece per straddler level
+  __shared__ int s_any[2], s_end[2], s_win[2];
+  __shared__ int s_seg[XSEG_MAX][3];     // (l, h, depth) of the waiting pieces
   const int T = blockDim.x, t = threadIdx.x;
+  const int P = min(n, limit);
   if (depth < 0) depth = n > 0 ? 2 * (31 - __clz(n)) : 0;
-  for (int i = t; i < n; i += T) { w.lo[i] = 0; w.hi[i] = n; }
-  if (t == 0) { s_any = n > 16 && limit > 0; s_end = n; }
+  int sl = 0, sh = n, sd = depth, nseg = 0;      // the straddler (uniform)
+  if (n > NMS_XL && P <= NMS_XL) {
+    while (sh > NMS_XL && sh - sl > 16 && sd > 0 && nseg < XSEG_MAX - 1) {
+      const int ct = x_partition1(A, sl, sh, wg, ph);
+      --sd;
+      if (ct <= P - 1) {                 // [sl, ct) lies in the prefix: it waits
+        if (t == 0) { s_seg[nseg][0] = sl; s_seg[nseg][1] = ct; s_seg[nseg][2] = sd; }
+        ++nseg;
+        sl = ct;
+      } else {
+        sh = ct;                         // [ct, sh) lies past the prefix: never read
+      }
+    }
+    if (t == 0) { s_seg[nseg][0] = sl; s_seg[nseg][1] = sh; s_seg[nseg][2] = sd; }
+    ++nseg;
+  } else {
+    if (t == 0) { s_seg[0][0] = 0; s_seg[0][1] = n; s_seg[0][2] = depth; }
+    nseg = 1;
+  }
   __syncthreads();
-  while (s_any) {
-    const int E = s_end;                 // positions past E belong to no active segment
-    __syncthreads();                     // every thread has read s_any / s_end
-    auto active = [&](int l, int h) { return h - l > 16 && l < limit; };
-    if (depth == 0) {
-      for (int i = t; i < E; i += T) {
-        const int l = w.lo[i], h = w.hi[i];
-        if (l == i && active(l, h)) heap_sort(A + l, h - l);
+  const int W0 = sh;                     // every piece lies in [0, W0)
+  bool inl = W0 <= NMS_XL;
+  if (inl)
+    for (int i = t; i < W0; i += T) c[i] = A[i];
+  int any = 0;
+  for (int s = 0; s < nseg; ++s) {
+    const int l = s_seg[s][0], h = s_seg[s][1], d = s_seg[s][2];
+    for (int i = l + t; i < h; i += T) {
+      if (inl) { wl.lo[i] = (u16)l; wl.hi[i] = (u16)h; }
+      else { wg.lo[i] = l; wg.hi[i] = h; }
+    }
+    if (t == 0) {
+      if (inl) wl.Lp[l] = (u16)d;
+      else wg.Lp[l] = d;
+    }
+    any |= h - l > 16 && l < limit;
+  }
+  if (t == 0) { s_any[0] = any; s_end[0] = W0; }
+  __syncthreads();
+  for (int lv = 0;; ++lv) {
+    const int q = lv & 1;
+    if (!s_any[q]) break;
+    const int E = s_end[q];              // positions past E belong to no active segment
+    if (inl) {
+      x_level(c, wl, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph);
+      continue;
+    }
+    x_level(A, wg, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph);
+    // the window: every segment meeting [0, P) ends by the active ones' end or P-1's segment's
+    if (t == 0) s_win[q] = max(s_end[q ^ 1], P > 0 ? wg.hi[P - 1] : 0);   // s_end = 0: none active
+    __syncthreads();
+    const int W = s_win[q];
+    if (W <= NMS_XL) {
+      for (int i = t; i < W; i += T) {
+        c[i] = A[i];
+        wl.lo[i] = (u16)wg.lo[i];
+        wl.hi[i] = (u16)wg.hi[i];
+        wl.Lp[i] = (u16)wg.Lp[i];        // the budgets at the heads (the rest is not read)
       }
       __syncthreads();
-      break;
+      inl = true;
     }
-    --depth;
-    for (int i = t; i < E; i += T) {     // pivots: __unguarded_partition_pivot
-      const int l = w.lo[i], h = w.hi[i];
-      if (l == i && active(l, h)) median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
-    }
-    if (t == 0) w.SR[E] = 0;
-    __syncthreads();
-    const int C = (E + T - 1) / T;
-    const int c0 = min(E, t * C), c1 = min(E, c0 + C);
-    int cL = 0, cR = 0;                  // stopper flags over this thread's chunk
-    for (int i = c0; i < c1; ++i) {
-      const int l = w.lo[i], h = w.hi[i];
-      int f = 0;
-      if (active(l, h) && i > l) {
-        const float p = A[l].score, v = A[i].score;
-        f = (!(v > p) ? 1 : 0) | (!(p > v) ? 2 : 0);
-      }
-      w.fl[i] = f;
-      cL += f & 1;
-      cR += f >> 1;
-    }
-    int totL, totR;
-    const int exL = block_excl_scan(cL, &totL);
-    const int exR = block_excl_scan(cR, &totR);
-    int run = exL;                       // PL[i] = left stoppers in [0, i]
-    for (int i = c0; i < c1; ++i) { run += w.fl[i] & 1; w.PL[i] = run; }
-    run = totR - exR - cR;               // SR[i] = right stoppers in [i, E)
-    for (int i = c1 - 1; i >= c0; --i) { run += w.fl[i] >> 1; w.SR[i] = run; }
-    __syncthreads();
-    for (int i = t; i < E; i += T) {     // l_k, r_k by rank within the segment
-      const int f = w.fl[i];
-      if (!f) continue;
-      const int l = w.lo[i], h = w.hi[i];
-      if (f & 1) w.Lp[l + w.PL[i] - w.PL[l]] = i;
-      if (f & 2) w.Rp[l + w.SR[i] - w.SR[h]] = i;
-    }
-    __syncthreads();
-    for (int i = t; i < E; i += T) {     // the swaps (disjoint pairs) and each segment's cut
-      if (!(w.fl[i] & 1)) continue;
-      const int l = w.lo[i], h = w.hi[i];
-      const int k = w.PL[i] - w.PL[l];
-      const int cntL = w.PL[h - 1] - w.PL[l], cntR = w.SR[l + 1] - w.SR[h];
-      const int r = k <= cntR ? w.Rp[l + k] : -1;
-      if (r > i) {
-        xswap(A, i, r);
-        const bool next = k + 1 <= cntL && k + 1 <= cntR && w.Lp[l + k + 1] < w.Rp[l + k + 1];
-        if (!next) w.cut[l] = k + 1 <= cntL ? min(w.Lp[l + k + 1], r) : r;
-      } else if (k == 1) {
-        w.cut[l] = i;                    // no swap at all: cut = l_1
-      }
-    }
-    if (t == 0) { s_any = 0; s_end = 0; }
-    __syncthreads();
-    for (int i = t; i < E; i += T) {     // [first, cut) and [cut, last), one level deeper
-      const int l = w.lo[i], h = w.hi[i];
-      if (!active(l, h)) continue;
-      const int c = w.cut[l];
-      const int nl = i < c ? l : c, nh = i < c ? c : h;
-      w.lo[i] = nl;
-      w.hi[i] = nh;
-      if (i == nl && active(nl, nh)) {   // one thread per new active segment
-        s_any = 1;
-        atomicMax(&s_end, nh);
-      }
-    }
-    __syncthreads();
   }
-  const int P = min(n, limit);
-  for (int i = t; i < P; i += T) {       // __final_insertion_sort = stable sort of every leaf
-    const int l = w.lo[i], h = w.hi[i];
-    if (l == i && h - l <= 16) insertion_sort(A + l, h - l);
-  }
-  __syncthreads();
+  if (inl) x_leaves(c, wl, P);
+  else x_leaves(A, wg, P);
+  return inl;
 }
 
 // any equal neighbours among sorted c[0..n)?  (n <= 16: std::sort is then stable anyway)
@@ -306,41 +476,113 @@ __device__ bool has_ties(const Cand* c, int n) {
   return __syncthreads_or(tie);
 }
 
-__device__ __forceinline__ int wave_min(int v) {
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-  return v;
-}
-
-// greedy NMS over sorted c[0..n) (LDS or global).  box(idx) -> the candidate's xyxy box;
-// emit(k, pos) writes output row k from c[pos] (called by thread 0).  Returns the kept count.
-template <typename BoxFn, typename EmitFn>
-__device__ int greedy(Cand* c, int n, float iou_thr, int max_det, BoxFn box, EmitFn emit) {
-  __shared__ int s_next[3];
+// greedy NMS over sorted c[0..n) (LDS or global), 64 candidates (one wave's ballot) at a time:
+//  * all waves: the tile's 64x64 "row suppresses later column" bit matrix (IoU >= thr), beside
+//    the sweep that suppresses every candidate from this tile on by the previous tile's kept boxes
+//    (so each candidate has met every kept box of the earlier tiles before its tile is decided);
+//  * wave 0: the sequential greedy over the tile with scalar bit operations -- the lowest live
+//    candidate is kept and its row clears the ones it suppresses -- stopping at max_det.
+// That is the one-box-at-a-time greedy exactly, with two barriers per 64 candidates instead of
+// one per kept box.  box(idx) -> the candidate's xyxy box, cached in LDS (bc) for the first
+// NMS_XL positions.  Suppressed candidates are marked in place, so the kept boxes are the
+// unsuppressed positions of c[0..*last] (emit_kept writes them).  Returns the kept count.
+template <typename BoxFn>
+__device__ int greedy(Cand* c, int n, float iou_thr, int max_det, float4* bc, BoxFn box, int* last) {
+  __shared__ unsigned long long s_row[64];
+  __shared__ float4 s_kb[2][64];         // the kept boxes of a tile, by tile parity
+  __shared__ int s_kn[2], s_kept, s_last;
+  const int T = blockDim.x, t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = T >> 6;
+  *last = -1;
   if (n <= 0) return 0;
-  if (threadIdx.x < 3) s_next[threadIdx.x] = INT_MAX;
+  const int nb = min(n, NMS_XL);
+  for (int i = t; i < nb; i += T) bc[i] = box(c[i].idx);
+  if (t == 0) { s_kn[0] = s_kn[1] = 0; s_kept = 0; s_last = -1; }
   __syncthreads();
-  int cur = 0, kept = 0;
-  for (int it = 0;; ++it) {
-    if (threadIdx.x == 0) emit(kept, cur);
-    if (++kept >= max_det) break;
-    const float4 cb = box(c[cur].idx);
-    int first = INT_MAX;                 // this thread's first surviving position after cur
-    for (int i = cur + 1 + threadIdx.x; i < n; i += blockDim.x) {
+  auto boxat = [&](int i) { return i < nb ? bc[i] : box(c[i].idx & INT_MAX); };
+  for (int t0 = 0, tp = 0; t0 < n; t0 += 64, tp ^= 1) {
+    const int kn = s_kn[tp ^ 1];
+    for (int i = t0 + t; kn > 0 && i < n; i += T) {
       const int id = c[i].idx;
       if (id < 0) continue;
-      if (!(iou(cb, box(id)) < iou_thr)) c[i].idx = id | NMS_DEAD;
-      else first = min(first, i);
+      const float4 bx = boxat(i);
+      for (int k = 0; k < kn; ++k)
+        if (!(iou(s_kb[tp ^ 1][k], bx) < iou_thr)) { c[i].idx = id | NMS_DEAD; break; }
     }
-    first = wave_min(first);
-    if ((threadIdx.x & 63) == 0 && first != INT_MAX) atomicMin(&s_next[it % 3], first);
-    // the buffer of the next iteration was last read before the previous barrier
-    if (threadIdx.x == 0) s_next[(it + 1) % 3] = INT_MAX;
+    for (int r = wv; r < 64; r += nw) {
+      const int pr = t0 + r, pc = t0 + lane;
+      bool sup = false;
+      if (pc < n && lane > r && c[pr].idx >= 0) sup = !(iou(boxat(pr), boxat(pc)) < iou_thr);
+      const unsigned long long m = __ballot(sup);
+      if (lane == 0) s_row[r] = m;
+    }
     __syncthreads();
-    cur = s_next[it % 3];
-    if (cur == INT_MAX) break;
+    if (wv == 0) {                       // the sequential greedy over the tile
+      const int i = t0 + lane;
+      const bool live = i < n && c[i].idx >= 0;
+      const unsigned long long row = s_row[lane];
+      unsigned long long alive = __ballot(live), keep = 0;
+      int kept = s_kept;
+      while (alive && kept < max_det) {
+        const int j = __builtin_ctzll(alive);
+        keep |= 1ull << j;
+        ++kept;
+        const unsigned rlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)row, j);
+        const unsigned rhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(row >> 32), j);
+        alive &= ~(((unsigned long long)rhi << 32) | rlo) & ~(1ull << j);
+      }
+      const bool kp = (keep >> lane) & 1;
+      if (live && !kp) c[i].idx |= NMS_DEAD;   // suppressed (or past the max_det-th: unread)
+      if (kp) s_kb[tp][__popcll(keep & ((1ull << lane) - 1))] = boxat(i);
+      if (lane == 0) {
+        s_kn[tp] = __popcll(keep);
+        s_kept = kept;
+        if (keep) s_last = t0 + 63 - __builtin_clzll(keep);
+      }
+    }
+    __syncthreads();
+    if (s_kept >= max_det) break;
   }
-  __syncthreads();
+  *last = s_last;
+  const int kept = s_kept;
+  __syncthreads();                       // s_* are reused by the next call
   return kept;
+}
+
+// emit(k, pos) for the k-th unsuppressed position of c[0..last], all threads at once
+template <typename EmitFn>
+__device__ void emit_kept(const Cand* c, int last, EmitFn emit, int& ph) {
+  const int m = last + 1, T = blockDim.x;
+  const int C = (m + T - 1) / T;
+  const int c0 = min(m, (int)threadIdx.x * C), c1 = min(m, c0 + C);
+  int cnt = 0;
+  for (int i = c0; i < c1; ++i) cnt += c[i].idx >= 0;
+  long long tot;
+  int k = (int)block_excl_scan(cnt, &tot, ph);
+  for (int i = c0; i < c1; ++i)
+    if (c[i].idx >= 0) emit(k++, i);
+}
+
+// LDS of the three kernels: the candidate array, then the sort window's index arrays (reused
+// as the greedy's box cache)
+constexpr size_t NMS_AUX_BYTES = (size_t)XWORK_ARRAYS * (NMS_XL + 1) * sizeof(u16);
+constexpr size_t NMS_LDS = (size_t)NMS_CAP * sizeof(Cand) + NMS_AUX_BYTES;
+static_assert(NMS_AUX_BYTES >= NMS_XL * sizeof(float4), "box cache fits the index arrays");
+static_assert(NMS_XL <= NMS_CAP && NMS_XL < 65536, "window indices are 16-bit");
+
+struct NmsSmem {
+  Cand* c;
+  XW<u16> wl;
+  float4* bc;
+};
+
+__device__ __forceinline__ NmsSmem nms_smem() {
+  extern __shared__ __attribute__((aligned(16))) unsigned char nms_sm[];
+  NmsSmem m;
+  m.c = reinterpret_cast<Cand*>(nms_sm);
+  u16* aux = reinterpret_cast<u16*>(nms_sm + (size_t)NMS_CAP * sizeof(Cand));
+  m.wl = xw_at(aux, NMS_XL + 1);
+  m.bc = reinterpret_cast<float4*>(aux);
+  return m;
 }
 
 __global__ void __launch_bounds__(NMS_THREADS) k_nms_scale(const hv_nms_scale* __restrict__ scales, int nscales,
@@ -348,7 +590,8 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_scale(const hv_nms_scale* _
                                                            Cand* __restrict__ gcand, int* __restrict__ gx,
                                                            long seg_stride, float* sboxes, float* sscores,
                                                            int64_t* slabels, int* scount) {
-  __shared__ Cand c[NMS_CAP];              // 64 KiB
+  const NmsSmem sm = nms_smem();
+  Cand* c = sm.c;
   __shared__ int s_n;
   const int sc = blockIdx.x % nscales, b = blockIdx.x / nscales;
   const long seg = (long)blockIdx.x;
@@ -365,8 +608,7 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_scale(const hv_nms_scale* _
     const float v = score[i];
     if (v > conf_thr) {
       const int slot = atomicAdd(&s_n, 1);
-      if (slot < NMS_CAP) c[slot] = Cand{v, (int)i};
-      else if (slot < cap) g[slot] = Cand{v, (int)i};   // past the LDS capacity
+      if (slot < NMS_BITONIC) c[slot] = Cand{v, (int)i};   // more: the exact path re-compacts
     }
   }
   __syncthreads();
@@ -382,39 +624,42 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_scale(const hv_nms_scale* _
       slabels[seg * max_det + k] = lab[e.idx];
     };
   };
-  int kept = 0;
-  bool exact = n > NMS_CAP;                // past the LDS: std::sort's order straight away
+  int kept = 0, last = -1, ph = 0;         // ph: scan calls (block_excl_scan)
+  bool exact = n > NMS_BITONIC;            // std::sort's order straight away
   if (!exact) {
     lds_sort(c, n);
     exact = has_ties(c, n);                // distinct scores: the one sorted order is the reference's
-    if (!exact) kept = greedy(c, n, iou_thr, max_det, box, emit_from(c));
+    if (!exact) {
+      kept = greedy(c, n, iou_thr, max_det, sm.bc, box, &last);
+      emit_kept(c, last, emit_from(c), ph);
+    }
   }
   if (exact) {
     // the reference's order (ties included): the masked candidates in cell order, std::sort
     // restated over the prefix the greedy reads; a greedy that runs off the prefix before
     // max_det widens it 4x and starts over (deterministic)
-    const XWork xw = xwork_at(gx + seg * XWORK_ARRAYS * (seg_stride + 1), seg_stride + 1);
+    const XWork xw = xw_at(gx + seg * XWORK_ARRAYS * (seg_stride + 1), seg_stride + 1);
     for (int limit = min(n, NMS_PREFIX0);; limit = min(n, 4 * limit)) {
       const long C = (cells + blockDim.x - 1) / blockDim.x;
       const long c0 = min(cells, (long)threadIdx.x * C), c1 = min(cells, c0 + C);
       int cnt = 0;
       for (long i = c0; i < c1; ++i) cnt += score[i] > conf_thr;
-      int tot;
-      int o = block_excl_scan(cnt, &tot);
+      long long tot;
+      int o = (int)block_excl_scan(cnt, &tot, ph);
       for (long i = c0; i < c1; ++i) {
         const float v = score[i];
         if (v > conf_thr && o < cap) g[o] = Cand{v, (int)i};
         o += v > conf_thr;
       }
       __syncthreads();
-      exact_sort(g, n, xw, -1, limit);
-      if (limit <= NMS_CAP) {              // the greedy reads the prefix from LDS
+      Cand* src = exact_sort(g, n, xw, c, sm.wl, -1, limit, ph) ? c : g;
+      if (src == g && limit <= NMS_CAP) {  // the greedy reads the prefix from LDS
         for (int i = threadIdx.x; i < limit; i += blockDim.x) c[i] = g[i];
         __syncthreads();
-        kept = greedy(c, limit, iou_thr, max_det, box, emit_from(c));
-      } else {
-        kept = greedy(g, limit, iou_thr, max_det, box, emit_from(g));
+        src = c;
       }
+      kept = greedy(src, limit, iou_thr, max_det, sm.bc, box, &last);
+      emit_kept(src, last, emit_from(src), ph);
       if (kept >= max_det || limit == n) break;
     }
   }
@@ -428,7 +673,8 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_final(int nscales, float io
                                                            Cand* __restrict__ gcand, int* __restrict__ gx,
                                                            long img_stride, float* boxes, float* scores,
                                                            int64_t* labels, int* count) {
-  __shared__ Cand c[NMS_CAP];
+  const NmsSmem sm = nms_smem();
+  Cand* c = sm.c;
   const int b = blockIdx.x;
   int n = 0;
   for (int s = 0; s < nscales; ++s) n += scount[b * nscales + s];
@@ -456,26 +702,29 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_final(int nscales, float io
       labels[(long)b * max_det + k] = slabels[from];
     };
   };
-  int kept = 0;
-  bool exact = n > NMS_CAP;
+  int kept = 0, last = -1, ph = 0;
+  bool exact = n > NMS_BITONIC;
   if (!exact) {
     gather(c);
     lds_sort(c, n);       // idx grows with the concatenation order
     exact = has_ties(c, n);
-    if (!exact) kept = greedy(c, n, iou_thr, max_det, box, emit_from(c));
+    if (!exact) {
+      kept = greedy(c, n, iou_thr, max_det, sm.bc, box, &last);
+      emit_kept(c, last, emit_from(c), ph);
+    }
   }
   if (exact) {            // as stage 1: std::sort's order over the prefix the greedy reads
-    const XWork xw = xwork_at(gx + (long)b * XWORK_ARRAYS * (img_stride + 1), img_stride + 1);
+    const XWork xw = xw_at(gx + (long)b * XWORK_ARRAYS * (img_stride + 1), img_stride + 1);
     for (int limit = min(n, NMS_PREFIX0);; limit = min(n, 4 * limit)) {
       gather(g);
-      exact_sort(g, n, xw, -1, limit);
-      if (limit <= NMS_CAP) {
+      Cand* src = exact_sort(g, n, xw, c, sm.wl, -1, limit, ph) ? c : g;
+      if (src == g && limit <= NMS_CAP) {
         for (int i = threadIdx.x; i < limit; i += blockDim.x) c[i] = g[i];
         __syncthreads();
-        kept = greedy(c, limit, iou_thr, max_det, box, emit_from(c));
-      } else {
-        kept = greedy(g, limit, iou_thr, max_det, box, emit_from(g));
+        src = c;
       }
+      kept = greedy(src, limit, iou_thr, max_det, sm.bc, box, &last);
+      emit_kept(src, last, emit_from(src), ph);
       if (kept >= max_det || limit == n) break;
     }
   }
@@ -491,10 +740,12 @@ __global__ void __launch_bounds__(NMS_THREADS) k_nms_final(int nscales, float io
 // torch.sort(vals, descending=True).indices on the CPU, exactly (one workgroup)
 __global__ void __launch_bounds__(NMS_THREADS) k_sort_desc_exact(const float* vals, int n, int depth, int* out_idx,
                                                                  Cand* A, int* gx) {
+  const NmsSmem sm = nms_smem();
   for (int i = threadIdx.x; i < n; i += blockDim.x) A[i] = Cand{vals[i], i};
   __syncthreads();
-  exact_sort(A, n, xwork_at(gx, (long)n + 1), depth, n);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) out_idx[i] = A[i].idx;
+  int ph = 0;
+  const Cand* src = exact_sort(A, n, xw_at(gx, (long)n + 1), sm.c, sm.wl, depth, n, ph) ? sm.c : A;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out_idx[i] = src[i].idx;
 }
 
 // workspace layout: [stage-1 Cand regions][stage-1 sort scratch][stage-2 Cand regions]
@@ -535,6 +786,16 @@ bool nms_args_ok(int batch, int nscales, int max_det, long max_cells) {
          (long)batch * nscales * max_det <= (1L << 30);
 }
 
+void nms_lds_attrs() {
+  static const bool done = [] {
+    (void)hipFuncSetAttribute((const void*)k_nms_scale, hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS);
+    (void)hipFuncSetAttribute((const void*)k_nms_final, hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS);
+    (void)hipFuncSetAttribute((const void*)k_sort_desc_exact, hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS);
+    return true;
+  }();
+  (void)done;
+}
+
 }  // namespace
 
 extern "C" size_t hv_nms_work_bytes(int batch, int nscales, int max_det, long max_cells) {
@@ -552,12 +813,13 @@ extern "C" int hv_nms(const hv_nms_scale* dev_scales, int nscales, int batch, fl
   const NmsLayout L = nms_layout(batch, nscales, max_det, max_cells);
   unsigned char* w = (unsigned char*)work;
   const size_t segs = (size_t)batch * nscales;
-  k_nms_scale<<<(unsigned)segs, NMS_THREADS, 0, s>>>(dev_scales, nscales, conf_thr, iou_thr, max_det,
+  nms_lds_attrs();
+  k_nms_scale<<<(unsigned)segs, NMS_THREADS, NMS_LDS, s>>>(dev_scales, nscales, conf_thr, iou_thr, max_det,
                                                       (Cand*)(w + L.cand1), (int*)(w + L.x1), L.seg_stride,
                                                       (float*)(w + L.boxes), (float*)(w + L.scores),
                                                       (int64_t*)(w + L.labels), (int*)(w + L.counts));
   HV_CHECK_LAUNCH();
-  k_nms_final<<<batch, NMS_THREADS, 0, s>>>(nscales, iou_thr, max_det, (const float*)(w + L.boxes),
+  k_nms_final<<<batch, NMS_THREADS, NMS_LDS, s>>>(nscales, iou_thr, max_det, (const float*)(w + L.boxes),
                                               (const float*)(w + L.scores), (const int64_t*)(w + L.labels),
                                               (const int*)(w + L.counts), (Cand*)(w + L.cand2), (int*)(w + L.x2),
                                               L.img_stride, boxes, scores, labels, count);
@@ -574,7 +836,8 @@ extern "C" int hv_sort_desc_exact(const float* vals, int n, int depth_limit, int
                                   hv_stream_t stream) {
   if (!vals || !out_idx || !work || n <= 0 || n > (1 << 28)) return HV_EINVAL;
   unsigned char* w = (unsigned char*)work;
-  k_sort_desc_exact<<<1, NMS_THREADS, 0, (hipStream_t)stream>>>(
+  nms_lds_attrs();
+  k_sort_desc_exact<<<1, NMS_THREADS, NMS_LDS, (hipStream_t)stream>>>(
       vals, n, depth_limit, out_idx, (Cand*)w, (int*)(w + align256((size_t)n * sizeof(Cand))));
   HV_CHECK_LAUNCH();
   return HV_OK;
