@@ -461,8 +461,10 @@ __global__ void __launch_bounds__(256) k_chan_final(const float* part, int n, in
   __shared__ float red[256];
   const int b = blockIdx.y, ch = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
   float s = 0.f;
-  if (ch < c)
+  if (ch < c) {
+#pragma unroll 8
     for (int k = q; k < nchunk; k += 4) s += part[((long)b * nchunk + k) * c + ch];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   if (q == 0 && ch < c)
