@@ -30,7 +30,8 @@ constexpr int NMS_THREADS = 1024;
 constexpr int NMS_DEAD = INT_MIN;   // sign bit of Cand::idx: suppressed
 constexpr int NMS_PREFIX0 = 1024;   // first prefix of the exact sort the greedy reads (widened 4x)
 constexpr int NMS_XL = 6144;        // exact-sort window (and greedy box cache) held in LDS
-constexpr int NMS_BITONIC = 2048;   // above: straight to the exact sort (as fast, and bf16 scores tie)
+constexpr int NMS_BITONIC = 2048;
+constexpr int NMS_WAVE = 64;        // segments this small are finished by one wave in registers   // above: straight to the exact sort (as fast, and bf16 scores tie)
 
 struct Cand {
   float score;
@@ -209,6 +210,179 @@ __device__ long long block_excl_scan(long long v, long long* total, int& ph) {
   return before + x - v;
 }
 
+// ---- one segment of <= 64 positions sorted by one wave, in registers ----------------------------
+// Lane j holds A[l + j]; every lane also holds its segment's bounds [slo, shi) (lane indices) and
+// depth budget sd (-1 = heap-sorted), so all segments of the wave are partitioned at once with
+// ballots instead of block barriers: the k-th left / right stopper of a segment is found by rank
+// through a 64-entry per-wave LDS table, pairs swap through ds_bpermute.  Same permutation as the
+// block levels (and std::sort); leaves end with a stable rank sort.
+__device__ __forceinline__ float lane_f(float v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ int lane_i(int v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ float rl_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ void wl_f(float& v, int lane, float x) {   // lane `lane` := x (uniform)
+  if ((int)(threadIdx.x & 63) == lane) v = x;
+}
+__device__ __forceinline__ void wl_i(int& v, int lane, int x) {
+  if ((int)(threadIdx.x & 63) == lane) v = x;
+}
+
+// A heap-sort operand held by one wave: element e (uniform) lives in register e / 64 of lane
+// e % 64 (x_wave_sort: one register).  (Four registers for the block levels' heap-sort fallback
+// of segments up to 256 measured ~4x slower than the one-thread LDS form: every access is R
+// readlanes plus selects on one dependent chain.)
+template <int R>
+struct WReg {
+  float s[R];
+  int x[R];
+};
+
+template <int R>
+__device__ __forceinline__ float wr_s(const WReg<R>& w, int e) {
+  float v = 0.f;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if ((e >> 6) == r) v = rl_f(w.s[r], e & 63);
+  return v;
+}
+template <int R>
+__device__ __forceinline__ int wr_x(const WReg<R>& w, int e) {
+  int v = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if ((e >> 6) == r) v = __builtin_amdgcn_readlane(w.x[r], e & 63);
+  return v;
+}
+template <int R>
+__device__ __forceinline__ void wr_set(WReg<R>& w, int e, float vs, int vi) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if ((e >> 6) == r) {
+      wl_f(w.s[r], e & 63, vs);
+      wl_i(w.x[r], e & 63, vi);
+    }
+}
+
+// std::__adjust_heap on elements [a, a + len) of w, serially with uniform indices
+template <int R>
+__device__ void wave_adjust_heap(WReg<R>& w, int a, int hole, int len, float vs, int vi) {
+  const int top = hole;
+  int child = hole;
+  while (child < (len - 1) / 2) {
+    child = 2 * (child + 1);
+    if (wr_s(w, a + child) > wr_s(w, a + child - 1)) --child;
+    wr_set(w, a + hole, wr_s(w, a + child), wr_x(w, a + child));
+    hole = child;
+  }
+  if ((len & 1) == 0 && child == (len - 2) / 2) {
+    child = 2 * (child + 1);
+    wr_set(w, a + hole, wr_s(w, a + child - 1), wr_x(w, a + child - 1));
+    hole = child - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && wr_s(w, a + parent) > vs) {
+    wr_set(w, a + hole, wr_s(w, a + parent), wr_x(w, a + parent));
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  wr_set(w, a + hole, vs, vi);
+}
+
+// std::__partial_sort(first, last, last) = make_heap + sort_heap on elements [a, a + len)
+template <int R>
+__device__ void wave_heap_sort(WReg<R>& w, int a, int len) {
+  if (len >= 2) {
+    for (int parent = (len - 2) / 2;; --parent) {
+      wave_adjust_heap(w, a, parent, len, wr_s(w, a + parent), wr_x(w, a + parent));
+      if (parent == 0) break;
+    }
+  }
+  for (int last = len; last > 1;) {
+    --last;
+    const float vs = wr_s(w, a + last);
+    const int vi = wr_x(w, a + last);
+    wr_set(w, a + last, wr_s(w, a), wr_x(w, a));
+    wave_adjust_heap(w, a, 0, last, vs, vi);
+  }
+}
+
+// std::sort's treatment of the segment A[l, h) (h - l <= 64) with depth budget d, in one wave;
+// LL / RR: this wave's 64-entry rank tables
+__device__ void x_wave_sort(Cand* A, int l, int h, int d, unsigned char* LL, unsigned char* RR) {
+  const int j = threadIdx.x & 63, m = h - l;
+  float sc = -INFINITY;
+  int ix = 0;
+  if (j < m) { const Cand e = A[l + j]; sc = e.score; ix = e.idx; }
+  int slo = j < m ? 0 : j, shi = j < m ? m : j + 1, sd = d;
+  const unsigned long long below = (1ull << j) - 1, above = ~((2ull << j) - 1);
+  for (;;) {
+    const int sz = shi - slo;
+    const bool act = sz > 16 && sd >= 0;
+    if (!__ballot(act)) break;
+    unsigned long long hz = __ballot(act && j == slo && sd == 0);
+    while (hz) {                         // spent budgets: std::__partial_sort
+      const int s0 = __builtin_ctzll(hz);
+      hz &= hz - 1;
+      const int e0 = __builtin_amdgcn_readlane(shi, s0);
+      WReg<1> w1{{sc}, {ix}};
+      wave_heap_sort(w1, s0, e0 - s0);
+      sc = w1.s[0];
+      ix = w1.x[0];
+      if (j >= s0 && j < e0) sd = -1;
+    }
+    const bool part = act && sd > 0;
+    // __move_median_to_first(slo, slo + 1, slo + sz / 2, shi - 1), per segment
+    const int a = slo + 1, b = slo + sz / 2, c = shi - 1;
+    const float va = lane_f(sc, a), vb = lane_f(sc, b), vc = lane_f(sc, c);
+    int X;
+    if (va > vb) X = vb > vc ? b : (va > vc ? c : a);
+    else X = va > vc ? a : (vb > vc ? c : b);
+    int src = j;
+    if (part) src = j == slo ? X : (j == X ? slo : j);
+    sc = lane_f(sc, src);
+    ix = lane_i(ix, src);
+    const float p = lane_f(sc, slo);
+    const bool fL = part && j > slo && !(sc > p), fR = part && j > slo && !(p > sc);
+    const unsigned long long bL = __ballot(fL), bR = __ballot(fR);
+    const unsigned long long seg = (shi >= 64 ? ~0ull : ((1ull << shi) - 1)) & ~((1ull << slo) - 1);
+    const int cntL = __popcll(bL & seg), cntR = __popcll(bR & seg);
+    const int kL = __popcll(bL & seg & below) + 1, kR = __popcll(bR & seg & above) + 1;
+    if (fL) LL[slo + kL] = (unsigned char)j;
+    if (fR) RR[slo + kR] = (unsigned char)j;
+    __builtin_amdgcn_wave_barrier();
+    const int rP = fL && kL <= cntR ? (int)RR[slo + kL] : -1;
+    const int lP = fR && kR <= cntL ? (int)LL[slo + kR] : 64;
+    const bool swL = fL && rP > j, swR = fR && lP < j;
+    const int K = __popcll(__ballot(swL) & seg);
+    int cut = 0;
+    if (part) cut = K == 0 ? (int)LL[slo + 1]
+                           : (K + 1 <= cntL ? min((int)LL[slo + K + 1], (int)RR[slo + K]) : (int)RR[slo + K]);
+    __builtin_amdgcn_wave_barrier();     // the tables are rewritten by the next level
+    src = swL ? rP : (swR ? lP : j);
+    sc = lane_f(sc, src);
+    ix = lane_i(ix, src);
+    if (part) {
+      if (j < cut) shi = cut;
+      else slo = cut;
+      --sd;
+    }
+  }
+  // __final_insertion_sort within the leaves: stable rank by score (heap-sorted runs stay put)
+  int rank = j - slo;
+  const bool leaf = sd >= 0 && shi - slo <= 16;
+  if (__ballot(leaf & (j < m))) {
+    int r = 0;
+    for (int dd = 0; dd < 16; ++dd) {
+      const int i = slo + dd;
+      const float si = lane_f(sc, min(i, 63));
+      if (i < shi) r += (si > sc) || (si == sc && i < j);
+    }
+    if (leaf) rank = r;
+  }
+  if (j < m) A[l + slo + rank] = Cand{sc, ix};
+}
+
 // Each segment carries its own std::sort depth budget, kept at Lp[head] (Lp[l + k] is written
 // for k >= 1 only); X_DONE marks a segment the heap-sort fallback has finished.
 template <typename I>
@@ -221,8 +395,8 @@ __device__ __forceinline__ bool x_active(int l, int h, int limit, I d) {
 
 // one recursion level: every active segment of A[0, E) partitioned at once (see above); a segment
 // whose budget is spent is heap-sorted instead (std::__partial_sort).  The split leaves s_any =
-// "an active segment remains" and s_end = the last one's end (the caller alternates two pairs of
-// them between levels, so the level never waits for their readers).
+// "an active segment of more than NMS_WAVE remains" and s_end = the last active one's end (the
+// caller alternates two pairs of them between levels, so the level never waits for their readers).
 template <typename I>
 __device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, int& s_any, int& s_end, int& ph) {
   const int T = blockDim.x, t = threadIdx.x;
@@ -308,9 +482,38 @@ __device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, i
       const I d = Rp[l];
       Lp[nl] = d;
       if (x_active(nl, nh, limit, d)) {
-        s_any = 1;
         atomicMax(&s_end, nh);
+        if (nh - nl > NMS_WAVE) s_any = 1;   // smaller ones finish in x_wave_phase
       }
+    }
+  }
+  __syncthreads();
+}
+
+// every active segment of [0, E) (all <= NMS_WAVE here): one wave each, waves over head chunks
+template <typename I>
+__device__ void x_wave_phase(Cand* A, const XW<I> w, int E, int limit) {
+  __shared__ unsigned char s_rank[NMS_THREADS / 64][2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int base = wv * 64; base < E; base += nw * 64) {
+    const int i = base + lane;
+    int h = 0, d = 0;
+    bool hd = false;
+    if (i < E) {
+      const int l = w.lo[i];
+      h = w.hi[i];
+      if (l == i) {
+        const I dd = w.Lp[l];
+        hd = x_active(l, h, limit, dd);
+        d = (int)dd;
+      }
+    }
+    unsigned long long hm = __ballot(hd);
+    while (hm) {
+      const int s0 = __builtin_ctzll(hm);
+      hm &= hm - 1;
+      x_wave_sort(A, base + s0, __builtin_amdgcn_readlane(h, s0), __builtin_amdgcn_readlane(d, s0),
+                  s_rank[wv][0], s_rank[wv][1]);
     }
   }
   __syncthreads();
@@ -435,13 +638,17 @@ __device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16
       if (inl) wl.Lp[l] = (u16)d;
       else wg.Lp[l] = d;
     }
-    any |= h - l > 16 && l < limit;
+    any |= h - l > NMS_WAVE && l < limit;
   }
   if (t == 0) { s_any[0] = any; s_end[0] = W0; }
   __syncthreads();
+  int Ew = W0;                            // the active segments' extent for the wave phase
   for (int lv = 0;; ++lv) {
     const int q = lv & 1;
-    if (!s_any[q]) break;
+    if (!s_any[q]) {
+      Ew = s_end[q];
+      break;
+    }
     const int E = s_end[q];              // positions past E belong to no active segment
     if (inl) {
       x_level(c, wl, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph);
@@ -463,8 +670,13 @@ __device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16
       inl = true;
     }
   }
-  if (inl) x_leaves(c, wl, P);
-  else x_leaves(A, wg, P);
+  if (inl) {
+    x_wave_phase(c, wl, Ew, limit);
+    x_leaves(c, wl, P);
+  } else {
+    x_wave_phase(A, wg, Ew, limit);
+    x_leaves(A, wg, P);
+  }
   return inl;
 }
 

@@ -487,7 +487,7 @@ def test_streaming_640_b1_frozen_graph_and_pipeline(gpu_device):
     # (2) the streaming pipeline on camera frames
     conf, iou, md = 0.25, 0.45, 100
     pipe = StreamingPipeline(m16, (720, 1280), (640, 640), conf_threshold=conf, iou_threshold=iou, max_detections=md)
-    matched_all, n_all, same_label, counts = 0, 0, 0, []
+    matched_all, n_all, same_label, counts, cands = 0, 0, 0, [], []
     for i, fr in enumerate(cases.camera_frames(60, 2, 720, 1280)):
         got = pipe(fr)
         with torch.no_grad():
@@ -498,6 +498,12 @@ def test_streaming_640_b1_frozen_graph_and_pipeline(gpu_device):
                                   for k, v in dec16.items()}, conf, iou, md)[0]
             det32 = m32.detect(ops.preprocess(fd, 640, 640, resample="pil"), conf + 0.05, iou, md)[0]
         counts.append(len(got["scores"]))
+        # candidates per scale above the threshold, and how many of them share a score (the tie
+        # order the exact sort reproduces)
+        cs = {k: v["class_scores"].reshape(-1) for k, v in sorted(dec16.items())}
+        cands.append({k: {"candidates": int((v > conf).sum()),
+                          "tied": int(v[v > conf].numel() - torch.unique(v[v > conf]).numel())}
+                      for k, v in cs.items()})
         assert len(got["scores"]) == ref["scores"].numel() > 0, (i, len(got["scores"]), ref["scores"].numel())
         np.testing.assert_array_equal(got["scores"], ref["scores"].numpy())
         np.testing.assert_array_equal(got["labels"], ref["labels"].numpy())
@@ -516,7 +522,8 @@ def test_streaming_640_b1_frozen_graph_and_pipeline(gpu_device):
         n_all += b32.shape[0]
     assert pipe.recaptures == 0
     frac = matched_all / max(n_all, 1)
-    rec["pipeline"] = {"frames": 2, "detections_per_frame": counts, "fp32_top_detections": n_all,
+    rec["pipeline"] = {"frames": 2, "detections_per_frame": counts, "candidates_per_scale": cands,
+                       "fp32_top_detections": n_all,
                        "fp32_top_matched_by_bf16_box_iou_0.5": round(frac, 4),
                        "label_agreement_of_matched": round(same_label / max(matched_all, 1), 4)}
     record_parity("streaming_640_b1", rec)
