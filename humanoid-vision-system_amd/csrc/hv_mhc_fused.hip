@@ -840,8 +840,8 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
 #pragma unroll
     for (int hl = 0; hl < HQT; ++hl) {
       const int r = (qq * HQT + hl) * 16 + fr;
-      const uint2 lo = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
-      const uint2 hi = *reinterpret_cast<const uint2*>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+      const uint2 lo = lds_b64<true>(sw + r * 64 + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+      const uint2 hi = lds_b64<true>(sw + r * 64 + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
       const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
       for (int t = 0; t < TT; ++t) acc2[hl][t] = mfma(af, bf[t], acc2[hl][t]);
@@ -915,8 +915,8 @@ __global__ void __launch_bounds__(256 * NG, 1) mhc_fused2_kernel(
       for (int dt = 0; dt < C::DT3; ++dt) {
         const int r = dt * 16 + fr;
         const unsigned char* row = wcp + (kc * C::DP + r) * 64;
-        const uint2 lo = *reinterpret_cast<const uint2*>(row + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
-        const uint2 hi = *reinterpret_cast<const uint2*>(row + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
+        const uint2 lo = lds_b64<true>(row + swz64(r, fg >> 1) * 16 + (fg & 1) * 8);
+        const uint2 hi = lds_b64<true>(row + swz64(r, 2 + (fg >> 1)) * 16 + (fg & 1) * 8);
         const uint4 af = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
         for (int t = 0; t < TT; ++t) acc3[dt][t] = mfma(af, h2f[j][t], acc3[dt][t]);
