@@ -185,7 +185,11 @@ __global__ void __launch_bounds__(256) k_pg2(const hv_mhc_prep_entry* __restrict
 template <typename T>
 __device__ __forceinline__ void fold_tile(const hv_mhc_prep_entry& e, const Scratch& sc, int tile, char* lds) {
   constexpr bool BF = std::is_same<T, unsigned short>::value;
-  constexpr int RB = BF ? 80 : 144;      // LDS row bytes: 32 k + 16 B pad
+  // LDS row bytes: 32 k + pad.  bf16: 96-B rows put the 16 rows of each ds_read_b128 lane group
+  // (rows 0-3 / 12-15 at chunk fg, 4-11 at fg+1, or the reverse) on 16 distinct 4-bank sets
+  // ((6 r + c) mod 16 is a bijection there); the 80-B rows had rows r and r+3 colliding
+  // (SQ_LDS_BANK_CONFLICT 0.36 of the LDS cycles)
+  constexpr int RB = BF ? 96 : 144;
   const int D = e.D, K = e.Hd;
   const int ntn = (D + 63) / 64;
   const int m0 = (tile / ntn) * 64, n0 = (tile % ntn) * 64;

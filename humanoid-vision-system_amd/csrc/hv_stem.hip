@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) k_conv_stem(const TI* __restrict__ x, int
 // fragment per (tap, 16-channel tile): 9 x 2 per wave), and wave w of a group computes row w as
 // D^T[channel][pixel] = W . X^T -- the tap's 32 input channels are exactly one MFMA k-step, the
 // B fragment (16 pixels x 8 channels per lane group) is one conflict-free 16-B LDS read shared by
-// the N/16 channel tiles, and each lane ends with 4 consecutive output channels of one pixel
+// the N/16 channel tiles (conflict-free through the chunk swizzle below), and each lane ends with 4 consecutive output channels of one pixel
 // (8-B stores, 64 contiguous bytes per pixel across the 4 lane groups).  Same per-tap k order as
 // the GEMM path (kh, kw, c); epilogue = hv_gemm_epi.h's (alpha*scale, bias, act).
 using bf = unsigned short;
@@ -116,6 +116,12 @@ __device__ __forceinline__ f32x4 mfma_bf16(const uint4& a, const uint4& b, const
 }
 
 constexpr int C3_CIN = 32, C3_TW = 64, C3_TH = 4, C3_HW = C3_TW + 2, C3_HH = C3_TH + 2;
+
+// 16-B chunk q of halo pixel p lives at chunk q ^ (2 * ((p >> 2) & 1)): a B-fragment read
+// (ds_read_b128, 16-lane groups of pixels p..p+15 with chunk g for lanes 0-3 / 12-15 and g+1 for
+// 4-11, or the reverse) then hits 16 distinct 4-bank sets.  Unswizzled, pixels p and p+4 share
+// banks (64 B per pixel): 2-way on every read (SQ_LDS_BANK_CONFLICT 0.46 of the LDS cycles).
+__device__ __forceinline__ int c3_chunk(int pix, int q) { return q ^ (((pix >> 2) & 1) << 1); }
 
 // NT = N/16 channel tiles; the workgroup has NT/2 groups of 4 waves, group h computing channel
 // tiles 2h, 2h+1 (so a wave holds 18 weight fragments + 8 accumulators at any N: 128 VGPRs)
@@ -149,7 +155,7 @@ __global__ void __launch_bounds__(128 * NT) k_conv3x3_c32(const hv_gemm_desc d, 
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (iy >= 0 && iy < H && ix >= 0 && ix < W)
       v = *reinterpret_cast<const uint4*>(X + (((long)b * H + iy) * W + ix) * C3_CIN + q * 8);
-    *reinterpret_cast<uint4*>(halo + pix * C3_CIN + q * 8) = v;
+    *reinterpret_cast<uint4*>(halo + pix * C3_CIN + c3_chunk(pix, q) * 8) = v;
   }
   __syncthreads();
   f32x4 acc[4][2];
@@ -163,7 +169,8 @@ __global__ void __launch_bounds__(128 * NT) k_conv3x3_c32(const hv_gemm_desc d, 
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
       for (int pt = 0; pt < 4; ++pt) {
-        const uint4 bfr = *reinterpret_cast<const uint4*>(halo + ((w + ky) * C3_HW + pt * 16 + fr + kx) * C3_CIN + g * 8);
+        const int pix = (w + ky) * C3_HW + pt * 16 + fr + kx;
+        const uint4 bfr = *reinterpret_cast<const uint4*>(halo + pix * C3_CIN + c3_chunk(pix, g) * 8);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc[pt][nt] = mfma_bf16(wf[ky * 3 + kx][nt], bfr, acc[pt][nt]);
       }
