@@ -32,3 +32,11 @@ for _ in range(50):
     ts.append(a.elapsed_time(b))
 ts.sort()
 print(f"NmsPlan.run: median {ts[len(ts) // 2] * 1e3:.1f} us, min {ts[0] * 1e3:.1f} us; kept {plan.count.tolist()}")
+# the same call against the oracle (CPU restatement of post_process with std::sort's tie order)
+from oracle import hv_oracle as O  # noqa: E402
+ref = O.post_process({k: {n: v[n][:1].cpu() for n in ("boxes", "class_scores", "class_indices")}
+                      for k, v in dec.items()}, 0.25, 0.45, 100)[0]
+k0 = int(plan.count[0])
+same = (k0 == ref["scores"].numel() and torch.equal(plan.scores[0, :k0].cpu(), ref["scores"])
+        and torch.equal(plan.boxes[0, :k0].cpu(), ref["boxes"]) and torch.equal(plan.labels[0, :k0].cpu(), ref["labels"]))
+print(f"image 0 equals the oracle: {same}")
