@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--no-pmc", dest="pmc", action="store_false",
                     help="skip the live rocprofv3 PMC passes (roofline traffic + mfma_busy) at N=1")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--single-stream", action="store_true",
+                    help="side-stream branches and prep overlap off for the whole run (a kernel trace of it then "
+                         "times every launch alone, as the roofline pass does)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercise the launcher, rendezvous and the one-line report (CPU tests)")
     return ap.parse_args()
@@ -353,6 +356,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu_sd = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).eval()
+    if a.single_stream:
+        model.set_options(branch_min_batch=1 << 30, prep_overlap_min_batch=1 << 30)
     x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=None)
 
     with torch.no_grad():

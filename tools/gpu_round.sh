@@ -22,6 +22,7 @@ for step in "$@"; do
     bench) timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
     benchq) timeout -k 10 300 python -u bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; } ; cat $OUT/bench.json ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-stream --no-large --steps 20 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; } ; f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/prof_summary.txt; head -25 $OUT/prof_summary.txt ;;
+    profss) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profss -o run --output-format csv -- python bench.py --single-stream --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 20 > $OUT/profss.log 2>&1 || { tail -30 $OUT/profss.log; exit 1; } ; f=$(find $OUT/profss -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 24 40 > $OUT/profss_summary.txt; python tools/gemm_family_avg.py $f >> $OUT/profss_summary.txt; grep -h '"avg_launch_ms"' $OUT/profss.log | head -1; tail -2 $OUT/profss_summary.txt ;;
     profinf) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/profinf -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 20 > $OUT/profinf.log 2>&1 || { tail -30 $OUT/profinf.log; exit 1; } ; f=$(find $OUT/profinf -name 'run_kernel_stats.csv' | head -1); d=$(dirname $f); python tools/prof_summary.py $d 29 40 > $OUT/profinf_summary.txt; head -25 $OUT/profinf_summary.txt ;;
     breakdown) timeout -k 10 300 python -u tools/gemm_breakdown.py > $OUT/gemm_breakdown.txt 2>&1 || { tail -30 $OUT/gemm_breakdown.txt; exit 1; } ; head -50 $OUT/gemm_breakdown.txt ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE; do timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python bench.py --no-pmc --no-cpu-baseline --no-latency --no-train --no-stream --no-large --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { tail -30 $OUT/pmc_$c.log; exit 1; } ; done ; python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_traffic.json ;;
