@@ -267,8 +267,8 @@ typedef struct hv_mhc_fused_args {
 #define HV_MV_TOK16       0x800  /* with HV_MV_TOK: 16-token tiles (Hd = 1024 always uses 16) */
 #define HV_MV_TOKSPLIT2   0x1000 /* with HV_MV_TOK, D = 256, Hd 512 / 1024: 16-token tiles shared by 2 / 4 workgroups, each */
 #define HV_MV_TOKSPLIT4   0x2000 /* owning Hd / NSPL of the h2 units; the last to finish reduces (split_work) */
-#define HV_MV_TOKSPLIT_SC1 0x4000 /* split hand-off by write-through (sc1) partial stores and sc1 loads
-                                     instead of agent release / acquire fences (opt-in; measured equal) */
+#define HV_MV_TOKSPLIT_SC1 0x4000 /* ignored since ABI 4 (round 6): the write-through hand-off was
+                                     removed; the fenced release / acquire hand-off is the only one */
 #define HV_MV_ABLATE_SHIFT 16    /* diagnostics (tools/mhc_ablate*.py; outputs garbage) */
 /* 1 when (D, Hd, dtype) has a fused kernel under `variant` */
 int hv_mhc_fused_supported(int D, int Hd, int dtype, int variant);
