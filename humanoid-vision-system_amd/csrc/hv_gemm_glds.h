@@ -683,6 +683,7 @@ int launch_infer(const hv_gemm_desc& d, hipStream_t s) {
 
 // per-TU launchers (hv_gemm_glds_*.hip)
 int hv_glds_infer_64x64(const hv_gemm_desc& d, hipStream_t s);
+int hv_glds_infer_32x64(const hv_gemm_desc& d, hipStream_t s);
 int hv_glds_infer_64x128(const hv_gemm_desc& d, hipStream_t s);
 int hv_glds_infer_128x64(const hv_gemm_desc& d, hipStream_t s);
 int hv_glds_infer_128x128(const hv_gemm_desc& d, hipStream_t s);

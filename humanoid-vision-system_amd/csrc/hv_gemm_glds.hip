@@ -73,7 +73,18 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
   if (d.N <= 64) return launch<128, 64>(d, s);
   // small grids (the ViT / head mHC GEMMs: M = 16 x 401 tokens): 64x64 tiles fill the 256 CUs
   const long t64x128 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 128);
-  if (!(d.variant & HV_GV_NO_SMALL) && t64x128 < 320) return launch<64, 64>(d, s);
+  if (!(d.variant & HV_GV_NO_SMALL) && t64x128 < 320) {
+    // long K on a grid of < 256 64x64 tiles (B=1: M ~ 400): 32-row tiles give each CU two or
+    // more workgroups whose barrier / LDS-read / MFMA chains overlap (a lone workgroup's chain
+    // sets the per-K-tile time, profiles/r04/deep8_rejected.txt).  HV_GLDS32=0 turns it off.
+    static const bool t32 = [] {
+      const char* e = getenv("HV_GLDS32");
+      return !(e && e[0] == '0');
+    }();
+    const long t64 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64);
+    if (t32 && !d.epi_mode && d.K >= 1024 && t64 < 256) return hv_glds_infer_32x64(d, s);
+    return launch<64, 64>(d, s);
+  }
   if (d.M <= 64 || t128 < 256 || (d.epi_mode && !(d.variant & HV_GV_TRAIN128))) return launch<64, 128>(d, s);
   return launch<128, 128>(d, s);
 }

@@ -251,6 +251,43 @@ def test_gemm_lds_dma_path_equals_register_path(gpu_device, M, N, K, conv):
     assert rel_err(fast, ref) < 1e-4
 
 
+@pytest.mark.parametrize("kind,M,N,K", [("plain", 401, 512, 2048), ("plain", 333, 96, 1024), ("ln", 400, 2048, 1024),
+                                         ("cat", 400, 512, 2560), ("conv", 400, 1024, 9 * 512), ("conv", 400, 200, 9 * 256)])
+def test_gemm_small_m_long_k_tile_vs_register_path(gpu_device, kind, M, N, K):
+    """The 32x64 LDS-DMA tile the automatic policy takes for small-M, long-K inference GEMMs (a
+    grid of < 256 64x64 tiles with K >= 1,024: the B=1 frame's 20x20 convs and D = 512 / 1024 mHC
+    chains) against the register-staged kernel: plain / LN-after-product / concat-K / implicit
+    3x3 conv, ragged M and N."""
+    ops = _ops()
+    from hv_amd import _lib
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    dev = gpu_device
+    if kind == "conv":
+        c = K // 9
+        x = torch.randn(1, 20, 20, c, generator=g).to(dt).to(dev)
+        w = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt).to(dev)
+        kw = dict(scale=(torch.rand(N, generator=g) + 0.5).to(dev), bias=torch.randn(N, generator=g).to(dev), act="silu")
+        run = lambda: ops.conv2d(x, w, 3, 1, 1, **kw)                          # noqa: E731
+    else:
+        a = (torch.randn(M, K if kind != "cat" else 512, generator=g) * (3 if kind == "ln" else 1) + 1).to(dt).to(dev)
+        b = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt).to(dev)
+        kw = dict(bias=torch.randn(N, generator=g).to(dev), act="gelu")
+        if kind == "ln":
+            mean, rstd = ops.row_stats(a, 1e-5)
+            kw.update(a_mean=mean, a_rstd=rstd, b_colsum=b.float().sum(1).contiguous())
+        if kind == "cat":
+            kw["a2"] = torch.randn(M, K - 512, generator=g).to(dt).to(dev)
+        run = lambda: ops.gemm(a, b, **kw)                                       # noqa: E731
+    fast = run()
+    with gemm_variant(_lib.GV_REGSTAGE):
+        slow = run()
+    d = (fast.float() - slow.float()).abs()
+    assert d.max().item() <= 2 ** -6 * max(1.0, slow.float().abs().max().item()), d.max().item()
+    assert rel_err(fast.float(), slow.float()) < 4e-3
+    assert torch.equal(run(), fast)                                              # deterministic
+
+
 SMALLK_CASES = [  # (kind, M, N, K): 1-8 k-tiles, ragged M / N (scalar store tail), every epilogue form
     ("plain", 4096, 512, 64), ("plain", 1000, 777, 128), ("ln_gelu", 1500, 1024, 256), ("gelu_res", 2048, 768, 512),
     ("res32_mod", 1200, 640, 256), ("scale_f32", 700, 384, 192), ("conv1x1", 2 * 40 * 40, 256, 128),
