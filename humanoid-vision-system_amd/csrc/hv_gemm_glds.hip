@@ -87,9 +87,13 @@ int hv_gemm_glds(const hv_gemm_desc& d, hipStream_t s) {
       const char* e = getenv("HV_GLDS32_K");
       return e ? atoi(e) : 0;
     }();
+    static const int t32t = [] {
+      const char* e = getenv("HV_GLDS32_TILES");
+      return e ? atoi(e) : 256;
+    }();
     const int kmin = t32k > 0 ? t32k : (d.M > 64 ? 256 : 1024);
     const long t64 = (long)hv_cdiv(d.M, 64) * hv_cdiv(d.N, 64);
-    if (t32 && !d.epi_mode && d.K >= kmin && t64 < 256) return hv_glds_infer_32x64(d, s);
+    if (t32 && !d.epi_mode && d.K >= kmin && t64 < t32t) return hv_glds_infer_32x64(d, s);
     return launch<64, 64>(d, s);
   }
   if (d.M <= 64 || t128 < 256 || (d.epi_mode && !(d.variant & HV_GV_TRAIN128))) return launch<64, 128>(d, s);
