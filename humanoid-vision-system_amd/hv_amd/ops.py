@@ -313,6 +313,7 @@ def _mhc_variant(D: int, T: Optional[int], variant: Optional[int], Hd: Optional[
 # the grid fits the 256 CUs in one round, 32-token tiles (half the weight traffic per token) after.
 TOK_MAX_T = {(128, 512): 12800, (256, 512): 51200, (256, 1024): 2048}   # (256, 1024): hidden split only
 TOK_CUS = 256
+TOK_SPLIT4_CUS = 256      # (256, 1024): the 4-way split while 4 x tiles <= this (else 2-way)
 
 
 def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
@@ -334,7 +335,7 @@ def _tok_variant(D: int, Hd: Optional[int], T: int, nsites: int = 1) -> int:
         # 32.6 (4-way) vs 57.7 us chain, T = 1,600 48.7 (2-way) vs 62.6 us
         if not (options().mhc_tok_split and v & L.MV_TOK16 and 2 * tiles16 <= TOK_CUS):
             return 0
-        v |= L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_CUS else L.MV_TOKSPLIT2
+        v |= L.MV_TOKSPLIT4 if 4 * tiles16 <= TOK_SPLIT4_CUS else L.MV_TOKSPLIT2
     return v
 
 
