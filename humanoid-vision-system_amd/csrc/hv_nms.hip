@@ -393,12 +393,18 @@ __device__ __forceinline__ bool x_active(int l, int h, int limit, I d) {
   return h - l > 16 && l < limit && d != x_done<I>();
 }
 
+constexpr int XHEAP_MAX = 8;
+struct XHeap {                           // segments whose depth budget is spent, this level
+  int n, l[XHEAP_MAX], h[XHEAP_MAX];
+};
+
 // one recursion level: every active segment of A[0, E) partitioned at once (see above); a segment
 // whose budget is spent is heap-sorted instead (std::__partial_sort).  The split leaves s_any =
 // "an active segment of more than NMS_WAVE remains" and s_end = the last active one's end (the
 // caller alternates two pairs of them between levels, so the level never waits for their readers).
 template <typename I>
-__device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, int& s_any, int& s_end, int& ph) {
+__device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, int& s_any, int& s_end, int& ph,
+                        XHeap& hp) {
   const int T = blockDim.x, t = threadIdx.x;
   // distinct arrays: lets the compiler batch the loads of consecutive elements
   I* __restrict__ lo = w.lo; I* __restrict__ hi = w.hi; I* __restrict__ PL = w.PL; I* __restrict__ SR = w.SR;
@@ -409,12 +415,43 @@ __device__ void x_level(Cand* __restrict__ A, const XW<I> w, int E, int limit, i
     const I d = Lp[l];
     if (!x_active(l, h, limit, d)) continue;
     if (d == 0) {
-      heap_sort(A + l, h - l);
-      Lp[l] = x_done<I>();
+      const int slot = h - l <= (int)blockDim.x ? atomicAdd(&hp.n, 1) : XHEAP_MAX;
+      if (slot < XHEAP_MAX) {
+        hp.l[slot] = l;                  // the whole workgroup takes it below
+        hp.h[slot] = h;
+      } else {
+        heap_sort(A + l, h - l);
+        Lp[l] = x_done<I>();
+      }
     } else {
       median_to_first(A, l, l + 1, l + (h - l) / 2, h - 1);
     }
   }
+  __syncthreads();
+  // spent budgets of up to blockDim.x positions: with no two scores equal the heap sort's result
+  // is THE sorted order, so a parallel rank sort gives it exactly; any tie -> the serial heap sort
+  // (its tie order is what std::sort leaves)
+  for (int q = 0, nq = min(hp.n, XHEAP_MAX); q < nq; ++q) {
+    const int l = hp.l[q], m = hp.h[q] - l;
+    Cand e{0.f, 0};
+    int rank = 0, tie = 0;
+    if (t < m) {
+      e = A[l + t];
+      for (int j = 0; j < m; ++j) {
+        const float v = A[l + j].score;
+        rank += v > e.score;
+        tie |= v == e.score && j != t;
+      }
+    }
+    if (!__syncthreads_or(tie)) {        // (also: every read of the segment is done)
+      if (t < m) A[l + rank] = e;
+    } else if (t == 0) {
+      heap_sort(A + l, m);
+    }
+    if (t == 0) Lp[l] = x_done<I>();
+    __syncthreads();
+  }
+  if (t == 0) hp.n = 0;                  // next read after this level's barriers
   if (t == 0) SR[E] = 0;
   __syncthreads();
   const int C = (E + T - 1) / T;
@@ -599,6 +636,7 @@ __device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16
                            int& ph) {
   constexpr int XSEG_MAX = 64;           // > 2 log2(2^30): one piece per straddler level
   __shared__ int s_any[2], s_end[2], s_win[2];
+  __shared__ XHeap s_heap;
   __shared__ int s_seg[XSEG_MAX][3];     // (l, h, depth) of the waiting pieces
   const int T = blockDim.x, t = threadIdx.x;
   const int P = min(n, limit);
@@ -640,7 +678,7 @@ __device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16
     }
     any |= h - l > NMS_WAVE && l < limit;
   }
-  if (t == 0) { s_any[0] = any; s_end[0] = W0; }
+  if (t == 0) { s_any[0] = any; s_end[0] = W0; s_heap.n = 0; }
   __syncthreads();
   int Ew = W0;                            // the active segments' extent for the wave phase
   for (int lv = 0;; ++lv) {
@@ -651,10 +689,10 @@ __device__ bool exact_sort(Cand* A, int n, const XWork wg, Cand* c, const XW<u16
     }
     const int E = s_end[q];              // positions past E belong to no active segment
     if (inl) {
-      x_level(c, wl, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph);
+      x_level(c, wl, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph, s_heap);
       continue;
     }
-    x_level(A, wg, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph);
+    x_level(A, wg, E, limit, s_any[q ^ 1], s_end[q ^ 1], ph, s_heap);
     // the window: every segment meeting [0, P) ends by the active ones' end or P-1's segment's
     if (t == 0) s_win[q] = max(s_end[q ^ 1], P > 0 ? wg.hi[P - 1] : 0);   // s_end = 0: none active
     __syncthreads();
