@@ -697,15 +697,21 @@ def test_gpu_post_process_large_matches_reference_fixture(gpu_device, case):
         assert not scores[b, n:].any() and not boxes[b, n:].any()
 
 
-@pytest.mark.parametrize("n,levels", [(1, 1), (16, 3), (17, 2), (300, 7), (5000, 40), (70000, 300)])
+@pytest.mark.parametrize("n,levels", [(1, 1), (16, 3), (17, 2), (300, 7), (5000, 40), (70000, 300),
+                                      (3000, 0), (900, 0)])
 def test_gpu_sort_desc_exact_matches_std_sort(gpu_device, n, levels):
     """hv_sort_desc_exact == the reference's CPU torch.sort(descending=True).indices (libstdc++
-    introsort: tie order included) on heavily tied values; with the depth limit forced to 0 / 1 /
-    3 it matches oracle/std_sort.py's restatement through the heap-sort fallback too."""
+    introsort: tie order included) on heavily tied values (levels > 0) and on distinct values
+    (levels = 0: the spent-budget segments take the parallel rank sort); with the depth limit
+    forced to 0 / 1 / 3 it matches oracle/std_sort.py's restatement through the heap-sort fallback
+    too."""
     from hv_amd import ops
     from oracle.std_sort import std_sort_desc
     g = torch.Generator().manual_seed(n)
-    v = (torch.randint(0, levels, (n,), generator=g).float() / levels) * torch.rand(1, generator=g)
+    if levels == 0:
+        v = torch.randperm(n, generator=g).float() / n + 0.5
+    else:
+        v = (torch.randint(0, levels, (n,), generator=g).float() / levels) * torch.rand(1, generator=g)
     got = ops.sort_desc_exact(v.to(gpu_device)).cpu()
     assert torch.equal(got, torch.sort(v, descending=True).indices)
     if n <= 5000:
