@@ -35,7 +35,8 @@ class HVOptions:
     group_qkv: bool = True            # q / k / v GEMM1 as one N = 3*2Hd GEMM (exact)
     parallel_qkv: bool = False        # q / k / v on three streams: measured slower (tools/ab_vit.py)
     prep_overlap: bool = False        # Sinkhorn + mHC prep on a side stream at every batch
-    prep_overlap_min_batch: int = 8   # ... and from this batch on (B=16: -0.9..-1.8 %; B=1 recompute: +0.7 %)
+    prep_overlap_min_batch: int = 1   # ... and from this batch on (B=16: -0.9..-1.8 %; B=1 recompute: -3 % on
+                                      # the closing build, +0.7 % before the 32x64 tile; profiles/r06/prep_overlap_b1_recompute_ab.txt)
     direct_stem: bool = True          # MFMA stem conv straight from the NCHW image (hv_conv_stem)
     splitk: bool = False              # split-K for small output grids: measured no gain
     splitk_small_m: int = 0           # ... but for GEMMs of at most this many rows (the 16-row final fusion)
