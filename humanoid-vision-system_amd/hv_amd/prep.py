@@ -129,7 +129,7 @@ class PrepProgram:
         self.linears: Dict[int, Tuple] = {}
         self.wtable = None
         self._wdirty = True
-        self._side = None                  # side stream of run(overlap=True)
+        self._sides: Dict[int, torch.cuda.Stream] = {}   # run(overlap=True): per forward stream
         self.param_ptrs = self._ptr_key()
 
     # ------------------------------------------------------------------ registration
@@ -230,13 +230,16 @@ class PrepProgram:
         lib = L.lib()
         if overlap:
             main = torch.cuda.current_stream()
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self.device)
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
+            # one side stream per forward stream (as runtime.Branches): a forward on another
+            # stream -- another thread's eager forward beside a graph capture -- never shares it
+            side = self._sides.get(main.cuda_stream)
+            if side is None:
+                side = self._sides.setdefault(main.cuda_stream, torch.cuda.Stream(device=self.device))
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
                 self._run_mhc(lib)
                 ev = torch.cuda.Event()
-                ev.record(self._side)
+                ev.record(side)
             ctx.prep_event = ev
         else:
             self._run_mhc(lib)
